@@ -1,0 +1,9 @@
+"""tensorflow_train_distributed_amd — an MI355X-native distributed training framework.
+
+Capabilities of boyuanf/tensorflow_train_distributed (a TF1 parameter-server trainer,
+/root/reference/distribute_training.py) re-designed for AMD Instinct MI355X (gfx950):
+PyTorch-ROCm tensors, hand-written CDNA4 HIP kernels, RCCL collectives over xGMI, a native
+C++ runtime (parameter server, checkpoint/event IO, data prefetch) and a
+tf.distribute/tf.train-shaped public API.
+"""
+__version__ = "0.1.0"

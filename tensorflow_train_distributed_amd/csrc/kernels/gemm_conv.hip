@@ -1,0 +1,771 @@
+// MFMA (bf16, gfx950) GEMM engine + implicit-GEMM convolution (fwd / dgrad / wgrad).
+//
+// This is the MatMul/Conv2D hot path of the framework: the dense layers of the reference's
+// MLP (tf.layers.dense, /root/reference/distribute_training.py:54,61 — fwd MatMul F1/F5 and
+// the backward MatMuls G3/G4 of SURVEY.md §2.6) and every conv / FC / projection of the
+// BASELINE.json north-star models (ResNet-50, BERT-Large).
+//
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §3, §5):
+//  * One templated kernel: BMxBN output tile (64/128 each), BK = 64, 256 threads = 4 waves in
+//    a 2x2 arrangement, each wave owning (BM/2)x(BN/2) as 16x16 tiles of
+//    v_mfma_f32_16x16x32_bf16 (fp32 accumulate).
+//  * Operands are staged global -> registers -> LDS (double buffered, one barrier per K-step,
+//    loads for step k+1 issued before the MFMAs of step k, LDS write after them: T14).
+//    Register staging lets the A loader be an implicit-GEMM *gather* with zero padding.
+//  * Each operand is either K-major (reduction dim contiguous: 16-B ds_read_b128 fragments,
+//    XOR-swizzled rows) or MN-major (rows contiguous: stored [k][rows] and read with the
+//    gfx950 transposing ds_read_b64_tr_b16, 32-B-slot XOR swizzle), so NN/NT/TN/TT GEMMs and
+//    the conv weight-gradient (both operands pixel-strided) share one engine, conflict-free.
+//  * The MFMA is issued with operands swapped (D = B·Aᵀ) so each lane ends up holding 4
+//    consecutive output columns of one row: 8-/16-byte vector stores in the epilogue.
+//  * XCD-aware bijective block remap (T1) so blocks sharing an A panel share an L2.
+//  * Split-K (grid.y) writes fp32 slabs that a reduce kernel sums (no float atomics).
+//  * Optional fused epilogue: bias, ReLU/GELU, residual add, accumulate-into-output,
+//    strided output-row remap (stride-2 1x1 dgrad), per-tile BatchNorm partial sums.
+#include "common.h"
+
+namespace ttdk {
+namespace {
+
+constexpr int BK = 64;
+constexpr int NTHR = 256;
+
+// ------------------------------------------------------------------ LDS layouts
+// K-major tile: ROWS x 64 bf16 (128 B per row, 8 chunks of 16 B), chunk ^= (row>>1)&7.
+__device__ __forceinline__ int kmaj_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// MN-major tile: 64 k-rows x ROWS bf16; 32-B slots XOR-swizzled so that the 8 k-rows a
+// half-wave touches in one ds_read_b64_tr_b16 land on distinct banks.
+template <int ROWS>
+__device__ __forceinline__ int mn_swz(int k) {
+  if constexpr (ROWS == 128)
+    return (k & 3) | ((k >> 1) & 4);
+  else
+    return ((k >> 1) & 1) | ((k >> 2) & 2);
+}
+template <int ROWS>
+__device__ __forceinline__ int mnmaj_off(int k, int col) {
+  return k * (ROWS * 2) + (((col >> 4) ^ mn_swz<ROWS>(k)) << 5) + ((col & 15) << 1);
+}
+
+__device__ __forceinline__ bf16x8_t lds_read_b128(const char* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+__device__ __forceinline__ s16x4_t lds_read_tr(const char* p) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p));
+}
+
+__device__ __forceinline__ uint4 ldg16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// ------------------------------------------------------------------ operand loaders
+// Every loader: Params; init(params, row0, tid); load(k0) -> regs; store(lds); frag(...).
+
+struct DenseParams {  // K-major: element (row, k) at p[row*ld + k]; MN-major: (k, row) at p[k*ld + row]
+  const bf16_t* p;
+  long long ld;
+  int rows;
+  int K;
+};
+
+struct GatherParams {  // conv operand geometry (see KConvGather / MNConvGather)
+  const bf16_t* x;
+  int Hs, Ws, Cs;
+  int P, Q;
+  int R, S;
+  int sh, sw, ph, pw, dh, dw;
+  int rows;
+  int K;
+};
+
+template <int ROWS>
+struct KDense {  // element (row, k) at p[row * ld + k]
+  using Params = DenseParams;
+  static constexpr int N = ROWS / 32;
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* ptr[N];
+  bool ok[N];
+  int c, K;
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    c = tid & 7;
+    K = P.K;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int row = row0 + (tid >> 3) + 32 * i;
+      ok[i] = row < P.rows;
+      ptr[i] = P.p + static_cast<long long>(ok[i] ? row : 0) * P.ld + c * 8;
+    }
+  }
+  __device__ __forceinline__ void load(int k0) {
+    const bool kin = k0 + c * 8 < K;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i] = (ok[i] && kin) ? ldg16(ptr[i] + k0) : make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + kmaj_off((tid >> 3) + 32 * i, c)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int rowbase, int ks, int lane) {
+    return lds_read_b128(lds + kmaj_off(rowbase + (lane & 15), ks * 4 + (lane >> 4)));
+  }
+};
+
+// Implicit-GEMM gather of a conv input patch, K-major: row = output pixel (n, p, q),
+// k = (r, s, c). DGRAD=false: forward conv, source pixel = p*stride - pad + r*dil.
+// DGRAD=true: data gradient, source pixel of dY = (p + pad - r*dil) / stride when divisible.
+template <int ROWS, bool DGRAD>
+struct KConvGather {
+  // x: source activations NHWC [Nimg, Hs, Ws, Cs]; (P, Q): pixel grid of the GEMM rows;
+  // rows = Nimg*P*Q; K = R*S*Cs.
+  using Params = GatherParams;
+  static constexpr int N = ROWS / 32;
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* x;
+  int Hs, Ws, Cs, cch, S, sh, sw, dh, dw, K, c;
+  int img[N], hb[N], wb[N];
+  bool ok[N];
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    x = P.x;
+    Hs = P.Hs;
+    Ws = P.Ws;
+    Cs = P.Cs;
+    cch = P.Cs >> 3;
+    S = P.S;
+    sh = P.sh;
+    sw = P.sw;
+    dh = P.dh;
+    dw = P.dw;
+    K = P.K;
+    c = tid & 7;
+    const int pq = P.P * P.Q;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int m = row0 + (tid >> 3) + 32 * i;
+      ok[i] = m < P.rows;
+      const int mm = ok[i] ? m : 0;
+      const int n = mm / pq, rem = mm - n * pq;
+      const int p = rem / P.Q, q = rem - p * P.Q;
+      img[i] = n * P.Hs;
+      if (DGRAD) {
+        hb[i] = p + P.ph;
+        wb[i] = q + P.pw;
+      } else {
+        hb[i] = p * P.sh - P.ph;
+        wb[i] = q * P.sw - P.pw;
+      }
+    }
+  }
+  __device__ __forceinline__ void load(int k0) {
+    const int kc = (k0 >> 3) + c;
+    const bool kin = kc * 8 < K;
+    const int tap = kc / cch, c8 = kc - tap * cch;
+    const int rr = tap / S, ss = tap - rr * S;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      int h, w;
+      bool v = ok[i] && kin;
+      if (DGRAD) {
+        const int hn = hb[i] - rr * dh, wn = wb[i] - ss * dw;
+        h = hn / sh;
+        w = wn / sw;
+        v = v && hn >= 0 && wn >= 0 && h * sh == hn && w * sw == wn;
+      } else {
+        h = hb[i] + rr * dh;
+        w = wb[i] + ss * dw;
+        v = v && h >= 0 && w >= 0;
+      }
+      v = v && h < Hs && w < Ws;
+      r[i] = v ? ldg16(x + ((static_cast<long long>(img[i] + h) * Ws + w) * Cs + c8 * 8)) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + kmaj_off((tid >> 3) + 32 * i, c)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int rowbase, int ks, int lane) {
+    return KDense<ROWS>::frag(lds, rowbase, ks, lane);
+  }
+};
+
+template <int ROWS>
+__device__ __forceinline__ bf16x8_t mn_frag(const char* lds, int colbase, int ks, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int ka = ks * 32 + 8 * g + q;
+  const int col = colbase + 4 * p;
+  const s16x4_t lo = lds_read_tr(lds + mnmaj_off<ROWS>(ka, col));
+  const s16x4_t hi = lds_read_tr(lds + mnmaj_off<ROWS>(ka + 4, col));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int ROWS>
+struct MNDense {  // element (k, row) at p[k * ld + row]
+  using Params = DenseParams;
+  static constexpr int CPR = ROWS / 8;           // 16-B chunks per k-row
+  static constexpr int KPP = NTHR / CPR;         // k-rows per pass
+  static constexpr int N = BK / KPP;             // passes
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* p;
+  long long ld;
+  int K, cc, kr;
+  bool cok;
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    cc = tid % CPR;
+    kr = tid / CPR;
+    ld = P.ld;
+    K = P.K;
+    cok = row0 + cc * 8 < P.rows;
+    p = P.p + row0 + cc * 8;
+  }
+  __device__ __forceinline__ void load(int k0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int k = k0 + kr + KPP * i;
+      r[i] = (cok && k < K) ? ldg16(p + static_cast<long long>(k) * ld) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + mnmaj_off<ROWS>(kr + KPP * i, cc * 8)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int colbase, int ks, int lane) {
+    return mn_frag<ROWS>(lds, colbase, ks, lane);
+  }
+};
+
+// Weight-gradient im2col operand, MN-major: k = output pixel (n, p, q), column = (r, s, c),
+// element = x[n, p*sh - ph + r*dh, q*sw - pw + s*dw, c].
+template <int ROWS>
+struct MNConvGather {
+  // x: conv input [Nimg, Hs, Ws, Cs]; (P, Q): output grid; rows = R*S*Cs; K = Nimg*P*Q.
+  using Params = GatherParams;
+  static constexpr int CPR = ROWS / 8;
+  static constexpr int KPP = NTHR / CPR;
+  static constexpr int N = BK / KPP;
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* x;
+  int H, W, C, P, Q, pq, sh, sw, K, kr, cc, roff, soff;
+  bool cok;
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& Pm, int row0, int tid) {
+    cc = tid % CPR;
+    kr = tid / CPR;
+    x = Pm.x;
+    H = Pm.Hs;
+    W = Pm.Ws;
+    C = Pm.Cs;
+    P = Pm.P;
+    Q = Pm.Q;
+    pq = Pm.P * Pm.Q;
+    sh = Pm.sh;
+    sw = Pm.sw;
+    K = Pm.K;
+    const int col = row0 + cc * 8;
+    cok = col < Pm.rows;
+    const int cl = cok ? col : 0;
+    const int tap = cl / C, c = cl - tap * C;
+    const int rr = tap / Pm.S, ss = tap - rr * Pm.S;
+    roff = rr * Pm.dh - Pm.ph;
+    soff = ss * Pm.dw - Pm.pw;
+    x += c;
+  }
+  __device__ __forceinline__ void load(int k0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int k = k0 + kr + KPP * i;
+      const int n = k / pq, rem = k - n * pq;
+      const int p = rem / Q, q = rem - p * Q;
+      const int h = p * sh + roff, w = q * sw + soff;
+      const bool v = cok && k < K && h >= 0 && w >= 0 && h < H && w < W;
+      r[i] = v ? ldg16(x + (static_cast<long long>(n * H + h) * W + w) * C) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + mnmaj_off<ROWS>(kr + KPP * i, cc * 8)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int colbase, int ks, int lane) {
+    return mn_frag<ROWS>(lds, colbase, ks, lane);
+  }
+};
+
+// ------------------------------------------------------------------ epilogues
+enum Act : int { kActNone = 0, kActRelu = 1, kActGelu = 2 };
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+struct EpiParams {
+  int mode;  // 0 = bf16 store, 1 = fp32 slab store (split-K), 2 = fp32 store
+  void* out;
+  long long ldo;
+  long long slab_stride;  // elements between split-K slabs (mode 1)
+  const float* bias;      // [N] or null
+  const bf16_t* residual; // same layout as out, or null
+  long long ldr;
+  int act;
+  int beta;               // accumulate: out = acc + out
+  // strided output-row remap (dgrad of strided 1x1 convs): row m=(n,p,q) -> (n, p*rs, q*rs) of [OH,OW]
+  int remap;
+  int rP, rQ, rOH, rOW, rs;
+  float* stat;  // BN partial sums: [tiles_m][2][N] (sum, sumsq) or null
+  float alpha;  // scale applied to acc
+};
+
+__device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
+  if (!E.remap) return m;
+  const int pq = E.rP * E.rQ;
+  const int n = m / pq, rem = m - n * pq;
+  const int p = rem / E.rQ, q = rem - p * E.rQ;
+  return (static_cast<long long>(n) * E.rOH + p * E.rs) * E.rOW + q * E.rs;
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM / 32][BN / 32], int n0, int mwave,
+                                         int nwave, int lane, int M, int N, int split, int tile_m, char* smem) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  const int g = lane >> 4, i16 = lane & 15;
+  if (E.mode != 0) {
+    float* out = static_cast<float*>(E.out) + (E.mode == 1 ? split * E.slab_stride : 0);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int m = mwave + tm * 16 + i16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int n = nwave + tn * 16 + 4 * g;
+        f32x4_t v = acc[tm][tn] * E.alpha;
+        float* o = out + static_cast<long long>(m) * E.ldo + n;
+        if (n + 3 < N) {
+          if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
+          *reinterpret_cast<f32x4_t*>(o) = v;
+        } else {
+          #pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (n + j < N) o[j] = v[j] + (E.beta ? o[j] : 0.f);
+        }
+      }
+    }
+    return;
+  }
+  bf16_t* out = static_cast<bf16_t*>(E.out);
+  float csum[TN][4], csq[TN][4];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) csum[tn][j] = csq[tn][j] = 0.f;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int m = mwave + tm * 16 + i16;
+    const bool mok = m < M;
+    const long long orow = mok ? out_row(E, m) : 0;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = nwave + tn * 16 + 4 * g;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[tm][tn][j] * E.alpha;
+      if (!mok) continue;
+      if (E.bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += (n + j < N) ? E.bias[n + j] : 0.f;
+      }
+      const bool full = n + 3 < N;
+      if (E.residual) {
+        const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
+        if (full) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(rp);
+          v[0] += __uint_as_float(rv.x << 16);
+          v[1] += __uint_as_float(rv.x & 0xffff0000u);
+          v[2] += __uint_as_float(rv.y << 16);
+          v[3] += __uint_as_float(rv.y & 0xffff0000u);
+        } else {
+          #pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (n + j < N) v[j] += bf2f(rp[j]);
+        }
+      }
+      bf16_t* op = out + orow * E.ldo + n;
+      if (E.beta) {
+        if (full) {
+          const uint2 ov = *reinterpret_cast<const uint2*>(op);
+          v[0] += __uint_as_float(ov.x << 16);
+          v[1] += __uint_as_float(ov.x & 0xffff0000u);
+          v[2] += __uint_as_float(ov.y << 16);
+          v[3] += __uint_as_float(ov.y & 0xffff0000u);
+        } else {
+          #pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (n + j < N) v[j] += bf2f(op[j]);
+        }
+      }
+      if (E.act == kActRelu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      } else if (E.act == kActGelu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
+      }
+      if (full) {
+        uint2 w;
+        w.x = pack_bf16x2(v[0], v[1]);
+        w.y = pack_bf16x2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(op) = w;
+      } else {
+        #pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (n + j < N) op[j] = f2bf(v[j]);
+      }
+      if (E.stat) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float b = bf2f(f2bf(v[j]));  // stats of the values actually stored
+          csum[tn][j] += b;
+          csq[tn][j] += b * b;
+        }
+      }
+    }
+  }
+  if (E.stat) {
+    // reduce over the 16 rows held by lanes with equal g, then over the two m-waves via LDS.
+    float* red = reinterpret_cast<float*>(smem);  // [2 (wm)][2][BN]
+    const int wm = (threadIdx.x >> 6) >> 1;
+    __syncthreads();
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s = csum[tn][j], q = csq[tn][j];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        if (i16 == 0) {
+          const int col = nwave - n0 + tn * 16 + 4 * g + j;  // column within the block tile
+          red[(wm * 2 + 0) * BN + col] = s;
+          red[(wm * 2 + 1) * BN + col] = q;
+        }
+      }
+    __syncthreads();
+    for (int t = threadIdx.x; t < BN; t += NTHR) {
+      const int n = n0 + t;
+      if (n < N) {
+        E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n] = red[0 * BN + t] + red[2 * BN + t];
+        E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n] = red[1 * BN + t] + red[3 * BN + t];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int xcd = bid & 7, idx = bid >> 3;
+  const int q = nblocks >> 3, r = nblocks & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int BM, int BN, class LA, class LB>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, typename LB::Params pb, EpiParams pe,
+                                                      int M, int N, int K, int tiles_m, int tiles_n, int kt_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (LA::BYTES + LB::BYTES)];
+  const int nblk = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  const int tile_n = t % tiles_n, tile_m = t / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  constexpr int TM = BM / 32, TN = BN / 32;
+
+  char* const sA0 = smem;
+  char* const sB0 = smem + 2 * LA::BYTES;
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ktiles = (K + BK - 1) / BK;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt1 = min(kt0 + kt_per_split, ktiles);
+
+  LA la;
+  LB lb;
+  la.init(pa, m0, tid);
+  lb.init(pb, n0, tid);
+  if (kt0 < kt1) {
+    la.load(kt0 * BK);
+    lb.load(kt0 * BK);
+    la.store(sA0, tid);
+    lb.store(sB0, tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const bool nxt = kt + 1 < kt1;
+    if (nxt) {
+      la.load((kt + 1) * BK);
+      lb.load((kt + 1) * BK);
+    }
+    const char* sa = sA0 + cur * LA::BYTES;
+    const char* sb = sB0 + cur * LB::BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a] = LA::frag(sa, wm * (BM / 2) + a * 16, ks, lane);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bfr[b] = LB::frag(sb, wn * (BN / 2) + b * 16, ks, lane);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+    }
+    if (nxt) {
+      la.store(sA0 + (cur ^ 1) * LA::BYTES, tid);
+      lb.store(sB0 + (cur ^ 1) * LB::BYTES, tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  epilogue<BM, BN>(pe, acc, n0, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane, M, N, blockIdx.y, tile_m, smem);
+}
+
+// Sums split-K fp32 slabs: out[i] = sum_s ws[s*n + i] (+ out[i] if beta), optional bf16 copy.
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long n, float* __restrict__ out,
+                                     int beta) {
+  const long long i4 = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  if (i4 + 3 < n) {
+    f32x4_t s = *reinterpret_cast<const f32x4_t*>(ws + i4);
+    for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4_t*>(ws + k * n + i4);
+    if (beta) s += *reinterpret_cast<const f32x4_t*>(out + i4);
+    *reinterpret_cast<f32x4_t*>(out + i4) = s;
+  } else {
+    for (long long i = i4; i < n; ++i) {
+      float s = 0.f;
+      for (int k = 0; k < splits; ++k) s += ws[k * n + i];
+      out[i] = s + (beta ? out[i] : 0.f);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host-side dispatch
+template <int BM, int BN, class LA, class LB>
+hipError_t launch(const typename LA::Params& pa, const typename LB::Params& pb, const EpiParams& pe, int M, int N,
+                  int K, int splits, hipStream_t st) {
+  const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+  const int ktiles = ceil_div(K, BK);
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  dim3 grid(tm * tn, splits);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB>), grid, dim3(NTHR), 0, st, pa, pb, pe, M, N, K, tm, tn, per);
+  return hipGetLastError();
+}
+
+// Tile choice: prefer 128x128; shrink a dimension when it is small.
+inline void pick_tile(int M, int N, int* bm, int* bn) {
+  *bm = (M <= 64) ? 64 : 128;
+  *bn = (N <= 64) ? 64 : 128;
+}
+
+template <template <int> class LA_T, template <int> class LB_T>
+hipError_t dispatch(const void* pa_raw, const void* pb_raw, const EpiParams& pe, int M, int N, int K, int splits,
+                    int bm, int bn, hipStream_t st) {
+#define TTDK_CASE(BM_, BN_)                                                                                        \
+  if (bm == BM_ && bn == BN_)                                                                                      \
+    return launch<BM_, BN_, LA_T<BM_>, LB_T<BN_>>(*static_cast<const typename LA_T<BM_>::Params*>(pa_raw),         \
+                                                  *static_cast<const typename LB_T<BN_>::Params*>(pb_raw), pe, M, N, \
+                                                  K, splits, st);
+  TTDK_CASE(128, 128)
+  TTDK_CASE(128, 64)
+  TTDK_CASE(64, 128)
+  TTDK_CASE(64, 64)
+#undef TTDK_CASE
+  return hipErrorInvalidValue;
+}
+
+template <int R>
+using KConvFwd = KConvGather<R, false>;
+template <int R>
+using KConvDgrad = KConvGather<R, true>;
+
+}  // namespace
+}  // namespace ttdk
+
+using namespace ttdk;
+
+// Epilogue descriptor passed from Python (ctypes Structure with identical layout).
+struct TtdkEpilogue {
+  int mode;
+  void* out;
+  long long ldo;
+  long long slab_stride;
+  const float* bias;
+  const bf16_t* residual;
+  long long ldr;
+  int act;
+  int beta;
+  int remap;
+  int rP, rQ, rOH, rOW, rs;
+  float* stat;
+  float alpha;
+};
+
+static EpiParams to_epi(const TtdkEpilogue* e) {
+  EpiParams p;
+  p.mode = e->mode;
+  p.out = e->out;
+  p.ldo = e->ldo;
+  p.slab_stride = e->slab_stride;
+  p.bias = e->bias;
+  p.residual = e->residual;
+  p.ldr = e->ldr;
+  p.act = e->act;
+  p.beta = e->beta;
+  p.remap = e->remap;
+  p.rP = e->rP;
+  p.rQ = e->rQ;
+  p.rOH = e->rOH;
+  p.rOW = e->rOW;
+  p.rs = e->rs;
+  p.stat = e->stat;
+  p.alpha = e->alpha == 0.f ? 1.f : e->alpha;
+  return p;
+}
+
+// General GEMM: C[M,N] = alpha * A·B with A either K-major (a_kmajor=1: A[m*lda + k]) or
+// MN-major (A[k*lda + m]); B either K-major (B[n*ldb + k]) or MN-major (B[k*ldb + n]).
+TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, const bf16_t* B, long long ldb,
+                               int b_kmajor, int M, int N, int K, int splits, int bm, int bn,
+                               const TtdkEpilogue* epi, hipStream_t st) {
+  EpiParams pe = to_epi(epi);
+  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
+  if (a_kmajor && b_kmajor) {
+    DenseParams pa{A, lda, M, K};
+    DenseParams pb{B, ldb, N, K};
+    return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  } else if (a_kmajor && !b_kmajor) {
+    DenseParams pa{A, lda, M, K};
+    DenseParams pb{B, ldb, N, K};
+    return dispatch<KDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  } else if (!a_kmajor && b_kmajor) {
+    DenseParams pa{A, lda, M, K};
+    DenseParams pb{B, ldb, N, K};
+    return dispatch<MNDense, KDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  } else {
+    DenseParams pa{A, lda, M, K};
+    DenseParams pb{B, ldb, N, K};
+    return dispatch<MNDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  }
+}
+
+struct TtdkConv {
+  int N, H, W, C;   // input NHWC
+  int K, R, S;      // filters [K][R][S][C]
+  int P, Q;         // output spatial
+  int sh, sw, ph, pw, dh, dw;
+};
+
+static bool is_pointwise(const TtdkConv* g) {
+  return g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0;
+}
+
+// y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]).
+TTDK_EXPORT int ttdk_conv_fwd(const bf16_t* x, const bf16_t* w, const TtdkConv* g, int bm, int bn,
+                              const TtdkEpilogue* epi, hipStream_t st) {
+  if (g->C % 8) return hipErrorInvalidValue;
+  EpiParams pe = to_epi(epi);
+  const int M = g->N * g->P * g->Q, N = g->K, K = g->R * g->S * g->C;
+  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
+  DenseParams pb{w, K, N, K};
+  if (is_pointwise(g)) {
+    DenseParams pa{x, g->C, M, K};
+    return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
+  }
+  GatherParams pa{x, g->H, g->W, g->C, g->P, g->Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};
+  return dispatch<KConvFwd, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
+}
+
+// dx[N,H,W,C] = conv_transpose(dy[N,P,Q,K], w): wt must hold w transposed to [C][R][S][K]
+// (ttdk_conv_weight_transpose). Rows of the GEMM are the pixels of dx.
+// Strided 1x1 (no padding) convs compute only the rows that receive a gradient and use the
+// epilogue's row remap; the caller zero-fills or pre-loads (beta=1) the other pixels.
+TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkConv* g, int bm, int bn,
+                                const TtdkEpilogue* epi, hipStream_t st) {
+  if (g->K % 8) return hipErrorInvalidValue;
+  EpiParams pe = to_epi(epi);
+  const int N = g->C, K = g->R * g->S * g->K;
+  DenseParams pb{wt, K, N, K};
+  if (g->R == 1 && g->S == 1 && g->ph == 0 && g->pw == 0) {
+    const int M = g->N * g->P * g->Q;
+    if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
+    DenseParams pa{dy, g->K, M, K};
+    if (g->sh != 1 || g->sw != 1) {
+      if (g->sh != g->sw) return hipErrorInvalidValue;
+      pe.remap = 1;
+      pe.rP = g->P;
+      pe.rQ = g->Q;
+      pe.rOH = g->H;
+      pe.rOW = g->W;
+      pe.rs = g->sh;
+    }
+    return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
+  }
+  const int M = g->N * g->H * g->W;
+  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
+  GatherParams pa{dy, g->P, g->Q, g->K, g->H, g->W, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};
+  return dispatch<KConvDgrad, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
+}
+
+// dw[K,R,S,C] (fp32) = sum over pixels of dy ⊗ im2col(x). `ws` is a split-K workspace of
+// splits*K*R*S*C floats (may be null when splits == 1, then dw is written directly).
+TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkConv* g, float* dw, float* ws,
+                                int splits, int beta, int bm, int bn, hipStream_t st) {
+  const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
+  if (g->C % 8 || g->K % 8) return hipErrorInvalidValue;
+  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
+  const int ktiles = ceil_div(K, BK);
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  if (splits > 1 && !ws) return hipErrorInvalidValue;
+  EpiParams pe{};
+  pe.alpha = 1.f;
+  pe.ldo = N;
+  if (splits > 1) {
+    pe.mode = 1;
+    pe.out = ws;
+    pe.slab_stride = static_cast<long long>(M) * N;
+  } else {
+    pe.mode = 2;
+    pe.out = dw;
+    pe.beta = beta;
+  }
+  DenseParams pa{dy, g->K, M, K};
+  hipError_t e;
+  if (is_pointwise(g)) {
+    DenseParams pb{x, g->C, N, K};
+    e = dispatch<MNDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  } else {
+    GatherParams pb{x, g->H, g->W, g->C, g->P, g->Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, N, K};
+    e = dispatch<MNDense, MNConvGather>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  }
+  if (e != hipSuccess || splits == 1) return e;
+  const long long n = static_cast<long long>(M) * N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ceil_div((n + 3) / 4, 256)), dim3(256), 0, st, ws, splits, n, dw, beta);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ceil_div((n + 3) / 4, 256)), dim3(256), 0, st, ws, splits, n, out, beta);
+  return hipGetLastError();
+}

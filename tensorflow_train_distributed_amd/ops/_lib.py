@@ -1,0 +1,90 @@
+"""ctypes bindings for ``libttd_hip.so`` (the gfx950 kernel library).
+
+Every kernel launcher has the C signature ``int ttdk_*(..., hipStream_t)``; this module
+declares the argument types once and launches on PyTorch's *current* HIP stream, so the
+kernels compose with torch's stream semantics, ``torch.cuda.graphs`` capture (hipGraph) and
+the collective engine's side streams. A non-zero return (hipError_t) raises immediately.
+
+There is deliberately no fallback here: a GPU op whose kernel library is missing or fails
+to load raises (the CPU path of each op lives in :mod:`.reference`).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_float, c_int, c_longlong, c_uint64, c_void_p
+
+import torch
+
+from .. import _native
+
+P = c_void_p
+I = c_int
+L = c_longlong
+F = c_float
+U64 = c_uint64
+
+
+class Epilogue(ctypes.Structure):
+    """Mirror of ``TtdkEpilogue`` in gemm_conv.hip."""
+
+    _fields_ = [
+        ("mode", c_int), ("out", c_void_p), ("ldo", c_longlong), ("slab_stride", c_longlong),
+        ("bias", c_void_p), ("residual", c_void_p), ("ldr", c_longlong), ("act", c_int),
+        ("beta", c_int), ("remap", c_int), ("rP", c_int), ("rQ", c_int), ("rOH", c_int),
+        ("rOW", c_int), ("rs", c_int), ("stat", c_void_p), ("alpha", c_float),
+    ]
+
+
+class ConvGeom(ctypes.Structure):
+    """Mirror of ``TtdkConv``: input NHWC [N,H,W,C], filter [K,R,S,C], output [N,P,Q,K]."""
+
+    _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "K", "R", "S", "P", "Q", "sh", "sw", "ph", "pw", "dh", "dw")]
+
+
+E = ctypes.POINTER(Epilogue)
+G = ctypes.POINTER(ConvGeom)
+
+# name -> argtypes (restype is always int = hipError_t). Structs are passed by reference.
+_SIGS = {
+    # gemm_conv.hip
+    "ttdk_gemm_bf16": [P, L, I, P, L, I, I, I, I, I, I, I, E, P],
+    "ttdk_conv_fwd": [P, P, G, I, I, E, P],
+    "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
+    "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
+    "ttdk_splitk_reduce": [P, I, L, P, I, P],
+}
+
+_fns = {}
+
+
+def register(sigs: dict):
+    _SIGS.update(sigs)
+
+
+def fn(name):
+    f = _fns.get(name)
+    if f is None:
+        lib = _native.hip()
+        f = getattr(lib, name)
+        f.argtypes = _SIGS[name]
+        f.restype = c_int
+        _fns[name] = f
+    return f
+
+
+class HipKernelError(RuntimeError):
+    pass
+
+
+def call(name, *args):
+    rc = fn(name)(*args)
+    if rc != 0:
+        raise HipKernelError("%s failed with hipError_t %d" % (name, rc))
+
+
+def stream():
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())

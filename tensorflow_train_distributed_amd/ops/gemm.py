@@ -1,0 +1,162 @@
+"""Launch wrappers for the MFMA GEMM / implicit-GEMM convolution kernels (gemm_conv.hip).
+
+Tensors here are CUDA (HIP) tensors in the layouts the kernels expect:
+activations NHWC bf16, conv filters [K, R, S, C] bf16 (TF keeps [R, S, C, K]; the layer
+converts once per step), weight gradients fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+
+
+def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,
+         slab_stride=0):
+    e = _lib.Epilogue()
+    e.mode = mode
+    e.out = out.data_ptr()
+    e.ldo = ldo if ldo is not None else out.shape[-1]
+    e.slab_stride = slab_stride
+    e.bias = bias.data_ptr() if bias is not None else None
+    e.residual = residual.data_ptr() if residual is not None else None
+    e.ldr = residual.shape[-1] if residual is not None else 0
+    e.act = act
+    e.beta = beta
+    e.stat = stat.data_ptr() if stat is not None else None
+    e.alpha = alpha
+    return e
+
+
+def effective_splits(K, splits, bk=64):
+    """Mirror of the kernel launcher's split-K clamping (every split gets >= 1 K-tile)."""
+    kt = -(-K // bk)
+    splits = max(1, min(splits, kt))
+    per = -(-kt // splits)
+    return -(-kt // per)
+
+
+def _check(t, dtype, name):
+    if t.dtype != dtype or not t.is_cuda or not t.is_contiguous():
+        raise ValueError("%s must be a contiguous CUDA %s tensor (got %s %s contig=%s)"
+                         % (name, dtype, t.dtype, t.device, t.is_contiguous()))
+
+
+def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16, bias=None,
+         act=ACT_NONE, residual=None, beta=0, alpha=1.0, splits=1, tile=(0, 0)):
+    """C = alpha * op(a) @ op(b) (+bias) (+residual) (+C if beta) -> act.
+
+    a: [M, K] (or [K, M] with trans_a); b: [K, N] (or [N, K] with trans_b); bf16, contiguous.
+    out_dtype bf16 (fused epilogue) or float32 (plain / split-K store).
+    """
+    _check(a, torch.bfloat16, "a")
+    _check(b, torch.bfloat16, "b")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else a.shape
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else b.shape
+    if K != Kb:
+        raise ValueError("gemm inner dims differ: %d vs %d" % (K, Kb))
+    if K % 8 or (trans_a and M % 8) or (not trans_b and N % 8):
+        raise ValueError("gemm needs the contiguous dims to be multiples of 8")
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    a_kmajor = 0 if trans_a else 1
+    lda = M if trans_a else K
+    b_kmajor = 1 if trans_b else 0
+    ldb = K if trans_b else N
+    if out.dtype == torch.float32:
+        splits = effective_splits(K, splits)
+        if splits > 1:
+            ws = torch.empty((splits, M, N), dtype=torch.float32, device=a.device)
+            e = _epi(ws, mode=1, ldo=N, slab_stride=M * N, alpha=alpha)
+            _lib.call("ttdk_gemm_bf16", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K,
+                      splits, tile[0], tile[1], ctypes.byref(e), _lib.stream())
+            _lib.call("ttdk_splitk_reduce", ws.data_ptr(), splits, M * N, out.data_ptr(), beta, _lib.stream())
+            return out
+        e = _epi(out, mode=2, ldo=N, beta=beta, alpha=alpha)
+    else:
+        e = _epi(out, bias=bias, residual=residual, act=act, beta=beta, alpha=alpha)
+    _lib.call("ttdk_gemm_bf16", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K, 1,
+              tile[0], tile[1], ctypes.byref(e), _lib.stream())
+    return out
+
+
+def conv_geom(x_shape, w_shape, stride, padding, dilation=(1, 1)):
+    N, H, W, C = x_shape
+    K, R, S, Cw = w_shape
+    if C != Cw:
+        raise ValueError("channel mismatch %d vs %d" % (C, Cw))
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    P = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
+    Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+    g = _lib.ConvGeom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw)
+    return g
+
+
+def conv_fwd(x, w, stride=(1, 1), padding=(0, 0), *, out=None, residual=None, act=ACT_NONE,
+             bias=None, stat=None, tile=(0, 0)):
+    """y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]) with optional fused epilogue.
+
+    stat: optional fp32 [ceil(N*P*Q/BM), 2, K] buffer receiving per-tile BN partial sums.
+    """
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.bfloat16, "w")
+    g = conv_geom(x.shape, w.shape, stride, padding)
+    if out is None:
+        out = torch.empty((g.N, g.P, g.Q, g.K), dtype=torch.bfloat16, device=x.device)
+    e = _epi(out, ldo=g.K, bias=bias, residual=residual, act=act, stat=stat)
+    _lib.call("ttdk_conv_fwd", x.data_ptr(), w.data_ptr(), ctypes.byref(g), tile[0], tile[1], ctypes.byref(e),
+              _lib.stream())
+    return out
+
+
+def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
+               tile=(0, 0)):
+    """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
+
+    For strided 1x1 convs only the sampled pixels are written: pass a zero-initialised `out`
+    or beta=1 with `out` already holding another gradient contribution.
+    """
+    _check(dy, torch.bfloat16, "dy")
+    _check(wt, torch.bfloat16, "wt")
+    C, R, S, K = wt.shape
+    g = conv_geom(x_shape, (K, R, S, C), stride, padding)
+    strided_pw = R == 1 and S == 1 and padding == (0, 0) and tuple(stride) != (1, 1)
+    if out is None:
+        alloc = torch.zeros if (strided_pw and not beta) else torch.empty
+        out = alloc(tuple(x_shape), dtype=torch.bfloat16, device=dy.device)
+    e = _epi(out, ldo=C, beta=beta, residual=residual)
+    _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), tile[0], tile[1], ctypes.byref(e),
+              _lib.stream())
+    return out
+
+
+def wgrad_splits(g, bm=128, bn=128, target_blocks=1024):
+    M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
+    tiles = -(-M // bm) * -(-N // bn)
+    ktiles = -(-K // 64)
+    s = max(1, min(ktiles // 4, -(-target_blocks // tiles)))
+    return s
+
+
+def conv_wgrad(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, splits=None,
+               tile=(0, 0)):
+    """dw[K,R,S,C] (fp32) = sum over pixels of dy x im2col(x)."""
+    _check(x, torch.bfloat16, "x")
+    _check(dy, torch.bfloat16, "dy")
+    g = conv_geom(x.shape, w_shape, stride, padding)
+    if out is None:
+        out = torch.empty(tuple(w_shape), dtype=torch.float32, device=x.device)
+    if splits is None:
+        splits = wgrad_splits(g)
+    ws = None
+    if splits > 1:
+        ws = torch.empty((splits,) + tuple(w_shape), dtype=torch.float32, device=x.device)
+    _lib.call("ttdk_conv_wgrad", x.data_ptr(), dy.data_ptr(), ctypes.byref(g), out.data_ptr(),
+              ws.data_ptr() if ws is not None else None, splits, beta, tile[0], tile[1], _lib.stream())
+    return out
