@@ -1,0 +1,328 @@
+// BatchNormalization (training mode, NHWC / channels-last) forward + backward on gfx950.
+//
+// North-star op (BASELINE.json "LayerNorm/BatchNorm"); the reference has BN commented out
+// (/root/reference/distribute_training.py:56) but ResNet-50 needs it in every block.
+//
+// Forward statistics come either from the conv epilogue (per-tile partial sums, see
+// gemm_conv.hip EpiParams::stat) or from ttdk_bn_stats_partial; both produce
+// partial[T][2][C] which ttdk_bn_reduce_partials folds (2-D grid, LDS tree, one float
+// atomic per block and channel) into sums[2][C]. Finalize kernels turn sums into per-channel
+// affine coefficients so the streaming passes are a single FMA per element:
+//   fwd:  out = act(y * scale + shift (+ residual)),  scale = gamma*rstd, shift = beta - mean*scale
+//   bwd:  g = dy * [out > 0];  dz = a*g + b*y + c with
+//         a = gamma*rstd, b = -gamma*rstd^3 * (sum(g*y) - mean*sum(g))/M, c = -a*sum(g)/M - b*mean
+// All streaming passes move 16 B (8 bf16 channels) per lane.
+#include "common.h"
+
+namespace ttdk {
+namespace {
+
+constexpr int kThreads = 256;
+
+// Sums over rows of x[M][C] (and of x^2), 8 channels per thread-column. Writes
+// partial[blockIdx.x][2][C]. Requires C % 8 == 0.
+__global__ __launch_bounds__(kThreads) void stats_partial_kernel(const bf16_t* __restrict__ x, long long M, int C,
+                                                                 float* __restrict__ partial, long long rows_per_block) {
+  __shared__ float red[2][kThreads][8];
+  const int cg = C >> 3;                          // 8-channel groups per row
+  const int cols = min(cg, kThreads);             // thread-columns
+  const int rlanes = kThreads / cols;             // rows processed concurrently
+  const int col = threadIdx.x % cols, rl = threadIdx.x / cols;
+  const long long r0 = blockIdx.x * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  for (int cbase = 0; cbase < cg; cbase += cols) {
+    const int c8 = cbase + col;
+    float s[8] = {0}, q[8] = {0};
+    if (rl < rlanes && c8 < cg) {
+      for (long long r = r0 + rl; r < r1; r += rlanes) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + r * C + c8 * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += f[j];
+          q[j] += f[j] * f[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][threadIdx.x][j] = s[j];
+      red[1][threadIdx.x][j] = q[j];
+    }
+    __syncthreads();
+    if (rl == 0 && c8 < cg) {
+      for (int k = 1; k < rlanes; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += red[0][col + k * cols][j];
+          q[j] += red[1][col + k * cols][j];
+        }
+      float* p = partial + static_cast<long long>(blockIdx.x) * 2 * C + c8 * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        p[j] = s[j];
+        p[C + j] = q[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Backward partial sums: g = dy * [out > 0] (relu) ; sums of g and g*y. Optionally writes g.
+__global__ __launch_bounds__(kThreads) void bwd_partial_kernel(const bf16_t* __restrict__ dy,
+                                                               const bf16_t* __restrict__ out,
+                                                               const bf16_t* __restrict__ y, long long M, int C,
+                                                               float* __restrict__ partial, long long rows_per_block,
+                                                               bf16_t* __restrict__ g_out) {
+  __shared__ float red[2][kThreads][8];
+  const int cg = C >> 3;
+  const int cols = min(cg, kThreads);
+  const int rlanes = kThreads / cols;
+  const int col = threadIdx.x % cols, rl = threadIdx.x / cols;
+  const long long r0 = blockIdx.x * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  for (int cbase = 0; cbase < cg; cbase += cols) {
+    const int c8 = cbase + col;
+    float s[8] = {0}, q[8] = {0};
+    if (rl < rlanes && c8 < cg) {
+      for (long long r = r0 + rl; r < r1; r += rlanes) {
+        const long long off = r * C + c8 * 8;
+        float g[8], yv[8];
+        uint4 graw = *reinterpret_cast<const uint4*>(dy + off);
+        unpack8(graw, g);
+        if (out) {
+          float o[8];
+          unpack8(*reinterpret_cast<const uint4*>(out + off), o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+          if (g_out) *reinterpret_cast<uint4*>(g_out + off) = pack8(g);
+        }
+        unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += g[j];
+          q[j] += g[j] * yv[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][threadIdx.x][j] = s[j];
+      red[1][threadIdx.x][j] = q[j];
+    }
+    __syncthreads();
+    if (rl == 0 && c8 < cg) {
+      for (int k = 1; k < rlanes; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += red[0][col + k * cols][j];
+          q[j] += red[1][col + k * cols][j];
+        }
+      float* p = partial + static_cast<long long>(blockIdx.x) * 2 * C + c8 * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        p[j] = s[j];
+        p[C + j] = q[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// sums[2C] += sum over t of partial[t][2C]. grid = (ceil(2C/64), slices); block = 64 x 4.
+__global__ __launch_bounds__(kThreads) void reduce_partials_kernel(const float* __restrict__ partial, int T, int C2,
+                                                                   float* __restrict__ sums, int t_per_slice) {
+  __shared__ float red[4][64];
+  const int cx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  const int t0 = blockIdx.y * t_per_slice, t1 = min(T, t0 + t_per_slice);
+  float s = 0.f;
+  if (c < C2)
+    for (int t = t0 + ty; t < t1; t += 4) s += partial[static_cast<long long>(t) * C2 + c];
+  red[ty][cx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C2) atomicAdd(&sums[c], red[0][cx] + red[1][cx] + red[2][cx] + red[3][cx]);
+}
+
+__global__ void fwd_finalize_kernel(const float* __restrict__ sums, float count, int C, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, float eps, float momentum, float* running_mean,
+                                    float* running_var, float* __restrict__ save_mean, float* __restrict__ save_rstd,
+                                    float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mean = sums[c] / count;
+  const float var = fmaxf(sums[C + c] / count - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + eps);
+  save_mean[c] = mean;
+  save_rstd[c] = rstd;
+  const float sc = (gamma ? gamma[c] : 1.f) * rstd;
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - mean * sc;
+  if (running_mean) {  // TF/Keras convention: moving = moving * momentum + batch * (1 - momentum)
+    const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
+    running_mean[c] = running_mean[c] * momentum + mean * (1.f - momentum);
+    running_var[c] = running_var[c] * momentum + unbiased * (1.f - momentum);
+  }
+}
+
+__global__ void bwd_finalize_kernel(const float* __restrict__ sums, float count, int C, const float* __restrict__ gamma,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
+                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sg = sums[c], sgy = sums[C + c];
+  const float m = mean[c], r = rstd[c];
+  const float gam = gamma ? gamma[c] : 1.f;
+  const float dgam = r * (sgy - m * sg);  // sum(g * xhat)
+  if (dgamma) dgamma[c] = dgam + (accumulate ? dgamma[c] : 0.f);
+  if (dbeta) dbeta[c] = sg + (accumulate ? dbeta[c] : 0.f);
+  const float a = gam * r;
+  const float b = -gam * r * r * dgam / count;
+  const float cc = -a * sg / count - b * m;
+  coef[c] = a;
+  coef[C + c] = b;
+  coef[2 * C + c] = cc;
+}
+
+// out = act(y*scale[c] + shift[c] (+ residual)); 8 channels per thread.
+__global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift,
+                                                         const bf16_t* __restrict__ residual, bf16_t* __restrict__ out,
+                                                         long long n8, int C, int relu) {
+  const int cg = C >> 3;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n8;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int c0 = static_cast<int>(i % cg) * 8;
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[i], f);
+    const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(scale + c0), s1 = *reinterpret_cast<const f32x4_t*>(scale + c0 + 4);
+    const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(shift + c0), h1 = *reinterpret_cast<const f32x4_t*>(shift + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = f[j] * s0[j] + h0[j];
+      f[4 + j] = f[4 + j] * s1[j] + h1[j];
+    }
+    if (residual) {
+      float r[8];
+      unpack8(reinterpret_cast<const uint4*>(residual)[i], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += r[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(f);
+  }
+}
+
+// dz = a*g + b*y + c, g = dy * [out > 0] if out given.
+__global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ out,
+                                                             const bf16_t* __restrict__ y,
+                                                             const float* __restrict__ coef, bf16_t* __restrict__ dz,
+                                                             long long n8, int C) {
+  const int cg = C >> 3;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n8;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int c0 = static_cast<int>(i % cg) * 8;
+    float g[8], yv[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
+    if (out) {
+      float o[8];
+      unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+    }
+    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      g[j] = coef[c] * g[j] + coef[C + c] * yv[j] + coef[2 * C + c];
+    }
+    reinterpret_cast<uint4*>(dz)[i] = pack8(g);
+  }
+}
+
+inline int grid_for(long long n, int per_block = kThreads, int cap = 8192) {
+  long long g = (n + per_block - 1) / per_block;
+  return static_cast<int>(g < cap ? (g < 1 ? 1 : g) : cap);
+}
+
+}  // namespace
+}  // namespace ttdk
+
+using namespace ttdk;
+
+// Number of partial rows ttdk_bn_stats_partial / ttdk_bn_bwd_partial will write.
+TTDK_EXPORT int ttdk_bn_num_partials(long long M, int C) {
+  const int cg = C >> 3;
+  const int cols = cg < kThreads ? cg : kThreads;
+  const int rlanes = kThreads / cols;
+  long long want = (M + 16LL * rlanes - 1) / (16LL * rlanes);  // >= 16 rows per row-lane
+  if (want > 1024) want = 1024;
+  if (want < 1) want = 1;
+  return static_cast<int>(want);
+}
+
+TTDK_EXPORT int ttdk_bn_stats_partial(const bf16_t* x, long long M, int C, float* partial, int nblocks, hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const long long rpb = (M + nblocks - 1) / nblocks;
+  hipLaunchKernelGGL(stats_partial_kernel, dim3(nblocks), dim3(kThreads), 0, st, x, M, C, partial, rpb);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bn_bwd_partial(const bf16_t* dy, const bf16_t* out, const bf16_t* y, long long M, int C,
+                                    float* partial, int nblocks, bf16_t* g_out, hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const long long rpb = (M + nblocks - 1) / nblocks;
+  hipLaunchKernelGGL(bwd_partial_kernel, dim3(nblocks), dim3(kThreads), 0, st, dy, out, y, M, C, partial, rpb, g_out);
+  return hipGetLastError();
+}
+
+// sums[2C] = sum of partial[T][2C] (sums is zeroed here).
+TTDK_EXPORT int ttdk_bn_reduce_partials(const float* partial, int T, int C, float* sums, hipStream_t st) {
+  const int C2 = 2 * C;
+  hipError_t e = hipMemsetAsync(sums, 0, sizeof(float) * C2, st);
+  if (e != hipSuccess) return e;
+  int slices = (T + 63) / 64;
+  if (slices > 64) slices = 64;
+  const int per = (T + slices - 1) / slices;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((C2 + 63) / 64, slices), dim3(kThreads), 0, st, partial, T, C2, sums,
+                     per);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bn_fwd_finalize(const float* sums, float count, int C, const float* gamma, const float* beta,
+                                     float eps, float momentum, float* running_mean, float* running_var,
+                                     float* save_mean, float* save_rstd, float* scale, float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, sums, count, C, gamma, beta, eps,
+                     momentum, running_mean, running_var, save_mean, save_rstd, scale, shift);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bn_bwd_finalize(const float* sums, float count, int C, const float* gamma, const float* mean,
+                                     const float* rstd, float* dgamma, float* dbeta, float* coef, int accumulate,
+                                     hipStream_t st) {
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, sums, count, C, gamma, mean, rstd,
+                     dgamma, dbeta, coef, accumulate);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* shift, const bf16_t* residual,
+                              bf16_t* out, long long n, int C, int relu, hipStream_t st) {
+  if (C % 8 || n % 8) return hipErrorInvalidValue;
+  const long long n8 = n / 8;
+  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, y, scale, shift, residual, out, n8, C,
+                     relu);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bn_bwd_apply(const bf16_t* dy, const bf16_t* out, const bf16_t* y, const float* coef, bf16_t* dz,
+                                  long long n, int C, hipStream_t st) {
+  if (C % 8 || n % 8) return hipErrorInvalidValue;
+  const long long n8 = n / 8;
+  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, dy, out, y, coef, dz, n8, C);
+  return hipGetLastError();
+}

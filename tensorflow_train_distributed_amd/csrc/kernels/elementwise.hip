@@ -1,0 +1,334 @@
+// Element-wise / layout kernels: dtype casts, channel padding, conv weight layout changes,
+// bias + activation (+ Philox dropout) forward/backward, bias-gradient column sums, add.
+//
+// Reference ops covered: BiasAdd F2 / BiasAddGrad G2, Elu F3 / EluGrad G6,
+// dropout F4 / G5 (tf.layers.dropout(rate=0.01, training=True),
+// /root/reference/distribute_training.py:57-58). Dropout keeps with probability 1-rate and
+// scales by 1/(1-rate); the mask comes from counter-based Philox4x32-10 (seed, offset) so the
+// backward pass regenerates it instead of storing it.
+// All bf16 streams are 16 B per lane (Guideline 13).
+#include "common.h"
+
+namespace ttdk {
+namespace {
+
+inline int grid_for(long long n, int cap = 16384) {
+  long long g = (n + 255) / 256;
+  return static_cast<int>(g < cap ? (g < 1 ? 1 : g) : cap);
+}
+
+#define GRID_STRIDE(i, n)                                                                     \
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < (n); \
+       i += static_cast<long long>(gridDim.x) * blockDim.x)
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
+  GRID_STRIDE(i, (n + 3) / 4) {
+    const long long o = i * 4;
+    if (o + 3 < n) {
+      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(x + o);
+      uint2 p;
+      p.x = pack_bf16x2(v[0], v[1]);
+      p.y = pack_bf16x2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(y + o) = p;
+    } else {
+      for (long long j = o; j < n; ++j) y[j] = f2bf(x[j]);
+    }
+  }
+}
+
+__global__ void bf16_to_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long long n) {
+  GRID_STRIDE(i, n) y[i] = bf2f(x[i]);
+}
+
+// x[rows][C] (any dtype via bf16 input) -> y[rows][Cp] with zero channels C..Cp-1.
+__global__ void pad_channels_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long rows, int C,
+                                    int Cp) {
+  GRID_STRIDE(i, rows * Cp) {
+    const long long r = i / Cp;
+    const int c = static_cast<int>(i - r * Cp);
+    y[i] = c < C ? x[r * C + c] : static_cast<bf16_t>(0);
+  }
+}
+
+__global__ void unpad_channels_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long rows, int Cp,
+                                      int C) {
+  GRID_STRIDE(i, rows * C) {
+    const long long r = i / C;
+    const int c = static_cast<int>(i - r * C);
+    y[i] = x[r * Cp + c];
+  }
+}
+
+// src [A][B][C] -> dst [C][B][A] (bf16), used for conv filters [K][RS][C] -> [C][RS][K].
+__global__ void transpose_aca_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, int A, int B, int C) {
+  __shared__ bf16_t tile[32][33];
+  const int b = blockIdx.z;
+  const int a0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int a = a0 + k, c = c0 + tx;
+    tile[k][tx] = (a < A && c < C) ? src[(static_cast<long long>(a) * B + b) * C + c] : static_cast<bf16_t>(0);
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, a = a0 + tx;
+    if (a < A && c < C) dst[(static_cast<long long>(c) * B + b) * A + a] = tile[tx][k];
+  }
+}
+
+// fp32 [A][B][C] -> fp32 [C][B][A] (checkpoint layout conversions: KRSC <-> RSCK done as 2-D)
+__global__ void transpose2d_f32_kernel(const float* __restrict__ src, float* __restrict__ dst, int R, int C) {
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    tile[k][tx] = (r < R && c < C) ? src[static_cast<long long>(r) * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (r < R && c < C) dst[static_cast<long long>(c) * R + r] = tile[tx][k];
+  }
+}
+
+enum Act : int { kNone = 0, kRelu = 1, kGelu = 2, kElu = 3 };
+
+__device__ __forceinline__ float act_fwd(float x, int act) {
+  switch (act) {
+    case kRelu: return fmaxf(x, 0.f);
+    case kGelu: return 0.5f * x * (1.f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
+    case kElu: return x > 0.f ? x : expm1f(x);
+    default: return x;
+  }
+}
+
+// derivative given pre-activation z (and post-activation a for ELU: d = a + 1 for z <= 0)
+__device__ __forceinline__ float act_grad(float z, int act) {
+  switch (act) {
+    case kRelu: return z > 0.f ? 1.f : 0.f;
+    case kGelu: {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      const float u = k0 * (z + k1 * z * z * z);
+      const float t = tanhf(u);
+      return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k0 * (1.f + 3.f * k1 * z * z);
+    }
+    case kElu: return z > 0.f ? 1.f : expf(z);
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ bool keep_bit(uint64_t seed, uint64_t offset, long long idx, float rate) {
+  uint32_t r[4];
+  Philox::gen(seed, offset, static_cast<uint64_t>(idx >> 2), r);
+  return Philox::uniform(r[idx & 3]) >= rate;
+}
+
+// y = dropout(act(x + bias)), x/y [rows][C] (T = float or bf16). Also writes z = x + bias if
+// zout (needed by the backward for GELU/ELU).
+template <typename T>
+__device__ __forceinline__ float ldv(const T* p, long long i) {
+  if constexpr (sizeof(T) == 2)
+    return bf2f(p[i]);
+  else
+    return p[i];
+}
+template <typename T>
+__device__ __forceinline__ void stv(T* p, long long i, float v) {
+  if constexpr (sizeof(T) == 2)
+    p[i] = f2bf(v);
+  else
+    p[i] = v;
+}
+
+template <typename T>
+__global__ void bias_act_dropout_fwd_kernel(const T* __restrict__ x, const float* __restrict__ bias,
+                                            T* __restrict__ y, long long n, int C, int act, float rate, uint64_t seed,
+                                            uint64_t offset) {
+  const float scale = rate > 0.f ? 1.f / (1.f - rate) : 1.f;
+  GRID_STRIDE(i, n) {
+    float v = ldv(x, i) + (bias ? bias[i % C] : 0.f);
+    v = act_fwd(v, act);
+    if (rate > 0.f) v = keep_bit(seed, offset, i, rate) ? v * scale : 0.f;
+    stv(y, i, v);
+  }
+}
+
+// dx = dy * dropout_mask * act'(z) with z = x + bias recomputed from the pre-activation x.
+template <typename T>
+__global__ void bias_act_dropout_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                            const float* __restrict__ bias, T* __restrict__ dx, long long n, int C,
+                                            int act, float rate, uint64_t seed, uint64_t offset) {
+  const float scale = rate > 0.f ? 1.f / (1.f - rate) : 1.f;
+  GRID_STRIDE(i, n) {
+    float g = ldv(dy, i);
+    if (rate > 0.f) g = keep_bit(seed, offset, i, rate) ? g * scale : 0.f;
+    const float z = ldv(x, i) + (bias ? bias[i % C] : 0.f);
+    stv(dx, i, g * act_grad(z, act));
+  }
+}
+
+// out[c] (+)= sum_r x[r][c]; grid.x over column chunks of 256, grid.y row slices; atomics.
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ x, long long rows, int C, float* __restrict__ out,
+                              long long rows_per_slice) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const long long r0 = blockIdx.y * rows_per_slice, r1 = min(rows, r0 + rows_per_slice);
+  float s = 0.f;
+  for (long long r = r0; r < r1; ++r) s += ldv(x, r * C + c);
+  atomicAdd(&out[c], s);
+}
+
+__global__ void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
+                                long long n8, float alpha, float beta) {
+  GRID_STRIDE(i, n8) {
+    float fa[8], fb[8];
+    unpack8(reinterpret_cast<const uint4*>(a)[i], fa);
+    unpack8(reinterpret_cast<const uint4*>(b)[i], fb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fa[j] = alpha * fa[j] + beta * fb[j];
+    reinterpret_cast<uint4*>(y)[i] = pack8(fa);
+  }
+}
+
+// fp8 (OCP e4m3fn / e5m2, gfx950 native) quantisation with a per-tensor scale:
+// q = sat(x * scale); amax (optional) accumulates max|x| for delayed scaling.
+__global__ void amax_bf16_kernel(const bf16_t* __restrict__ x, long long n, float* __restrict__ amax) {
+  float m = 0.f;
+  GRID_STRIDE(i, n) m = fmaxf(m, fabsf(bf2f(x[i])));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+}
+
+__global__ void quant_fp8_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q, long long n,
+                                 const float* __restrict__ scale, int e5m2) {
+  const float s = *scale;
+  const float lim = e5m2 ? 57344.f : 448.f;
+  GRID_STRIDE(i, n) {
+    const float v = fminf(fmaxf(bf2f(x[i]) * s, -lim), lim);
+    // gfx950 v_cvt_pk_{fp8,bf8}_f32 produce OCP e4m3fn / e5m2 (round-to-nearest-even)
+    const int packed = e5m2 ? __builtin_amdgcn_cvt_pk_bf8_f32(v, v, 0, false) : __builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false);
+    q[i] = static_cast<uint8_t>(packed & 0xff);
+  }
+}
+
+__global__ void dequant_fp8_kernel(const uint8_t* __restrict__ q, bf16_t* __restrict__ x, long long n,
+                                   const float* __restrict__ scale, int e5m2) {
+  const float inv = 1.f / *scale;
+  GRID_STRIDE(i, n) {
+    const int b = q[i];
+    const float v = e5m2 ? __builtin_amdgcn_cvt_f32_bf8(b, 0) : __builtin_amdgcn_cvt_f32_fp8(b, 0);
+    x[i] = f2bf(v * inv);
+  }
+}
+
+}  // namespace
+}  // namespace ttdk
+
+using namespace ttdk;
+
+TTDK_EXPORT int ttdk_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st) {
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, x, y, n);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bf16_to_f32(const bf16_t* x, float* y, long long n, hipStream_t st) {
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_pad_channels(const bf16_t* x, bf16_t* y, long long rows, int C, int Cp, hipStream_t st) {
+  hipLaunchKernelGGL(pad_channels_kernel, dim3(grid_for(rows * Cp)), dim3(256), 0, st, x, y, rows, C, Cp);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_unpad_channels(const bf16_t* x, bf16_t* y, long long rows, int Cp, int C, hipStream_t st) {
+  hipLaunchKernelGGL(unpad_channels_kernel, dim3(grid_for(rows * C)), dim3(256), 0, st, x, y, rows, Cp, C);
+  return hipGetLastError();
+}
+
+// [A][B][C] -> [C][B][A] bf16
+TTDK_EXPORT int ttdk_transpose_aca_bf16(const bf16_t* src, bf16_t* dst, int A, int B, int C, hipStream_t st) {
+  dim3 grid((C + 31) / 32, (A + 31) / 32, B);
+  hipLaunchKernelGGL(transpose_aca_kernel, grid, dim3(256), 0, st, src, dst, A, B, C);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_transpose2d_f32(const float* src, float* dst, int R, int C, hipStream_t st) {
+  dim3 grid((C + 31) / 32, (R + 31) / 32);
+  hipLaunchKernelGGL(transpose2d_f32_kernel, grid, dim3(256), 0, st, src, dst, R, C);
+  return hipGetLastError();
+}
+
+// dtype 0 = fp32, 1 = bf16
+TTDK_EXPORT int ttdk_bias_act_dropout_fwd(const void* x, const float* bias, void* y, long long n, int C, int act,
+                                          float rate, unsigned long long seed, unsigned long long offset, int dtype,
+                                          hipStream_t st) {
+  if (dtype == 0)
+    hipLaunchKernelGGL(bias_act_dropout_fwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st,
+                       static_cast<const float*>(x), bias, static_cast<float*>(y), n, C, act, rate, seed, offset);
+  else
+    hipLaunchKernelGGL(bias_act_dropout_fwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st,
+                       static_cast<const bf16_t*>(x), bias, static_cast<bf16_t*>(y), n, C, act, rate, seed, offset);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bias_act_dropout_bwd(const void* dy, const void* x, const float* bias, void* dx, long long n,
+                                          int C, int act, float rate, unsigned long long seed,
+                                          unsigned long long offset, int dtype, hipStream_t st) {
+  if (dtype == 0)
+    hipLaunchKernelGGL(bias_act_dropout_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st,
+                       static_cast<const float*>(dy), static_cast<const float*>(x), bias, static_cast<float*>(dx), n, C,
+                       act, rate, seed, offset);
+  else
+    hipLaunchKernelGGL(bias_act_dropout_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st,
+                       static_cast<const bf16_t*>(dy), static_cast<const bf16_t*>(x), bias, static_cast<bf16_t*>(dx), n,
+                       C, act, rate, seed, offset);
+  return hipGetLastError();
+}
+
+// out[C] = (beta ? out : 0) + column sums of x[rows][C]
+TTDK_EXPORT int ttdk_colsum(const void* x, long long rows, int C, float* out, int beta, int dtype, hipStream_t st) {
+  if (!beta) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * C, st);
+    if (e != hipSuccess) return e;
+  }
+  long long slices = (rows + 127) / 128;
+  if (slices > 256) slices = 256;
+  if (slices < 1) slices = 1;
+  const long long per = (rows + slices - 1) / slices;
+  dim3 grid((C + 255) / 256, static_cast<int>(slices));
+  if (dtype == 0)
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, static_cast<const float*>(x), rows, C, out, per);
+  else
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(x), rows, C, out, per);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long long n, float alpha, float beta,
+                              hipStream_t st) {
+  if (n % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, a, b, y, n / 8, alpha, beta);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_amax_bf16(const bf16_t* x, long long n, float* amax, int reset, hipStream_t st) {
+  if (reset) {
+    hipError_t e = hipMemsetAsync(amax, 0, sizeof(float), st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(amax_bf16_kernel, dim3(grid_for(n, 2048)), dim3(256), 0, st, x, n, amax);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_quant_fp8(const bf16_t* x, uint8_t* q, long long n, const float* scale, int e5m2, hipStream_t st) {
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, q, n, scale, e5m2);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_dequant_fp8(const uint8_t* q, bf16_t* x, long long n, const float* scale, int e5m2,
+                                 hipStream_t st) {
+  hipLaunchKernelGGL(dequant_fp8_kernel, dim3(grid_for(n)), dim3(256), 0, st, q, x, n, scale, e5m2);
+  return hipGetLastError();
+}

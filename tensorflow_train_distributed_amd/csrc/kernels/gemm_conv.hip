@@ -77,8 +77,8 @@ struct GatherParams {  // conv operand geometry (see KConvGather / MNConvGather)
   int K;
 };
 
-template <int ROWS>
-struct KDense {  // element (row, k) at p[row * ld + k]
+template <int ROWS, bool VEC = true>
+struct KDense {  // element (row, k) at p[row * ld + k]; VEC: K % 8 == 0, ld % 8 == 0, 16-B aligned base
   using Params = DenseParams;
   static constexpr int N = ROWS / 32;
   static constexpr int BYTES = ROWS * BK * 2;
@@ -97,9 +97,24 @@ struct KDense {  // element (row, k) at p[row * ld + k]
     }
   }
   __device__ __forceinline__ void load(int k0) {
-    const bool kin = k0 + c * 8 < K;
+    if constexpr (VEC) {
+      const bool kin = k0 + c * 8 < K;
 #pragma unroll
-    for (int i = 0; i < N; ++i) r[i] = (ok[i] && kin) ? ldg16(ptr[i] + k0) : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < N; ++i) r[i] = (ok[i] && kin) ? ldg16(ptr[i] + k0) : make_uint4(0, 0, 0, 0);
+    } else {
+      const int kb = k0 + c * 8;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t lo = (ok[i] && kb + 2 * e < K) ? ptr[i][k0 + 2 * e] : 0u;
+          const uint32_t hi = (ok[i] && kb + 2 * e + 1 < K) ? ptr[i][k0 + 2 * e + 1] : 0u;
+          w[e] = lo | (hi << 16);
+        }
+        r[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
   }
   __device__ __forceinline__ void store(char* lds, int tid) const {
 #pragma unroll
@@ -200,8 +215,8 @@ __device__ __forceinline__ bf16x8_t mn_frag(const char* lds, int colbase, int ks
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int ROWS>
-struct MNDense {  // element (k, row) at p[k * ld + row]
+template <int ROWS, bool VEC = true>
+struct MNDense {  // element (k, row) at p[k * ld + row]; VEC: rows % 8 == 0, ld % 8 == 0, aligned base
   using Params = DenseParams;
   static constexpr int CPR = ROWS / 8;           // 16-B chunks per k-row
   static constexpr int KPP = NTHR / CPR;         // k-rows per pass
@@ -209,7 +224,7 @@ struct MNDense {  // element (k, row) at p[k * ld + row]
   static constexpr int BYTES = ROWS * BK * 2;
   const bf16_t* p;
   long long ld;
-  int K, cc, kr;
+  int K, cc, kr, rows_left;
   bool cok;
   uint4 r[N];
   __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
@@ -218,13 +233,27 @@ struct MNDense {  // element (k, row) at p[k * ld + row]
     ld = P.ld;
     K = P.K;
     cok = row0 + cc * 8 < P.rows;
+    rows_left = P.rows - (row0 + cc * 8);
     p = P.p + row0 + cc * 8;
   }
   __device__ __forceinline__ void load(int k0) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int k = k0 + kr + KPP * i;
-      r[i] = (cok && k < K) ? ldg16(p + static_cast<long long>(k) * ld) : make_uint4(0, 0, 0, 0);
+      if constexpr (VEC) {
+        r[i] = (cok && k < K) ? ldg16(p + static_cast<long long>(k) * ld) : make_uint4(0, 0, 0, 0);
+      } else {
+        const bf16_t* q = p + static_cast<long long>(k) * ld;
+        const bool kok = cok && k < K;
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t lo = (kok && 2 * e < rows_left) ? q[2 * e] : 0u;
+          const uint32_t hi = (kok && 2 * e + 1 < rows_left) ? q[2 * e + 1] : 0u;
+          w[e] = lo | (hi << 16);
+        }
+        r[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
     }
   }
   __device__ __forceinline__ void store(char* lds, int tid) const {
@@ -341,7 +370,7 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
         const int n = nwave + tn * 16 + 4 * g;
         f32x4_t v = acc[tm][tn] * E.alpha;
         float* o = out + static_cast<long long>(m) * E.ldo + n;
-        if (n + 3 < N) {
+        if (n + 3 < N && (E.ldo & 3) == 0) {
           if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
           *reinterpret_cast<f32x4_t*>(o) = v;
         } else {
@@ -375,7 +404,7 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += (n + j < N) ? E.bias[n + j] : 0.f;
       }
-      const bool full = n + 3 < N;
+      const bool full = n + 3 < N && (E.ldo & 3) == 0 && (E.ldr & 3) == 0;
       if (E.residual) {
         const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
         if (full) {
@@ -593,6 +622,10 @@ hipError_t dispatch(const void* pa_raw, const void* pb_raw, const EpiParams& pe,
 }
 
 template <int R>
+using KDenseS = KDense<R, false>;
+template <int R>
+using MNDenseS = MNDense<R, false>;
+template <int R>
 using KConvFwd = KConvGather<R, false>;
 template <int R>
 using KConvDgrad = KConvGather<R, true>;
@@ -648,23 +681,23 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
                                const TtdkEpilogue* epi, hipStream_t st) {
   EpiParams pe = to_epi(epi);
   if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
-  if (a_kmajor && b_kmajor) {
-    DenseParams pa{A, lda, M, K};
-    DenseParams pb{B, ldb, N, K};
-    return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
-  } else if (a_kmajor && !b_kmajor) {
-    DenseParams pa{A, lda, M, K};
-    DenseParams pb{B, ldb, N, K};
-    return dispatch<KDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
-  } else if (!a_kmajor && b_kmajor) {
-    DenseParams pa{A, lda, M, K};
-    DenseParams pb{B, ldb, N, K};
-    return dispatch<MNDense, KDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
-  } else {
-    DenseParams pa{A, lda, M, K};
-    DenseParams pb{B, ldb, N, K};
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  // 16-B vector operand loads need the contiguous dim and the leading dim to be multiples
+  // of 8 elements and 16-B aligned bases; otherwise both operands use the masked scalar path.
+  const bool vec = al(A) && al(B) && lda % 8 == 0 && ldb % 8 == 0 && (a_kmajor ? K % 8 == 0 : M % 8 == 0) &&
+                   (b_kmajor ? K % 8 == 0 : N % 8 == 0);
+  DenseParams pa{A, lda, M, K};
+  DenseParams pb{B, ldb, N, K};
+  if (vec) {
+    if (a_kmajor && b_kmajor) return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+    if (a_kmajor) return dispatch<KDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+    if (b_kmajor) return dispatch<MNDense, KDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
     return dispatch<MNDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
   }
+  if (a_kmajor && b_kmajor) return dispatch<KDenseS, KDenseS>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  if (a_kmajor) return dispatch<KDenseS, MNDenseS>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  if (b_kmajor) return dispatch<MNDenseS, KDenseS>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  return dispatch<MNDenseS, MNDenseS>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
 }
 
 struct TtdkConv {

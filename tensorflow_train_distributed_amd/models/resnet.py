@@ -1,0 +1,282 @@
+"""ResNet-50 v1.5 (the BASELINE.json headline model) on the gfx950 kernel library.
+
+Execution model (MI355X-first):
+* activations NHWC bf16; conv filters stored [K, R, S, C] (the implicit-GEMM B operand);
+* all variables (conv kernels, BN gamma/beta/moving stats, FC) live in one FlatParams store
+  laid out in *backward-completion order*, so gradient all-reduce buckets are contiguous
+  slices of the flat gradient buffer that complete front to back during backward;
+* every conv+BN(+ReLU)(+residual) unit is hand-scheduled:
+    fwd: implicit-GEMM conv whose epilogue emits per-tile BN partial sums -> tiny reduce +
+         finalize -> one fused apply pass (scale/shift, residual add, ReLU);
+    bwd: one fused BN-backward reduce pass (ReLU mask from the saved output, shortcut
+         gradient emitted on the fly) -> finalize -> apply -> wgrad (split-K, fp32 straight
+         into the flat gradient slice) + dgrad (accumulating into the shortcut gradient);
+* the explicit forward/backward order gives the collective engine exact "gradient ready"
+  points, and makes the whole step capturable into hipGraphs.
+
+Variable names follow tf.keras.applications.ResNet50 (conv{stage}_block{b}_{i}_conv/kernel,
+..._bn/{gamma,beta,moving_mean,moving_variance}, predictions/{kernel,bias}); checkpoint
+conversion to TF's [R,S,C,K] kernel layout happens in the checkpoint layer.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..train.flat import FlatParams, ParamSpec
+
+STAGES_50 = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
+
+
+def _he_init(fan_in):
+    def init(t, gen):
+        std = math.sqrt(2.0 / fan_in) / 0.87962566103423978  # truncated-normal (+-2 sigma) correction
+        t.normal_(0.0, std, generator=gen)
+        t.clamp_(-2 * std, 2 * std)
+    return init
+
+
+def _fill(v):
+    def init(t, gen):
+        t.fill_(v)
+    return init
+
+
+def _glorot(fan_in, fan_out):
+    def init(t, gen):
+        lim = math.sqrt(6.0 / (fan_in + fan_out))
+        t.uniform_(-lim, lim, generator=gen)
+    return init
+
+
+@dataclass
+class ConvSpec:
+    name: str
+    cin: int
+    cout: int
+    k: int
+    stride: int
+    pad: int
+    cin_store: int  # channels as stored (stem input padded 3 -> 8)
+
+
+class ResNet:
+    def __init__(self, stages=STAGES_50, num_classes=1000, in_channels=3, device="cuda", seed=0,
+                 bn_momentum=0.9, bn_eps=1e-5, width=64):
+        self.device = torch.device(device)
+        self.num_classes = num_classes
+        self.in_channels = in_channels
+        self.in_store = 8 if in_channels <= 8 else (in_channels + 7) // 8 * 8
+        self.bn_momentum = bn_momentum
+        self.bn_eps = bn_eps
+        self.stem = ConvSpec("conv1", in_channels, width, 7, 2, 3, self.in_store)
+        self.blocks = []  # list of dicts
+        cin = width
+        for si, (mid, n, stride) in enumerate(stages):
+            for b in range(n):
+                s = stride if b == 0 else 1
+                pre = "conv%d_block%d" % (si + 2, b + 1)
+                blk = {
+                    "c1": ConvSpec(pre + "_1", cin, mid, 1, 1, 0, cin),
+                    "c2": ConvSpec(pre + "_2", mid, mid, 3, s, 1, mid),
+                    "c3": ConvSpec(pre + "_3", mid, mid * 4, 1, 1, 0, mid),
+                    "cd": ConvSpec(pre + "_0", cin, mid * 4, 1, s, 0, cin) if (s != 1 or cin != mid * 4) else None,
+                }
+                self.blocks.append(blk)
+                cin = mid * 4
+        self.feat = cin
+        self.params = FlatParams(self._specs(), self.device, seed=seed)
+
+    # ----------------------------------------------------------------- variables
+    def _conv_specs(self, c: ConvSpec):
+        fan_in = c.k * c.k * c.cin
+        return [
+            ParamSpec(c.name + "_conv/kernel", (c.cout, c.k, c.k, c.cin_store), _he_init(fan_in), True,
+                      meta={"layout": "KRSC", "tf_shape": (c.k, c.k, c.cin, c.cout), "cin": c.cin}),
+            ParamSpec(c.name + "_bn/gamma", (c.cout,), _fill(1.0), False),
+            ParamSpec(c.name + "_bn/beta", (c.cout,), _fill(0.0), False),
+            ParamSpec(c.name + "_bn/moving_mean", (c.cout,), _fill(0.0), False, trainable=False),
+            ParamSpec(c.name + "_bn/moving_variance", (c.cout,), _fill(1.0), False, trainable=False),
+        ]
+
+    def _specs(self):
+        specs = [
+            ParamSpec("predictions/kernel", (self.feat, self.num_classes), _glorot(self.feat, self.num_classes), True),
+            ParamSpec("predictions/bias", (self.num_classes,), _fill(0.0), False),
+        ]
+        for blk in reversed(self.blocks):  # backward-completion order
+            for key in ("c3", "c2", "cd", "c1"):
+                if blk[key] is not None:
+                    specs += self._conv_specs(blk[key])
+        specs += self._conv_specs(self.stem)
+        # zero the padded input channels of the stem kernel (they must stay zero)
+        stem_k = specs[-5]
+        base_init = stem_k.init
+        cin = self.in_channels
+
+        def stem_init(t, gen, base_init=base_init, cin=cin):
+            base_init(t, gen)
+            t[..., cin:] = 0.0
+        stem_k.init = stem_init
+        return specs
+
+    def conv_list(self) -> List[ConvSpec]:
+        out = [self.stem]
+        for blk in self.blocks:
+            out += [blk[k] for k in ("c1", "c2", "c3", "cd") if blk[k] is not None]
+        return out
+
+    # ----------------------------------------------------------------- GPU engine
+    def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None):
+        from ..ops import gemm as G
+        from ..ops import kernels as K
+        P = self.params
+        N, H, W, C = x.shape
+        Pp = (H + 2 * c.pad - c.k) // c.stride + 1
+        Q = (W + 2 * c.pad - c.k) // c.stride + 1
+        M = N * Pp * Q
+        bm = 128 if M > 64 else 64
+        bn = 128 if c.cout > 64 else 64
+        T = -(-M // bm)
+        partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
+        y = G.conv_fwd(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
+                       tile=(bm, bn))
+        sums = K.bn_reduce_partials(partial, T, c.cout)
+        st = K.BNState(c.cout, x.device)
+        pre = c.name + "_bn/"
+        K.bn_fwd_finalize(sums, M, P.var[pre + "gamma"], P.var[pre + "beta"], self.bn_eps, self.bn_momentum,
+                          P.var[pre + "moving_mean"], P.var[pre + "moving_variance"], st)
+        y2 = y.view(M, c.cout)
+        out = K.bn_apply(y2, st.scale, st.shift, residual=None if residual is None else residual.view(M, c.cout),
+                         relu=relu).view(N, Pp, Q, c.cout)
+        return out, (x, y, out if relu else None, st)
+
+    def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0):
+        from ..ops import gemm as G
+        from ..ops import kernels as K
+        P = self.params
+        x, y, out, st = ctx
+        N, Pp, Q, Kc = y.shape
+        M = N * Pp * Q
+        pre = c.name + "_bn/"
+        dz = K.bn_backward(dout.view(M, Kc), None if out is None else out.view(M, Kc), y.view(M, Kc),
+                           P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
+                           g_out=None if g_out is None else g_out.view(M, Kc)).view(N, Pp, Q, Kc)
+        wname = c.name + "_conv/kernel"
+        G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+        self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
+        if not need_dx:
+            return None
+        wt = K.krsc_to_crsk(P.c[wname])
+        return G.conv_dgrad(dz, wt, x.shape, (c.stride, c.stride), (c.pad, c.pad), out=dx, beta=dx_beta)
+
+    def _ready(self, name):
+        if self._grad_hook is not None:
+            self._grad_hook(name)
+
+    def forward_backward(self, images, labels, grad_scale: Optional[float] = None, grad_hook=None):
+        """One training forward + backward on the GPU engine.
+
+        images: [N, H, W, in_channels] bf16 (NHWC); labels: [N] int. Writes every trainable
+        gradient into params.grad; returns a device fp32[2] = (mean loss, mean accuracy).
+        grad_hook(name) is called as soon as the gradients of every variable up to and
+        including `name` (in flat-layout order) are final — the bucketed all-reduce cut points.
+        """
+        from ..ops import gemm as G
+        from ..ops import kernels as K
+        self._grad_hook = grad_hook
+        P = self.params
+        N = images.shape[0]
+        if grad_scale is None:
+            grad_scale = 1.0 / N
+        x = images if images.shape[-1] == self.in_store else K.pad_channels(images.contiguous(), self.in_store)
+        # ---- forward
+        s_out, s_ctx = self._convbn_fwd(self.stem, x, relu=True)
+        h, arg = K.maxpool_fwd(s_out, 3, 2, 1)
+        ctxs = []
+        for blk in self.blocks:
+            o1, c1 = self._convbn_fwd(blk["c1"], h, True)
+            o2, c2 = self._convbn_fwd(blk["c2"], o1, True)
+            if blk["cd"] is not None:
+                sc, cd = self._convbn_fwd(blk["cd"], h, False)
+            else:
+                sc, cd = h, None
+            o3, c3 = self._convbn_fwd(blk["c3"], o2, True, residual=sc)
+            ctxs.append((c1, c2, c3, cd))
+            h = o3
+        feat_shape = h.shape
+        pooled = K.avgpool_fwd(h)
+        logits = G.gemm(pooled, P.c["predictions/kernel"], bias=P.var["predictions/bias"])
+        sums, dlogits, _, _ = K.sparse_xent(logits, labels, grad_scale)
+        # ---- backward
+        G.gemm(pooled, dlogits, trans_a=True, out=P.g["predictions/kernel"])
+        K.colsum(dlogits, out=P.g["predictions/bias"])
+        self._ready("predictions/bias")
+        dpooled = G.gemm(dlogits, P.c["predictions/kernel"], trans_b=True)
+        dh = K.avgpool_bwd(dpooled, feat_shape)
+        for blk, (c1, c2, c3, cd) in zip(reversed(self.blocks), reversed(ctxs)):
+            g_sc = torch.empty_like(dh)
+            d2 = self._convbn_bwd(blk["c3"], dh, c3, g_out=g_sc)
+            d1 = self._convbn_bwd(blk["c2"], d2, c2)
+            if blk["cd"] is not None:
+                dx = self._convbn_bwd(blk["cd"], g_sc, cd)
+            else:
+                dx = g_sc
+            dh = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1)
+        dstem = K.maxpool_bwd(dh, arg, s_out.shape, 3, 2, 1)
+        self._convbn_bwd(self.stem, dstem, s_ctx, need_dx=False)
+        self._grad_hook = None
+        return sums
+
+    # ----------------------------------------------------------------- reference (CPU / oracle)
+    def reference_loss(self, images, labels, params=None):
+        """fp32 PyTorch implementation of the same network (NCHW internally), used on CPU and
+        as the numerics oracle for the GPU engine. Returns (loss, accuracy, logits); BN uses
+        batch statistics (training mode) and does not touch the moving averages."""
+        P = params if params is not None else {n: self.params.var[n] for n in self.params.names()}
+        x = images.float().permute(0, 3, 1, 2)
+
+        def convbn(c, t, relu, res=None):
+            w = P[c.name + "_conv/kernel"][..., :t.shape[1]].permute(0, 3, 1, 2)
+            y = F.conv2d(t, w, stride=c.stride, padding=c.pad)
+            y = F.batch_norm(y, None, None, P[c.name + "_bn/gamma"], P[c.name + "_bn/beta"], training=True,
+                             eps=self.bn_eps)
+            if res is not None:
+                y = y + res
+            return F.relu(y) if relu else y
+
+        h = convbn(self.stem, x, True)
+        h = F.max_pool2d(h, 3, 2, 1)
+        for blk in self.blocks:
+            o = convbn(blk["c1"], h, True)
+            o = convbn(blk["c2"], o, True)
+            sc = convbn(blk["cd"], h, False) if blk["cd"] is not None else h
+            h = convbn(blk["c3"], o, True, sc)
+        pooled = h.mean((2, 3))
+        logits = pooled @ P["predictions/kernel"] + P["predictions/bias"]
+        loss = F.cross_entropy(logits, labels.long())
+        acc = (logits.argmax(1) == labels.long()).float().mean()
+        return loss, acc, logits
+
+    def reference_forward_backward(self, images, labels, grad_scale=None):
+        """CPU training step: autograd through reference_loss, gradients written to the flat
+        gradient buffer (same contract as forward_backward)."""
+        P = self.params
+        leaves = {n: P.var[n].detach().clone().requires_grad_(P.spec(n).trainable) for n in P.names()}
+        loss, acc, _ = self.reference_loss(images, labels, leaves)
+        scale = 1.0 if grad_scale is None else grad_scale * images.shape[0]
+        (loss * scale).backward()
+        with torch.no_grad():
+            for n, t in leaves.items():
+                if t.grad is not None:
+                    P.g[n].copy_(t.grad)
+        return torch.stack([loss.detach(), acc.detach()])
+
+
+def resnet50(num_classes=1000, device="cuda", **kw) -> ResNet:
+    return ResNet(STAGES_50, num_classes=num_classes, device=device, **kw)

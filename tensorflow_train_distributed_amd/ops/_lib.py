@@ -52,6 +52,42 @@ _SIGS = {
     "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
+    # batchnorm.hip
+    "ttdk_bn_num_partials": [L, I],
+    "ttdk_bn_stats_partial": [P, L, I, P, I, P],
+    "ttdk_bn_bwd_partial": [P, P, P, L, I, P, I, P, P],
+    "ttdk_bn_reduce_partials": [P, I, I, P, P],
+    "ttdk_bn_fwd_finalize": [P, F, I, P, P, F, F, P, P, P, P, P, P, P],
+    "ttdk_bn_bwd_finalize": [P, F, I, P, P, P, P, P, P, I, P],
+    "ttdk_bn_apply": [P, P, P, P, P, L, I, I, P],
+    "ttdk_bn_bwd_apply": [P, P, P, P, P, L, I, P],
+    # pool.hip
+    "ttdk_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
+    "ttdk_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
+    "ttdk_avgpool_fwd": [P, P, P, I, I, I, P],
+    "ttdk_avgpool_bwd": [P, P, I, I, I, P],
+    # xent.hip
+    "ttdk_sparse_xent": [P, I, P, I, I, I, F, P, P, P, P, P],
+    # optim.hip
+    "ttdk_opt_sgd": [P, P, P, P, P, I, P, P, P, I, P],
+    "ttdk_opt_adam": [P, P, P, P, P, P, I, P, P, P, I, P],
+    "ttdk_opt_lamb": [P, P, P, P, P, P, P, I, I, P, P, P, P, P],
+    "ttdk_sumsq": [P, L, P, P],
+    "ttdk_lr_schedule": [P, P, I, P, F, F, I, P],
+    # elementwise.hip
+    "ttdk_f32_to_bf16": [P, P, L, P],
+    "ttdk_bf16_to_f32": [P, P, L, P],
+    "ttdk_pad_channels": [P, P, L, I, I, P],
+    "ttdk_unpad_channels": [P, P, L, I, I, P],
+    "ttdk_transpose_aca_bf16": [P, P, I, I, I, P],
+    "ttdk_transpose2d_f32": [P, P, I, I, P],
+    "ttdk_bias_act_dropout_fwd": [P, P, P, L, I, I, F, U64, U64, I, P],
+    "ttdk_bias_act_dropout_bwd": [P, P, P, P, L, I, I, F, U64, U64, I, P],
+    "ttdk_colsum": [P, L, I, P, I, I, P],
+    "ttdk_add_bf16": [P, P, P, L, F, F, P],
+    "ttdk_amax_bf16": [P, L, P, I, P],
+    "ttdk_quant_fp8": [P, P, L, P, I, P],
+    "ttdk_dequant_fp8": [P, P, L, P, I, P],
 }
 
 _fns = {}
@@ -80,6 +116,11 @@ def call(name, *args):
     rc = fn(name)(*args)
     if rc != 0:
         raise HipKernelError("%s failed with hipError_t %d" % (name, rc))
+
+
+def query(name, *args):
+    """Call a host-side helper that returns a plain int (not a hipError_t)."""
+    return fn(name)(*args)
 
 
 def stream():

@@ -59,8 +59,6 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     Kb, N = (b.shape[1], b.shape[0]) if trans_b else b.shape
     if K != Kb:
         raise ValueError("gemm inner dims differ: %d vs %d" % (K, Kb))
-    if K % 8 or (trans_a and M % 8) or (not trans_b and N % 8):
-        raise ValueError("gemm needs the contiguous dims to be multiples of 8")
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     a_kmajor = 0 if trans_a else 1

@@ -1,0 +1,240 @@
+"""Thin launch wrappers for the non-GEMM gfx950 kernels (BatchNorm, pooling, fused
+cross-entropy, element-wise/layout, optimizers, fp8). All tensors are CUDA tensors; every
+launch goes to PyTorch's current stream. See the .hip files for the math."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_ELU = 0, 1, 2, 3
+
+
+def _s():
+    return _lib.stream()
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------ BatchNorm (NHWC)
+def bn_num_partials(M, C):
+    return _lib.query("ttdk_bn_num_partials", M, C)
+
+
+def bn_stats_partial(x2d, partial=None):
+    """Per-block partial sums of x and x^2 over rows of x2d [M, C] -> (partial [T,2,C], T)."""
+    M, C = x2d.shape
+    T = bn_num_partials(M, C)
+    if partial is None:
+        partial = torch.empty((T, 2, C), dtype=torch.float32, device=x2d.device)
+    _lib.call("ttdk_bn_stats_partial", x2d.data_ptr(), M, C, partial.data_ptr(), T, _s())
+    return partial, T
+
+
+def bn_reduce_partials(partial, T, C, sums=None):
+    if sums is None:
+        sums = torch.empty((2, C), dtype=torch.float32, device=partial.device)
+    _lib.call("ttdk_bn_reduce_partials", partial.data_ptr(), T, C, sums.data_ptr(), _s())
+    return sums
+
+
+class BNState:
+    """Per-call saved statistics of a training-mode BN forward."""
+
+    __slots__ = ("mean", "rstd", "scale", "shift")
+
+    def __init__(self, C, device):
+        buf = torch.empty((4, C), dtype=torch.float32, device=device)
+        self.mean, self.rstd, self.scale, self.shift = buf[0], buf[1], buf[2], buf[3]
+
+
+def bn_fwd_finalize(sums, count, gamma, beta, eps, momentum, running_mean, running_var, state):
+    C = sums.shape[-1]
+    _lib.call("ttdk_bn_fwd_finalize", sums.data_ptr(), float(count), C, _p(gamma), _p(beta), float(eps),
+              float(momentum), _p(running_mean), _p(running_var), state.mean.data_ptr(), state.rstd.data_ptr(),
+              state.scale.data_ptr(), state.shift.data_ptr(), _s())
+
+
+def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None):
+    M, C = y2d.shape
+    if out is None:
+        out = torch.empty_like(y2d)
+    _lib.call("ttdk_bn_apply", y2d.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(residual), out.data_ptr(),
+              M * C, C, int(relu), _s())
+    return out
+
+
+def bn_backward(dout, out_for_relu, y, gamma, state, dgamma, dbeta, *, g_out=None, dz=None, accumulate=False):
+    """dz = BN-backward(relu-mask(dout)). Writes dgamma/dbeta (fp32 [C]) and optionally the
+    relu-masked gradient g_out (needed by residual shortcuts)."""
+    M, C = y.shape
+    T = bn_num_partials(M, C)
+    partial = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
+    _lib.call("ttdk_bn_bwd_partial", dout.data_ptr(), _p(out_for_relu), y.data_ptr(), M, C, partial.data_ptr(), T,
+              _p(g_out), _s())
+    sums = bn_reduce_partials(partial, T, C)
+    coef = torch.empty((3, C), dtype=torch.float32, device=y.device)
+    _lib.call("ttdk_bn_bwd_finalize", sums.data_ptr(), float(M), C, _p(gamma), state.mean.data_ptr(),
+              state.rstd.data_ptr(), _p(dgamma), _p(dbeta), coef.data_ptr(), int(accumulate), _s())
+    if dz is None:
+        dz = torch.empty_like(y)
+    _lib.call("ttdk_bn_bwd_apply", dout.data_ptr(), _p(out_for_relu), y.data_ptr(), coef.data_ptr(), dz.data_ptr(),
+              M * C, C, _s())
+    return dz
+
+
+# ------------------------------------------------------------------ pooling
+def pool_out(H, k, s, p):
+    return (H + 2 * p - k) // s + 1
+
+
+def maxpool_fwd(x, k=3, s=2, p=1):
+    N, H, W, C = x.shape
+    P, Q = pool_out(H, k, s, p), pool_out(W, k, s, p)
+    y = torch.empty((N, P, Q, C), dtype=x.dtype, device=x.device)
+    arg = torch.empty((N, P, Q, C), dtype=torch.uint8, device=x.device)
+    _lib.call("ttdk_maxpool_fwd", x.data_ptr(), y.data_ptr(), arg.data_ptr(), N, H, W, C, P, Q, k, k, s, s, p, p, _s())
+    return y, arg
+
+
+def maxpool_bwd(dy, arg, x_shape, k=3, s=2, p=1):
+    N, H, W, C = x_shape
+    P, Q = dy.shape[1], dy.shape[2]
+    dx = torch.empty(tuple(x_shape), dtype=dy.dtype, device=dy.device)
+    _lib.call("ttdk_maxpool_bwd", dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, C, P, Q, k, k, s, s, p, p,
+              _s())
+    return dx
+
+
+def avgpool_fwd(x):
+    N, H, W, C = x.shape
+    y = torch.empty((N, C), dtype=x.dtype, device=x.device)
+    _lib.call("ttdk_avgpool_fwd", x.data_ptr(), y.data_ptr(), None, N, H * W, C, _s())
+    return y
+
+
+def avgpool_bwd(dy, x_shape):
+    N, H, W, C = x_shape
+    dx = torch.empty(tuple(x_shape), dtype=dy.dtype, device=dy.device)
+    _lib.call("ttdk_avgpool_bwd", dy.data_ptr(), dx.data_ptr(), N, H * W, C, _s())
+    return dx
+
+
+# ------------------------------------------------------------------ cross-entropy
+def sparse_xent(logits, labels, grad_scale=None, *, want_grad=True, want_rows=False, sums=None):
+    """Fused sparse softmax cross-entropy fwd+bwd + in_top_k(1).
+
+    Returns (sums[2] = (mean loss, mean accuracy), dlogits or None, loss_rows or None, correct or None).
+    """
+    rows, V = logits.shape
+    if grad_scale is None:
+        grad_scale = 1.0 / rows
+    lab = labels if labels.dtype in (torch.int32, torch.int64) else labels.long()
+    if sums is None:
+        sums = torch.empty(2, dtype=torch.float32, device=logits.device)
+    dl = torch.empty_like(logits) if want_grad else None
+    lr = torch.empty(rows, dtype=torch.float32, device=logits.device) if want_rows else None
+    corr = torch.empty(rows, dtype=torch.uint8, device=logits.device) if want_rows else None
+    _lib.call("ttdk_sparse_xent", logits.data_ptr(), _DT[logits.dtype], lab.data_ptr(),
+              0 if lab.dtype == torch.int32 else 1, rows, V, float(grad_scale), _p(lr), _p(dl), _p(corr),
+              sums.data_ptr(), _s())
+    return sums, dl, lr, corr
+
+
+# ------------------------------------------------------------------ element-wise / layout
+def f32_to_bf16(x, out=None):
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    _lib.call("ttdk_f32_to_bf16", x.data_ptr(), out.data_ptr(), x.numel(), _s())
+    return out
+
+
+def bf16_to_f32(x, out=None):
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    _lib.call("ttdk_bf16_to_f32", x.data_ptr(), out.data_ptr(), x.numel(), _s())
+    return out
+
+
+def pad_channels(x, Cp):
+    C = x.shape[-1]
+    rows = x.numel() // C
+    y = torch.empty(x.shape[:-1] + (Cp,), dtype=x.dtype, device=x.device)
+    _lib.call("ttdk_pad_channels", x.data_ptr(), y.data_ptr(), rows, C, Cp, _s())
+    return y
+
+
+def krsc_to_crsk(w, out=None):
+    """bf16 conv filter [K,R,S,C] -> [C,R,S,K] (the data-gradient operand)."""
+    K, R, S, C = w.shape
+    if out is None:
+        out = torch.empty((C, R, S, K), dtype=w.dtype, device=w.device)
+    _lib.call("ttdk_transpose_aca_bf16", w.data_ptr(), out.data_ptr(), K, R * S, C, _s())
+    return out
+
+
+def bias_act_dropout(x, bias, act=ACT_NONE, rate=0.0, seed=0, offset=0, out=None):
+    C = x.shape[-1]
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("ttdk_bias_act_dropout_fwd", x.data_ptr(), _p(bias), out.data_ptr(), x.numel(), C, act, float(rate),
+              seed, offset, _DT[x.dtype], _s())
+    return out
+
+
+def bias_act_dropout_bwd(dy, x, bias, act=ACT_NONE, rate=0.0, seed=0, offset=0, out=None):
+    C = x.shape[-1]
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("ttdk_bias_act_dropout_bwd", dy.data_ptr(), x.data_ptr(), _p(bias), out.data_ptr(), x.numel(), C, act,
+              float(rate), seed, offset, _DT[x.dtype], _s())
+    return out
+
+
+def colsum(x2d, out=None, beta=0):
+    rows, C = x2d.shape
+    if out is None:
+        out = torch.empty(C, dtype=torch.float32, device=x2d.device)
+    _lib.call("ttdk_colsum", x2d.data_ptr(), rows, C, out.data_ptr(), int(beta), _DT[x2d.dtype], _s())
+    return out
+
+
+def add_bf16(a, b, out=None, alpha=1.0, beta=1.0):
+    if out is None:
+        out = torch.empty_like(a)
+    _lib.call("ttdk_add_bf16", a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), float(alpha), float(beta), _s())
+    return out
+
+
+# ------------------------------------------------------------------ fp8 (OCP e4m3fn / e5m2)
+def amax(x, out=None, reset=True):
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=x.device)
+    _lib.call("ttdk_amax_bf16", x.data_ptr(), x.numel(), out.data_ptr(), int(reset), _s())
+    return out
+
+
+def quant_fp8(x, scale, e5m2=False, out=None):
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _lib.call("ttdk_quant_fp8", x.data_ptr(), out.data_ptr(), x.numel(), scale.data_ptr(), int(e5m2), _s())
+    return out
+
+
+def dequant_fp8(q, scale, e5m2=False, out=None):
+    if out is None:
+        out = torch.empty(q.shape, dtype=torch.bfloat16, device=q.device)
+    _lib.call("ttdk_dequant_fp8", q.data_ptr(), out.data_ptr(), q.numel(), scale.data_ptr(), int(e5m2), _s())
+    return out
+
+
+# ------------------------------------------------------------------ optimizer primitives
+def sumsq(x, out=None):
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=x.device)
+    _lib.call("ttdk_sumsq", x.data_ptr(), x.numel(), out.data_ptr(), _s())
+    return out

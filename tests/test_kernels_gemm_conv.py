@@ -11,7 +11,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (1000, 200, 784), (128, 1000, 2048), (4096, 64, 64),
-                                   (72, 136, 520)])
+                                   (72, 136, 520), (128, 100, 200), (128, 25, 50), (77, 10, 25), (3, 5, 7)])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 def test_gemm_layouts(M, N, K, ta, tb):
     from tensorflow_train_distributed_amd.ops import gemm as G

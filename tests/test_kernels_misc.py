@@ -1,0 +1,147 @@
+"""Numerics of BN / pooling / xent / element-wise / fp8 / optimizer kernels vs PyTorch fp32."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_batchnorm_fwd_bwd_relu_residual():
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(0)
+    M, C = 3000, 96
+    y = (torch.randn(M, C, device="cuda") * 2 + 1).bfloat16()
+    res = torch.randn(M, C, device="cuda").bfloat16()
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda")
+    rm = torch.zeros(C, device="cuda")
+    rv = torch.ones(C, device="cuda")
+    partial, T = K.bn_stats_partial(y)
+    sums = K.bn_reduce_partials(partial, T, C)
+    st = K.BNState(C, "cuda")
+    K.bn_fwd_finalize(sums, M, gamma, beta, 1e-5, 0.9, rm, rv, st)
+    out = K.bn_apply(y, st.scale, st.shift, residual=res, relu=True)
+    yr = y.float().requires_grad_(True)
+    g_r = gamma.clone().requires_grad_(True)
+    b_r = beta.clone().requires_grad_(True)
+    ref = torch.relu(F.batch_norm(yr, None, None, g_r, b_r, training=True, eps=1e-5) + res.float())
+    assert _rel(out, ref) < 1e-2
+    torch.testing.assert_close(rm, 0.1 * y.float().mean(0), rtol=1e-3, atol=1e-3)
+    dout = torch.randn(M, C, device="cuda").bfloat16()
+    ref.backward(dout.float())
+    dg = torch.empty(C, device="cuda")
+    db = torch.empty(C, device="cuda")
+    g_sc = torch.empty_like(dout)
+    dz = K.bn_backward(dout, out, y, gamma, st, dg, db, g_out=g_sc)
+    assert _rel(dz, yr.grad) < 2e-2
+    assert _rel(dg, g_r.grad) < 1e-2
+    assert _rel(db, b_r.grad) < 1e-2
+    assert _rel(g_sc, dout.float() * (out.float() > 0)) < 1e-6
+
+
+def test_maxpool_avgpool():
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(1)
+    x = torch.randn(2, 17, 17, 64, device="cuda").bfloat16()
+    y, arg = K.maxpool_fwd(x, 3, 2, 1)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(y.float(), yr.permute(0, 2, 3, 1))
+    dy = torch.randn_like(y)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    dx = K.maxpool_bwd(dy, arg, x.shape, 3, 2, 1)
+    assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    p = K.avgpool_fwd(x)
+    assert _rel(p, x.float().mean((1, 2))) < 1e-2
+    dp = torch.randn(2, 64, device="cuda").bfloat16()
+    dxa = K.avgpool_bwd(dp, x.shape)
+    assert _rel(dxa, (dp.float() / (17 * 17))[:, None, None, :].expand(x.shape)) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sparse_xent_in_top_k(dtype):
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(2)
+    z = torch.randn(37, 1000, device="cuda").to(dtype)
+    lab = torch.randint(0, 1000, (37,), device="cuda")
+    lab[0] = z[0].float().argmax()
+    z[1, 5] = z[1].float().max() + 1
+    z[1, 7] = z[1, 5]  # tie on the max: strictly-greater rule -> label 5 is top-1
+    lab[1] = 5
+    sums, dl, rows, corr = K.sparse_xent(z, lab, want_rows=True)
+    zr = z.float().requires_grad_(True)
+    loss = F.cross_entropy(zr, lab, reduction="none")
+    loss.mean().backward()
+    assert _rel(rows, loss) < 1e-3
+    assert _rel(dl, zr.grad) < 1e-2
+    greater = (z.float() > z.float().gather(1, lab[:, None])).sum(1)
+    assert torch.equal(corr.bool(), greater < 1)
+    assert abs(float(sums[0]) - float(loss.mean())) < 1e-3
+    assert abs(float(sums[1]) - float((greater < 1).float().mean())) < 1e-6
+    assert bool(corr[1])
+
+
+def test_bias_act_dropout():
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(3)
+    x = torch.randn(512, 200, device="cuda")
+    b = torch.randn(200, device="cuda")
+    for act, fn in [(K.ACT_ELU, F.elu), (K.ACT_RELU, F.relu), (K.ACT_GELU, lambda t: F.gelu(t, approximate="tanh"))]:
+        y = K.bias_act_dropout(x, b, act)
+        assert _rel(y, fn(x + b)) < 1e-5
+        xr = x.clone().requires_grad_(True)
+        fn(xr + b).backward(torch.ones_like(x))
+        dx = K.bias_act_dropout_bwd(torch.ones_like(x), x, b, act)
+        assert _rel(dx, xr.grad) < 1e-4
+    y = K.bias_act_dropout(torch.ones(1 << 20, 8, device="cuda"), None, K.ACT_NONE, rate=0.25, seed=7, offset=3)
+    keep = (y != 0).float().mean().item()
+    assert abs(keep - 0.75) < 0.005
+    assert torch.allclose(y[y != 0], torch.full_like(y[y != 0], 1 / 0.75))
+    g = K.bias_act_dropout_bwd(torch.ones_like(y), torch.ones_like(y), None, K.ACT_NONE, rate=0.25, seed=7, offset=3)
+    assert torch.equal(g, y)
+
+
+def test_fp8_roundtrip():
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    x = (torch.randn(4096, device="cuda") * 3).bfloat16()
+    am = K.amax(x)
+    assert abs(float(am) - float(x.float().abs().max())) < 1e-6
+    scale = (448.0 / am).float()
+    q = K.quant_fp8(x, scale)
+    xd = K.dequant_fp8(q, scale)
+    assert _rel(xd, x) < 0.05
+    ref = (x.float() * scale).to(torch.float8_e4m3fn)
+    assert torch.equal(q, ref.view(torch.uint8))
+
+
+def test_flat_optimizers_match_cpu():
+    from tensorflow_train_distributed_amd.train.flat import FlatParams, ParamSpec, FlatSGD, FlatAdam, FlatLAMB, Schedule
+    torch.manual_seed(4)
+    specs = [ParamSpec("a/kernel", (300, 70), lambda t, g: t.normal_(generator=g)),
+             ParamSpec("a/bias", (70,), lambda t, g: t.normal_(generator=g), weight_decay=False),
+             ParamSpec("b/kernel", (40000,), lambda t, g: t.normal_(generator=g))]
+    for idx, make in enumerate([lambda p: FlatSGD(p, Schedule(kind=1, base_lr=0.1, decay_steps=2, decay_rate=0.5, staircase=True),
+                                   momentum=0.9, weight_decay=0.01),
+                 lambda p: FlatSGD(p, Schedule(base_lr=0.05)),
+                 lambda p: FlatAdam(p, Schedule(base_lr=1e-3), weight_decay=0.01, max_grad_norm=1.0),
+                 lambda p: FlatAdam(p, Schedule(base_lr=1e-3), weight_decay=0.01, decoupled=True),
+                 lambda p: FlatLAMB(p, Schedule(kind=2, base_lr=1e-2, warmup_steps=2, total_steps=10),
+                                    weight_decay=0.01)]):
+        pc = FlatParams(specs, "cpu", compute_dtype=None, seed=5)
+        pg = FlatParams(specs, "cuda", seed=5)
+        oc, og = make(pc), make(pg)
+        for it in range(4):
+            gr = torch.randn(pc.numel)
+            pc.grad.copy_(gr)
+            pg.grad.copy_(gr)
+            oc.step()
+            og.step()
+        d = (pg.master.cpu() - pc.master).abs()
+        assert _rel(pg.master.cpu(), pc.master) < 1e-5, (idx, int(d.argmax()), float(d.max()))
+        assert _rel(pg.compute.float().cpu(), pc.master) < 1e-2
