@@ -234,21 +234,30 @@ class ResNet:
         return sums
 
     # ----------------------------------------------------------------- reference (CPU / oracle)
-    def reference_loss(self, images, labels, params=None):
+    def reference_loss(self, images, labels, params=None, bf16_activations=False):
         """fp32 PyTorch implementation of the same network (NCHW internally), used on CPU and
         as the numerics oracle for the GPU engine. Returns (loss, accuracy, logits); BN uses
-        batch statistics (training mode) and does not touch the moving averages."""
+        batch statistics (training mode) and does not touch the moving averages.
+
+        bf16_activations=True rounds every tensor the GPU engine stores in bf16 (conv outputs,
+        unit outputs, pooled features, logits) with a straight-through estimator, so the
+        oracle follows the engine's rounding points and only accumulation order differs."""
         P = params if params is not None else {n: self.params.var[n] for n in self.params.names()}
         x = images.float().permute(0, 3, 1, 2)
 
+        def rnd(t):
+            if not bf16_activations:
+                return t
+            return t + (t.to(torch.bfloat16).float() - t).detach()
+
         def convbn(c, t, relu, res=None):
             w = P[c.name + "_conv/kernel"][..., :t.shape[1]].permute(0, 3, 1, 2)
-            y = F.conv2d(t, w, stride=c.stride, padding=c.pad)
+            y = rnd(F.conv2d(t, w, stride=c.stride, padding=c.pad))
             y = F.batch_norm(y, None, None, P[c.name + "_bn/gamma"], P[c.name + "_bn/beta"], training=True,
                              eps=self.bn_eps)
             if res is not None:
                 y = y + res
-            return F.relu(y) if relu else y
+            return rnd(F.relu(y) if relu else y)
 
         h = convbn(self.stem, x, True)
         h = F.max_pool2d(h, 3, 2, 1)
@@ -257,8 +266,8 @@ class ResNet:
             o = convbn(blk["c2"], o, True)
             sc = convbn(blk["cd"], h, False) if blk["cd"] is not None else h
             h = convbn(blk["c3"], o, True, sc)
-        pooled = h.mean((2, 3))
-        logits = pooled @ P["predictions/kernel"] + P["predictions/bias"]
+        pooled = rnd(h.mean((2, 3)))
+        logits = rnd(pooled @ P["predictions/kernel"] + P["predictions/bias"])
         loss = F.cross_entropy(logits, labels.long())
         acc = (logits.argmax(1) == labels.long()).float().mean()
         return loss, acc, logits

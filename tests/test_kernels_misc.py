@@ -136,8 +136,12 @@ def test_flat_optimizers_match_cpu():
         pc = FlatParams(specs, "cpu", compute_dtype=None, seed=5)
         pg = FlatParams(specs, "cuda", seed=5)
         oc, og = make(pc), make(pg)
+        valid = torch.zeros(pc.numel, dtype=torch.bool)
+        for sp in specs:
+            o = pc.offsets[sp.name]
+            valid[o:o + int(torch.tensor(sp.shape).prod())] = True
         for it in range(4):
-            gr = torch.randn(pc.numel)
+            gr = torch.randn(pc.numel) * valid  # padding between variables never carries gradient
             pc.grad.copy_(gr)
             pg.grad.copy_(gr)
             oc.step()
@@ -145,3 +149,18 @@ def test_flat_optimizers_match_cpu():
         d = (pg.master.cpu() - pc.master).abs()
         assert _rel(pg.master.cpu(), pc.master) < 1e-5, (idx, int(d.argmax()), float(d.max()))
         assert _rel(pg.compute.float().cpu(), pc.master) < 1e-2
+
+
+def test_colsum_and_dgrad_accumulate():
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(6)
+    x = torch.randn(1000, 100, device="cuda").bfloat16()
+    assert _rel(K.colsum(x), x.float().sum(0)) < 1e-4
+    dy = torch.randn(2, 8, 8, 64, device="cuda").bfloat16()
+    w = (torch.randn(64, 3, 3, 32, device="cuda") / 24).bfloat16()
+    base = torch.randn(2, 8, 8, 32, device="cuda").bfloat16()
+    ref = G.conv_dgrad(dy, w.permute(3, 1, 2, 0).contiguous(), (2, 8, 8, 32), (1, 1), (1, 1)).float() + base.float()
+    out = base.clone()
+    G.conv_dgrad(dy, w.permute(3, 1, 2, 0).contiguous(), (2, 8, 8, 32), (1, 1), (1, 1), out=out, beta=1)
+    assert _rel(out, ref) < 1e-2

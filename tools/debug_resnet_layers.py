@@ -1,0 +1,95 @@
+"""Layer-by-layer comparison of the ResNet GPU engine vs the fp32 reference (debug aid)."""
+import torch
+import torch.nn.functional as F
+from tensorflow_train_distributed_amd.models.resnet import resnet50
+from tensorflow_train_distributed_amd.ops import kernels as K
+
+torch.manual_seed(0)
+m = resnet50(num_classes=100, device="cuda", seed=3)
+P = m.params
+x = torch.randn(8, 64, 64, 3, device="cuda").bfloat16()
+
+def rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-20))
+
+def ref_convbn(c, t_nhwc, relu, res=None):
+    t = t_nhwc.float().permute(0, 3, 1, 2)
+    w = P.c[c.name + "_conv/kernel"].float()[..., :t.shape[1]].permute(0, 3, 1, 2)
+    y = F.conv2d(t, w, stride=c.stride, padding=c.pad)
+    y = F.batch_norm(y, None, None, P.var[c.name + "_bn/gamma"], P.var[c.name + "_bn/beta"], training=True, eps=1e-5)
+    if res is not None:
+        y = y + res.float().permute(0, 3, 1, 2)
+    y = F.relu(y) if relu else y
+    return y.permute(0, 2, 3, 1)
+
+xin = K.pad_channels(x, 8)
+o, ctx = m._convbn_fwd(m.stem, xin, True)
+print("stem", rel(o, ref_convbn(m.stem, x, True)))
+y_conv = ctx[1]
+w = P.c["conv1_conv/kernel"].float()[..., :3].permute(0, 3, 1, 2)
+yr = F.conv2d(x.float().permute(0, 3, 1, 2), w, stride=2, padding=3).permute(0, 2, 3, 1)
+print("stem conv only", rel(y_conv, yr))
+h, arg = K.maxpool_fwd(o, 3, 2, 1)
+for i, blk in enumerate(m.blocks):
+    o1, _ = m._convbn_fwd(blk["c1"], h, True)
+    e1 = rel(o1, ref_convbn(blk["c1"], h, True))
+    o2, _ = m._convbn_fwd(blk["c2"], o1, True)
+    e2 = rel(o2, ref_convbn(blk["c2"], o1, True))
+    if blk["cd"] is not None:
+        sc, _ = m._convbn_fwd(blk["cd"], h, False)
+        ed = rel(sc, ref_convbn(blk["cd"], h, False))
+    else:
+        sc, ed = h, 0.0
+    o3, _ = m._convbn_fwd(blk["c3"], o2, True, residual=sc)
+    e3 = rel(o3, ref_convbn(blk["c3"], o2, True, res=sc))
+    print("block", i, tuple(h.shape), "c1 %.4f c2 %.4f cd %.4f c3 %.4f" % (e1, e2, ed, e3))
+    h = o3
+
+# ---------------- block-level backward check (engine inputs, fp32 autograd reference)
+print("backward:")
+h, arg = K.maxpool_fwd(o, 3, 2, 1)
+for i, blk in enumerate(m.blocks[:5] + [None] + m.blocks[13:15]):
+    if blk is None:
+        h = torch.randn(8, 4, 4, 1024, device="cuda").bfloat16()
+        continue
+    # engine forward/backward of one block
+    o1, c1 = m._convbn_fwd(blk["c1"], h, True)
+    o2, c2 = m._convbn_fwd(blk["c2"], o1, True)
+    if blk["cd"] is not None:
+        sc, cd = m._convbn_fwd(blk["cd"], h, False)
+    else:
+        sc, cd = h, None
+    o3, c3 = m._convbn_fwd(blk["c3"], o2, True, residual=sc)
+    dout = torch.randn_like(o3)
+    m._grad_hook = None
+    g_sc = torch.empty_like(dout)
+    d2 = m._convbn_bwd(blk["c3"], dout, c3, g_out=g_sc)
+    d1 = m._convbn_bwd(blk["c2"], d2, c2)
+    dx = m._convbn_bwd(blk["cd"], g_sc, cd) if blk["cd"] is not None else g_sc
+    dh = m._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1)
+    # reference
+    names = [blk[k].name for k in ("c1", "c2", "c3", "cd") if blk[k] is not None]
+    leaves = {}
+    for n in names:
+        for suf in ("_conv/kernel", "_bn/gamma", "_bn/beta"):
+            leaves[n + suf] = (P.c[n + suf].float() if suf == "_conv/kernel" else P.var[n + suf]).clone().requires_grad_(True)
+    hr = h.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    def cbr(c, t, relu, res=None):
+        w = leaves[c.name + "_conv/kernel"].permute(0, 3, 1, 2)
+        y = F.conv2d(t, w, stride=c.stride, padding=c.pad)
+        y = F.batch_norm(y, None, None, leaves[c.name + "_bn/gamma"], leaves[c.name + "_bn/beta"], training=True, eps=1e-5)
+        if res is not None:
+            y = y + res
+        return F.relu(y) if relu else y
+    r1 = cbr(blk["c1"], hr, True)
+    r2 = cbr(blk["c2"], r1, True)
+    rs = cbr(blk["cd"], hr, False) if blk["cd"] is not None else hr
+    r3 = cbr(blk["c3"], r2, True, rs)
+    r3.backward(dout.float().permute(0, 3, 1, 2))
+    errs = ["dx %.4f" % rel(dh, hr.grad.permute(0, 2, 3, 1))]
+    for n in names:
+        errs.append("%s dw %.4f dg %.4f db %.4f" % (n[-3:], rel(P.g[n + "_conv/kernel"], leaves[n + "_conv/kernel"].grad),
+                                                 rel(P.g[n + "_bn/gamma"], leaves[n + "_bn/gamma"].grad),
+                                                 rel(P.g[n + "_bn/beta"], leaves[n + "_bn/beta"].grad)))
+    print("block", i, tuple(h.shape), " | ".join(errs))
+    h = o3
