@@ -355,8 +355,10 @@ __device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
 }
 
 template <int BM, int BN>
-__device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM / 32][BN / 32], int n0, int mwave,
-                                         int nwave, int lane, int M, int N, int split, int tile_m, char* smem) {
+__device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM / 32][BN / 32], int m0, int n0,
+                                         int mwave, int nwave, int lane, int M, int N, int split, int tile_m,
+                                         char* smem) {
+  static_assert(BM * (BN * 2 + 16) + 4 * 2 * BN * 4 <= 2 * (BM + BN) * BK * 2, "staged epilogue must fit in LDS");
   constexpr int TM = BM / 32, TN = BN / 32;
   const int g = lane >> 4, i16 = lane & 15;
   if (E.mode != 0) {
@@ -382,111 +384,124 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
     }
     return;
   }
-  bf16_t* out = static_cast<bf16_t*>(E.out);
-  float csum[TN][4], csq[TN][4];
+  // ---- bf16 output: stage the tile through LDS (the K loop ended on a barrier, so the
+  // operand buffers are free), then every thread stores whole 16-B chunks of full rows:
+  // one wave-instruction writes 4 x 256 contiguous bytes instead of 16 x 32-B segments.
+  constexpr int PITCH = BN * 2 + 16;  // 16-B aligned rows; +16 B breaks the bank period
+  const int tid = threadIdx.x;
 #pragma unroll
-  for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) csum[tn][j] = csq[tn][j] = 0.f;
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
-    const int m = mwave + tm * 16 + i16;
-    const bool mok = m < M;
-    const long long orow = mok ? out_row(E, m) : 0;
+  for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      const int n = nwave + tn * 16 + 4 * g;
-      float v[4];
+      const int r = mwave - m0 + tm * 16 + i16, c = nwave - n0 + tn * 16 + 4 * g;
+      const f32x4_t v = acc[tm][tn] * E.alpha;
+      uint2 w;
+      w.x = pack_bf16x2(v[0], v[1]);
+      w.y = pack_bf16x2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) = w;
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;       // 16-B chunks per row
+  constexpr int RPP = NTHR / CPR;   // rows per pass
+  const int c = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + c * 8;
+  const bool nfull = n + 8 <= N;
+  const bool vst = nfull && (E.ldo & 7) == 0;
+  const bool vres = nfull && (E.ldr & 7) == 0;
+  bf16_t* out = static_cast<bf16_t*>(E.out);
+  float bias8[8], s8[8], q8[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[tm][tn][j] * E.alpha;
-      if (!mok) continue;
-      if (E.bias) {
+  for (int j = 0; j < 8; ++j) {
+    bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
+    s8[j] = q8[j] = 0.f;
+  }
+  for (int r = r0; r < BM; r += RPP) {
+    const int m = m0 + r;
+    if (m >= M || n >= N) break;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16), f);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += (n + j < N) ? E.bias[n + j] : 0.f;
-      }
-      const bool full = n + 3 < N && (E.ldo & 3) == 0 && (E.ldr & 3) == 0;
-      if (E.residual) {
-        const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
-        if (full) {
-          const uint2 rv = *reinterpret_cast<const uint2*>(rp);
-          v[0] += __uint_as_float(rv.x << 16);
-          v[1] += __uint_as_float(rv.x & 0xffff0000u);
-          v[2] += __uint_as_float(rv.y << 16);
-          v[3] += __uint_as_float(rv.y & 0xffff0000u);
-        } else {
-          #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (n + j < N) v[j] += bf2f(rp[j]);
-        }
-      }
-      bf16_t* op = out + orow * E.ldo + n;
-      if (E.beta) {
-        if (full) {
-          const uint2 ov = *reinterpret_cast<const uint2*>(op);
-          v[0] += __uint_as_float(ov.x << 16);
-          v[1] += __uint_as_float(ov.x & 0xffff0000u);
-          v[2] += __uint_as_float(ov.y << 16);
-          v[3] += __uint_as_float(ov.y & 0xffff0000u);
-        } else {
-          #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (n + j < N) v[j] += bf2f(op[j]);
-        }
-      }
-      if (E.act == kActRelu) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-      } else if (E.act == kActGelu) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
-      }
-      if (full) {
-        uint2 w;
-        w.x = pack_bf16x2(v[0], v[1]);
-        w.y = pack_bf16x2(v[2], v[3]);
-        *reinterpret_cast<uint2*>(op) = w;
+    for (int j = 0; j < 8; ++j) f[j] += bias8[j];
+    if (E.residual) {
+      const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
+      float rv[8];
+      if (vres) {
+        unpack8(*reinterpret_cast<const uint4*>(rp), rv);
       } else {
-        #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (n + j < N) op[j] = f2bf(v[j]);
-      }
-      if (E.stat) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float b = bf2f(f2bf(v[j]));  // stats of the values actually stored
-          csum[tn][j] += b;
-          csq[tn][j] += b * b;
-        }
+        for (int j = 0; j < 8; ++j) rv[j] = n + j < N ? bf2f(rp[j]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += rv[j];
+    }
+    bf16_t* op = out + out_row(E, m) * E.ldo + n;
+    if (E.beta) {
+      float ov[8];
+      if (vst) {
+        unpack8(*reinterpret_cast<const uint4*>(op), ov);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ov[j] = n + j < N ? bf2f(op[j]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += ov[j];
+    }
+    if (E.act == kActRelu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    } else if (E.act == kActGelu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
+    }
+    const uint4 packed = pack8(f);
+    if (vst) {
+      *reinterpret_cast<uint4*>(op) = packed;
+    } else {
+      const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (n + j < N) op[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+    }
+    if (E.stat) {
+      float sv[8];
+      unpack8(packed, sv);  // statistics of the values actually stored
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s8[j] += sv[j];
+        q8[j] += sv[j] * sv[j];
       }
     }
   }
   if (E.stat) {
-    // reduce over the 16 rows held by lanes with equal g, then over the two m-waves via LDS.
-    float* red = reinterpret_cast<float*>(smem);  // [2 (wm)][2][BN]
-    const int wm = (threadIdx.x >> 6) >> 1;
-    __syncthreads();
+    // lanes sharing a chunk column: lane % CPR equal -> reduce over the wave, then over 4 waves.
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
+    for (int j = 0; j < 8; ++j) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float s = csum[tn][j], q = csq[tn][j];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s += __shfl_xor(s, o, 64);
-          q += __shfl_xor(q, o, 64);
-        }
-        if (i16 == 0) {
-          const int col = nwave - n0 + tn * 16 + 4 * g + j;  // column within the block tile
-          red[(wm * 2 + 0) * BN + col] = s;
-          red[(wm * 2 + 1) * BN + col] = q;
-        }
+      for (int o = CPR; o < 64; o <<= 1) {
+        s8[j] += __shfl_xor(s8[j], o, 64);
+        q8[j] += __shfl_xor(q8[j], o, 64);
       }
+    }
+    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [4 waves][2][BN]
+    const int w = tid >> 6;
+    if ((tid & 63) < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(w * 2 + 0) * BN + c * 8 + j] = s8[j];
+        red[(w * 2 + 1) * BN + c * 8 + j] = q8[j];
+      }
+    }
     __syncthreads();
-    for (int t = threadIdx.x; t < BN; t += NTHR) {
-      const int n = n0 + t;
-      if (n < N) {
-        E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n] = red[0 * BN + t] + red[2 * BN + t];
-        E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n] = red[1 * BN + t] + red[3 * BN + t];
+    for (int t = tid; t < BN; t += NTHR) {
+      if (n0 + t < N) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          ss += red[(k * 2 + 0) * BN + t];
+          qq += red[(k * 2 + 1) * BN + t];
+        }
+        E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t] = ss;
+        E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t] = qq;
       }
     }
   }
@@ -562,26 +577,50 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, t
     __syncthreads();
     cur ^= 1;
   }
-  epilogue<BM, BN>(pe, acc, n0, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane, M, N, blockIdx.y, tile_m, smem);
+  epilogue<BM, BN>(pe, acc, m0, n0, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane, M, N, blockIdx.y, tile_m, smem);
 }
 
-// Sums split-K fp32 slabs: out[i] = sum_s ws[s*n + i] (+ out[i] if beta), optional bf16 copy.
+// Sums split-K fp32 slabs: out[i] (+)= sum_s ws[s*n + i]. grid.y groups slabs by 8 so even a
+// small output (a few K elements) gets enough threads in flight; with >1 group the partial
+// sums land with float atomics into a pre-zeroed (or beta-preloaded) output.
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long n, float* __restrict__ out,
-                                     int beta) {
+                                     int beta, int per_group, int atomic) {
   const long long i4 = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
   if (i4 >= n) return;
+  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
   if (i4 + 3 < n) {
-    f32x4_t s = *reinterpret_cast<const f32x4_t*>(ws + i4);
-    for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4_t*>(ws + k * n + i4);
-    if (beta) s += *reinterpret_cast<const f32x4_t*>(out + i4);
-    *reinterpret_cast<f32x4_t*>(out + i4) = s;
+    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = s0; k < s1; ++k) s += *reinterpret_cast<const f32x4_t*>(ws + k * n + i4);
+    if (atomic) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(out + i4 + j, s[j]);
+    } else {
+      if (beta) s += *reinterpret_cast<const f32x4_t*>(out + i4);
+      *reinterpret_cast<f32x4_t*>(out + i4) = s;
+    }
   } else {
     for (long long i = i4; i < n; ++i) {
-      float s = 0.f;
-      for (int k = 0; k < splits; ++k) s += ws[k * n + i];
-      out[i] = s + (beta ? out[i] : 0.f);
+      float t = 0.f;
+      for (int k = s0; k < s1; ++k) t += ws[k * n + i];
+      if (atomic)
+        atomicAdd(out + i, t);
+      else
+        out[i] = t + (beta ? out[i] : 0.f);
     }
   }
+}
+
+hipError_t splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {
+  const int per_group = 8;
+  const int groups = (splits + per_group - 1) / per_group;
+  const int atomic = groups > 1;
+  if (atomic && !beta) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * n, st);
+    if (e != hipSuccess) return e;
+  }
+  dim3 grid(ceil_div((n + 3) / 4, 256), groups);
+  hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, ws, splits, n, out, beta, per_group, atomic);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ host-side dispatch
@@ -793,12 +832,9 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
     e = dispatch<MNDense, MNConvGather>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
   }
   if (e != hipSuccess || splits == 1) return e;
-  const long long n = static_cast<long long>(M) * N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ceil_div((n + 3) / 4, 256)), dim3(256), 0, st, ws, splits, n, dw, beta);
-  return hipGetLastError();
+  return splitk_reduce(ws, splits, static_cast<long long>(M) * N, dw, beta, st);
 }
 
 TTDK_EXPORT int ttdk_splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ceil_div((n + 3) / 4, 256)), dim3(256), 0, st, ws, splits, n, out, beta);
-  return hipGetLastError();
+  return splitk_reduce(ws, splits, n, out, beta, st);
 }

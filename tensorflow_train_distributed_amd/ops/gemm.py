@@ -14,6 +14,23 @@ from . import _lib
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
+# Optional launch log (kind, M, N, K, splits) for matching rocprofv3 dispatches to layer
+# shapes: enable with TTD_GEMM_LOG=1, read/reset via gemm_log().
+import os as _os
+_LOG = [] if _os.environ.get("TTD_GEMM_LOG") else None
+
+
+def gemm_log(reset=False):
+    out = list(_LOG or [])
+    if reset and _LOG is not None:
+        _LOG.clear()
+    return out
+
+
+def _log(kind, M, N, K, splits=1):
+    if _LOG is not None:
+        _LOG.append((kind, int(M), int(N), int(K), int(splits)))
+
 
 def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,
          slab_stride=0):
@@ -61,6 +78,7 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
         raise ValueError("gemm inner dims differ: %d vs %d" % (K, Kb))
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    _log("gemm_%s%s" % ("t" if trans_a else "n", "t" if trans_b else "n"), M, N, K, splits)
     a_kmajor = 0 if trans_a else 1
     lda = M if trans_a else K
     b_kmajor = 1 if trans_b else 0
@@ -107,6 +125,7 @@ def conv_fwd(x, w, stride=(1, 1), padding=(0, 0), *, out=None, residual=None, ac
     g = conv_geom(x.shape, w.shape, stride, padding)
     if out is None:
         out = torch.empty((g.N, g.P, g.Q, g.K), dtype=torch.bfloat16, device=x.device)
+    _log("fwd_%dx%d_s%d" % (g.R, g.S, g.sh), g.N * g.P * g.Q, g.K, g.R * g.S * g.C)
     e = _epi(out, ldo=g.K, bias=bias, residual=residual, act=act, stat=stat)
     _lib.call("ttdk_conv_fwd", x.data_ptr(), w.data_ptr(), ctypes.byref(g), tile[0], tile[1], ctypes.byref(e),
               _lib.stream())
@@ -128,17 +147,22 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     if out is None:
         alloc = torch.zeros if (strided_pw and not beta) else torch.empty
         out = alloc(tuple(x_shape), dtype=torch.bfloat16, device=dy.device)
+    _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * (g.P * g.Q if strided_pw else g.H * g.W), C, R * S * K)
     e = _epi(out, ldo=C, beta=beta, residual=residual)
     _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), tile[0], tile[1], ctypes.byref(e),
               _lib.stream())
     return out
 
 
-def wgrad_splits(g, bm=128, bn=128, target_blocks=1024):
+def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
+    """Split-K factor for the weight gradient: enough blocks to fill 256 CUs twice, but every
+    split keeps >= min_ktiles K-steps (the slab write + reduce is pure overhead)."""
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
+    bm = 64 if M <= 64 else 128
+    bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
     ktiles = -(-K // 64)
-    s = max(1, min(ktiles // 4, -(-target_blocks // tiles)))
+    s = max(1, min(ktiles // min_ktiles, -(-target_blocks // tiles)))
     return s
 
 
@@ -152,6 +176,7 @@ def conv_wgrad(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=
         out = torch.empty(tuple(w_shape), dtype=torch.float32, device=x.device)
     if splits is None:
         splits = wgrad_splits(g)
+    _log("wgrad_%dx%d_s%d" % (g.R, g.S, g.sh), g.K, g.R * g.S * g.C, g.N * g.P * g.Q, splits)
     ws = None
     if splits > 1:
         ws = torch.empty((splits,) + tuple(w_shape), dtype=torch.float32, device=x.device)
