@@ -102,6 +102,18 @@ class FlatParams:
     def zero_grad(self):
         self.grad.zero_()
 
+    def valid_mask(self):
+        """1.0 on trainable variable elements, 0.0 on alignment padding / non-trainables."""
+        m = getattr(self, "_valid", None)
+        if m is None:
+            m = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+            for s in self.specs:
+                if s.trainable:
+                    o = self.offsets[s.name]
+                    m[o:o + (int(np.prod(s.shape)) if len(s.shape) else 1)] = 1.0
+            self._valid = m
+        return m
+
     def chunk_table(self):
         """Device tensors (chunks, seg_wd_mask) for the optim.hip kernels."""
         if self._chunks is None:
@@ -242,10 +254,13 @@ class FlatOptimizer:
         if increment:
             self._host_step += 1
 
+    def _masked_grad(self):
+        return self.p.grad * self.p.valid_mask()
+
     def _clip_scale_cpu(self):
         gs = float(self.hyper[H_GRADSCALE])
         if self.max_grad_norm > 0:
-            n = float(self.p.grad.norm()) * gs
+            n = float(self._masked_grad().norm()) * gs
             if n > self.max_grad_norm:
                 gs *= self.max_grad_norm / n
         return gs
@@ -278,7 +293,7 @@ class FlatSGD(FlatOptimizer):
             return
         with torch.no_grad():
             lr = float(self.hyper[H_LR])
-            g = self.p.grad * self._clip_scale_cpu()
+            g = self._masked_grad() * self._clip_scale_cpu()
             if self.weight_decay:
                 g = g + self._wd_vector() * self.p.master
             if self.mom is None:
@@ -321,7 +336,7 @@ class FlatAdam(FlatOptimizer):
         with torch.no_grad():
             lr = float(self.hyper[H_LR])
             bc1, bc2 = float(self.hyper[H_BC1]), float(self.hyper[H_BC2])
-            g = self.p.grad * self._clip_scale_cpu()
+            g = self._masked_grad() * self._clip_scale_cpu()
             wdv = FlatSGD._wd_vector(self) if self.weight_decay else None
             if wdv is not None and not self.decoupled:
                 g = g + wdv * self.p.master
@@ -361,7 +376,7 @@ class FlatLAMB(FlatOptimizer):
         with torch.no_grad():
             lr = float(self.hyper[H_LR])
             bc1, bc2 = float(self.hyper[H_BC1]), float(self.hyper[H_BC2])
-            g = self.p.grad * self._clip_scale_cpu()
+            g = self._masked_grad() * self._clip_scale_cpu()
             self.m.mul_(self.beta1).add_((1 - self.beta1) * g)
             self.v.mul_(self.beta2).add_((1 - self.beta2) * g * g)
             u = (self.m / bc1) / ((self.v / bc2).sqrt() + self.eps)
