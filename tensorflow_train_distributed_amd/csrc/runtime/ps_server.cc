@@ -552,6 +552,7 @@ class Server {
           int nd = ttd_bundle_reader_entry(r, key.c_str(), &dt, shape, &nb, nullptr, nullptr, nullptr);
           if (nd < 0) continue;
           if (key == "global_step") {
+            if (task_ != 0) continue;  // the global step lives on ps task 0
             int64_t gs = 0;
             if (ttd_bundle_reader_read(r, key.c_str(), &gs, 8) == 0) global_step_ = gs;
             ++restored;
