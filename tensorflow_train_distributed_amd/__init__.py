@@ -4,6 +4,16 @@ Capabilities of boyuanf/tensorflow_train_distributed (a TF1 parameter-server tra
 /root/reference/distribute_training.py) re-designed for AMD Instinct MI355X (gfx950):
 PyTorch-ROCm tensors, hand-written CDNA4 HIP kernels, RCCL collectives over xGMI, a native
 C++ runtime (parameter server, checkpoint/event IO, data prefetch) and a
-tf.distribute/tf.train-shaped public API.
+tf.distribute/tf.train-shaped public API:
+
+    import tensorflow_train_distributed_amd as ttd
+    ttd.train.MonitoredTrainingSession / ttd.train.SyncReplicasOptimizer / ttd.train.Server
+    ttd.distribute.MirroredStrategy / MultiWorkerMirroredStrategy / ParameterServerStrategy
+    ttd.train.Checkpoint / CheckpointManager (TensorBundle V2 on disk)
 """
 __version__ = "0.1.0"
+
+from . import data, distribute, models, parallel, summary, train  # noqa: E402
+from .parallel.ps import device  # noqa: E402
+from .utils import app, errors, flags  # noqa: E402
+from .train.graph import placeholder  # noqa: E402

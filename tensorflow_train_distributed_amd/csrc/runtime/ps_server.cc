@@ -74,6 +74,7 @@ enum Op : uint32_t {
   kShutdown = 17,
   kListVars = 18,
   kStats = 19,
+  kCounterAdd = 20,
 };
 
 enum Status : uint32_t { kOk = 0, kErr = 1, kClosed = 2, kNotFound = 3, kShuttingDown = 4 };
@@ -582,6 +583,15 @@ class Server {
         }
         return kOk;
       }
+      case kCounterAdd: {  // named int64 counters (e.g. "workers_done" for coordinated shutdown)
+        std::string name = b.str();
+        int64_t d = b.get<int64_t>();
+        if (!b.ok) return kErr;
+        std::lock_guard<std::mutex> lk(vars_mu_);
+        const int64_t v = (counters_[name] += d);
+        put<int64_t>(out, v);
+        return kOk;
+      }
       case kStats: {
         int64_t dropped = 0, step = -1;
         std::lock_guard<std::mutex> lk(vars_mu_);
@@ -624,6 +634,7 @@ class Server {
   std::atomic<bool> ready_{false};
   std::atomic<int64_t> generation_{0};
   std::atomic<int64_t> global_step_{0};
+  std::map<std::string, int64_t> counters_;
 
   std::mutex q_mu_;
   std::condition_variable q_cv_;

@@ -30,7 +30,7 @@ from .cluster import ClusterSpec, split_address
 # wire ops (must match ps_server.cc)
 OP_PING, OP_INIT, OP_IS_READY, OP_SET_READY, OP_PULL, OP_APPLY_GD, OP_ACCUM_APPLY, OP_TAKE_APPLY = 1, 2, 3, 4, 5, 6, 7, 8
 OP_DEQUEUE, OP_ENQUEUE, OP_CLOSE_QUEUE, OP_GET_GS, OP_SET_GS, OP_SET_ACCUM_STEP = 9, 10, 11, 12, 13, 14
-OP_SAVE, OP_RESTORE, OP_SHUTDOWN, OP_LIST, OP_STATS = 15, 16, 17, 18, 19
+OP_SAVE, OP_RESTORE, OP_SHUTDOWN, OP_LIST, OP_STATS, OP_COUNTER_ADD = 15, 16, 17, 18, 19, 20
 ST_OK, ST_ERR, ST_CLOSED, ST_NOT_FOUND, ST_SHUTTING_DOWN = 0, 1, 2, 3, 4
 
 DT_FLOAT, DT_INT64 = 1, 9
@@ -194,16 +194,19 @@ class PSClient:
         self.conns = [PSConnection(a, connect_timeout) for a in cluster.job_tasks("ps")]
         # blocking ops (token dequeue / take) get their own connections so heartbeats and
         # other calls are not stuck behind them
-        self._blocking: Dict[int, PSConnection] = {}
+        self._blocking: Dict[tuple, PSConnection] = {}
         self.by_task: List[List[str]] = [[] for _ in range(self.n_ps)]
         for n, t in self.placement.items():
             self.by_task[t].append(n)
 
-    def blocking_conn(self, task: int) -> PSConnection:
-        c = self._blocking.get(task)
+    def blocking_conn(self, task: int, purpose: str = "dequeue") -> PSConnection:
+        """Dedicated connection per (task, purpose): a worker blocked in the token dequeue
+        must not hold the connection the chief's queue-runner thread takes through."""
+        key = (task, purpose)
+        c = self._blocking.get(key)
         if c is None:
             c = PSConnection(self.cluster.task_address("ps", task), self._connect_timeout)
-            self._blocking[task] = c
+            self._blocking[key] = c
         return c
 
     def close(self):
@@ -309,7 +312,7 @@ class PSClient:
         def run(t):
             try:
                 names = by_task[t]
-                _check(*self.blocking_conn(t).call(OP_TAKE_APPLY, [struct.pack("<IfBII", num_required, lr, 0, 0,
+                _check(*self.blocking_conn(t, "take").call(OP_TAKE_APPLY, [struct.pack("<IfBII", num_required, lr, 0, 0,
                                                                                len(names))] +
                                                    [_name(n) for n in names], timeout_ms=0), "take_apply")
             except Exception as e:  # noqa: BLE001
@@ -323,7 +326,7 @@ class PSClient:
         if errs:
             raise errs[0]
         names = by_task[0]
-        body = _check(*self.blocking_conn(0).call(OP_TAKE_APPLY, [struct.pack("<IfBII", num_required, lr, 1,
+        body = _check(*self.blocking_conn(0, "take").call(OP_TAKE_APPLY, [struct.pack("<IfBII", num_required, lr, 1,
                                                                               tokens_per_step, len(names))] +
                                                   [_name(n) for n in names], timeout_ms=0), "take_apply")
         return struct.unpack("<q", body)[0]
@@ -347,6 +350,12 @@ class PSClient:
     def set_accum_step(self, v: int):
         for c in self.conns:
             _check(*c.call(OP_SET_ACCUM_STEP, [struct.pack("<q", int(v))]), "set_accum_step")
+
+    def counter_add(self, name: str, delta: int = 1, task: int = 0) -> int:
+        """Atomically add to a named int64 counter on a PS task; returns the new value."""
+        return struct.unpack("<q", _check(*self.conns[task].call(OP_COUNTER_ADD, [_name(name) +
+                                                                                  struct.pack("<q", delta)]),
+                                           "counter_add"))[0]
 
     def stats(self, task: int = 0) -> dict:
         d, s, q = struct.unpack("<qqq", _check(*self.conns[task].call(OP_STATS), "stats"))

@@ -1,1 +1,2 @@
-
+"""Utilities: flags/app, errors, protobuf helpers, event files, hipGraph capture, tracing."""
+from . import errors, flags
