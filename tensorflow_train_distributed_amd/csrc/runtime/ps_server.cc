@@ -746,6 +746,13 @@ TTD_EXPORT int ttd_ps_client_call(void* h, uint32_t op, int nseg, const void* co
 
 TTD_EXPORT const void* ttd_ps_client_resp(void* h) { return static_cast<Client*>(h)->resp.data(); }
 TTD_EXPORT uint64_t ttd_ps_client_resp_len(void* h) { return static_cast<Client*>(h)->resp.size(); }
+// Unblocks a call in progress on another thread (no lock): the peer read fails and the
+// blocked ttd_ps_client_call returns -1. Used to cancel blocking takes/dequeues at shutdown.
+TTD_EXPORT void ttd_ps_client_abort(void* h) {
+  auto* c = static_cast<Client*>(h);
+  if (c) ::shutdown(c->fd, SHUT_RDWR);
+}
+
 TTD_EXPORT void ttd_ps_client_close(void* h) {
   auto* c = static_cast<Client*>(h);
   if (!c) return;

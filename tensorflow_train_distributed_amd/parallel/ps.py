@@ -56,6 +56,7 @@ def _lib():
         lib.ttd_ps_client_resp_len.restype = ctypes.c_uint64
         lib.ttd_ps_client_resp_len.argtypes = [vp]
         lib.ttd_ps_client_close.argtypes = [vp]
+        lib.ttd_ps_client_abort.argtypes = [vp]
         lib._ps_sigs = True
     return lib
 
@@ -155,7 +156,14 @@ class PSConnection:
             body = ctypes.string_at(lib.ttd_ps_client_resp(self._h), n) if n else b""
         return st, body
 
+    def abort(self):
+        """Cancel a call blocked on another thread (it raises UnavailableError)."""
+        h = self._h
+        if h is not None:
+            _lib().ttd_ps_client_abort(h)
+
     def close(self):
+        self.abort()
         with self._lock:
             if self._h is not None:
                 _lib().ttd_ps_client_close(self._h)
@@ -209,7 +217,13 @@ class PSClient:
             self._blocking[key] = c
         return c
 
+    def cancel_blocking(self, purpose: Optional[str] = None):
+        for (t, p), c in list(self._blocking.items()):
+            if purpose is None or p == purpose:
+                c.abort()
+
     def close(self):
+        self.cancel_blocking()
         for c in self.conns + list(self._blocking.values()):
             c.close()
 

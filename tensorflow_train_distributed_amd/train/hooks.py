@@ -466,3 +466,6 @@ class SyncReplicasOptimizerHook(SessionRunHook):
                 op.client.close_queue()
             except errors.OpError:
                 pass
+            op.client.cancel_blocking("take")  # unblock the queue runner's pending take
+            if self._thread is not None:
+                self._thread.join(10)
