@@ -106,3 +106,39 @@ def test_convbn_unit_backward_oracle(which):
     if dx is not None:
         dxr = conv2d_input(xf.shape, wf, dzb, stride=c.stride, padding=c.pad).permute(0, 2, 3, 1)
         assert rel(dx, dxr) < 2e-2
+
+
+@pytest.mark.gpu
+def test_resnet_step_hipgraph_replay_matches_eager():
+    """A whole training step (fwd, bwd, in-graph LR schedule, momentum update) captured into a
+    hipGraph and replayed must reproduce the eager steps (up to float-atomic summation order in
+    the BN-statistics / bias reductions)."""
+    from tensorflow_train_distributed_amd.train.flat import FlatSGD, Schedule
+    from tensorflow_train_distributed_amd.utils.graphs import capture
+
+    def make():
+        m = ResNet(((64, 1, 1), (128, 1, 2)), num_classes=10, device="cuda", seed=5)
+        o = FlatSGD(m.params, Schedule(kind=2, base_lr=0.1, warmup_steps=2, end_lr=0.0, power=2.0,
+                                       total_steps=100), momentum=0.9, weight_decay=5e-5)
+        return m, o
+
+    torch.manual_seed(0)
+    x = torch.randn(8, 32, 32, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (8,), device="cuda", dtype=torch.int32)
+    m1, o1 = make()
+    m2, o2 = make()
+
+    def step(m, o):
+        s = m.forward_backward(x, y)
+        o.step()
+        return s
+
+    eager = [step(m1, o1).clone() for _ in range(4)]
+    graph, out = capture(lambda: step(m2, o2), warmup=1)  # warmup = step 1, capture records (no run)
+    replays = [graph.replay().clone() for _ in range(3)]  # steps 2..4
+    torch.cuda.synchronize()
+    for a, b in zip(eager[1:], replays):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-3)
+    d = (m1.params.master - m2.params.master).abs().max()
+    assert float(d) < 1e-3 * float(m1.params.master.abs().max()), float(d)
+    assert int(o1.step_t) == int(o2.step_t) == 4
