@@ -1,0 +1,592 @@
+// Fused multi-head attention (flash-style) forward and backward for head_dim 64 on gfx950
+// MFMA (v_mfma_f32_16x16x32_bf16): BERT-Large self-attention (SURVEY.md §2.6 [NS] BERT
+// kernels; BASELINE.json config 4). The S x S score matrix is never materialised.
+//
+// Layout: token-major activations straight out of / into the fused QKV projection GEMM:
+//   element (b, s, h, d) of Q/K/V/O/dQ/dK/dV at base + (b*S + s)*ld + h*64 + d
+// so no transposes surround the kernels. Per (batch, head) softmax statistics lse2 / delta
+// are fp32 [B*H][S]. Scores live in the log2 domain: s2 = (q.k) * log2(e)/sqrt(64),
+// P = exp2(s2 - lse2).
+//
+// Options: per-batch key lengths (keys >= len masked), and attention-probability dropout
+// whose keep mask is a counter hash of (seed, step, site, (b*H+h, q, key)) — regenerated
+// identically in both backward kernels, never stored.
+//
+// Kernels (4 waves / workgroup, XCD-aware block order so the Q-blocks of one head share an
+// L2):
+//   fwd     : 128 query rows per workgroup (32 per wave); K/V tiles of 64 keys double-buffered
+//             in LDS (register-staged prefetch); online softmax in registers; the swapped QK^T
+//             puts 4 keys x 1 query in each lane, so P feeds the PV MFMA without any shuffle.
+//   bwd_kv  : 128 keys per workgroup; loops over 64-query tiles of Q/dO (one LDS image read
+//             by rows for S, dP and by columns (ds_read_b64_tr_b16) for dV^T, dK^T); dK, dV
+//             accumulate in registers — no cross-workgroup sums.
+//   bwd_q   : 128 queries per workgroup; recomputes S, dP per key tile; dQ in registers
+//             (deterministic, no float atomics).
+//   delta   : delta = rowsum(dO * O) per (b, h, q).
+#include "tile_common.h"
+
+namespace ttdk {
+namespace {
+
+using tile::mfma;
+using tile::off64;
+using tile::pack_frag;
+using tile::rd_col;
+using tile::rd_row;
+
+constexpr int D = 64;
+constexpr int KT = 64;    // keys (fwd/bwd_q) or queries (bwd_kv) per streamed tile
+constexpr int QBLK = 128; // rows per workgroup
+constexpr int TILE_BYTES = KT * D * 2;
+
+struct AttnParams {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  const bf16_t* o;
+  const bf16_t* dout;
+  long long ldq, ldk, ldv, ldo, lddo;
+  bf16_t* out;   // fwd: O ; bwd_q: dQ ; bwd_kv: dK
+  bf16_t* out2;  // bwd_kv: dV
+  long long ld_out, ld_out2;
+  float* lse;          // [B*H][S] log2 domain
+  const float* delta;  // [B*H][S]
+  const int* seqlen;   // [B] or null
+  int B, H, S;
+  float scale_log2;    // log2(e) / sqrt(D)
+  float scale;         // 1 / sqrt(D)
+  uint32_t drop_thr;
+  float drop_scale;    // 1 / (1 - p)
+  const long long* rng;
+  uint32_t site;
+};
+
+__device__ __forceinline__ uint4 ldg16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__device__ __forceinline__ bf16x8_t ldg_frag(const bf16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+
+// 64 rows x 64 cols tile loader: thread t moves rows (t >> 3) and (t >> 3) + 32, chunk t & 7.
+struct TileLoader {
+  const bf16_t* base;
+  long long ld;
+  int r, c;
+  uint4 v[2];
+  __device__ __forceinline__ void init(const bf16_t* b, long long l, int tid) {
+    base = b;
+    ld = l;
+    r = tid >> 3;
+    c = tid & 7;
+  }
+  __device__ __forceinline__ void load(int row0, int nrows) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = row0 + r + 32 * j;
+      v[j] = row < nrows ? ldg16(base + static_cast<long long>(row) * ld + c * 8) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) *reinterpret_cast<uint4*>(lds + off64(r + 32 * j, c * 8)) = v[j];
+  }
+};
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ------------------------------------------------------------------------------ forward
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
+  const int qblocks = P.S / QBLK;
+  const int t = tile::xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / qblocks, qblk = t - bh * qblocks;
+  const int b = bh / P.H, h = bh - b * P.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q0 = qblk * QBLK + wave * 32;
+  const int len = P.seqlen ? min(P.seqlen[b], P.S) : P.S;
+  const long long tok0 = static_cast<long long>(b) * P.S;
+
+  bf16x8_t qf[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      qf[qb][ks] = ldg_frag(P.q + (tok0 + q0 + qb * 16 + i16) * P.ldq + h * D + ks * 32 + g * 8);
+
+  TileLoader lk, lv;
+  lk.init(P.k + tok0 * P.ldk + h * D, P.ldk, tid);
+  lv.init(P.v + tok0 * P.ldv + h * D, P.ldv, tid);
+
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4_t o[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) o[qb][db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t key = DROP ? drop_key(P.rng, P.site) : 0u;
+  const int ntiles = (len + KT - 1) / KT;
+  if (ntiles > 0) {
+    lk.load(0, len);
+    lv.load(0, len);
+    lk.store(smem);
+    lv.store(smem + TILE_BYTES);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const bool nxt = kt + 1 < ntiles;
+    if (nxt) {
+      lk.load((kt + 1) * KT, len);
+      lv.load((kt + 1) * KT, len);
+    }
+    const char* sK = smem + cur * 2 * TILE_BYTES;
+    const char* sV = sK + TILE_BYTES;
+    // ---- S^T tile: lane holds keys kb*16 + 4g + i for query qb*16 + i16
+    f32x4_t s[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bf16x8_t k0 = rd_row(sK, kb * 16 + i16, g);
+      const bf16x8_t k1 = rd_row(sK, kb * 16 + i16, 4 + g);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        s[qb][kb] = mfma(k0, qf[qb][0], f32x4_t{0.f, 0.f, 0.f, 0.f});
+        s[qb][kb] = mfma(k1, qf[qb][1], s[qb][kb]);
+      }
+    }
+    const int kbase = kt * KT;
+    const bool full = kbase + KT <= len;
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = s[qb][kb][i] * P.scale_log2;
+          if (!full && kbase + kb * 16 + 4 * g + i >= len) v = -INFINITY;
+          s[qb][kb][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m[qb], mx);
+      const float msub = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = fast_exp2(m[qb] - msub);
+      m[qb] = mnew;
+      float rs = 0.f;
+      const int qrow = q0 + qb * 16 + i16;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = fast_exp2(s[qb][kb][i] - msub);
+          rs += p;
+          float pd = p;
+          if constexpr (DROP) {
+            const unsigned long long idx =
+                (static_cast<unsigned long long>(bh) * P.S + qrow) * P.S + (kbase + kb * 16 + 4 * g + i);
+            pd = drop_keep(key, idx, P.drop_thr) ? p : 0.f;
+          }
+          s[qb][kb][i] = pd;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[qb] = l[qb] * alpha + rs;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[qb][db] *= alpha;
+      pf[qb][0] = pack_frag(s[qb][0], s[qb][1]);
+      pf[qb][1] = pack_frag(s[qb][2], s[qb][3]);
+    }
+    // ---- O += P V
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8_t vf = rd_col(sV, ks * 32, ks * 32 + 16, db * 16, lane);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) o[qb][db] = mfma(vf, pf[qb][ks], o[qb][db]);
+      }
+    if (nxt) {
+      lk.store(smem + (cur ^ 1) * 2 * TILE_BYTES);
+      lv.store(smem + (cur ^ 1) * 2 * TILE_BYTES + TILE_BYTES);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // ---- normalise, store O (bf16) and lse2
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrow = q0 + qb * 16 + i16;
+    const float inv = l[qb] > 0.f ? (DROP ? P.drop_scale : 1.f) / l[qb] : 0.f;
+    bf16_t* op = P.out + (tok0 + qrow) * P.ld_out + h * D + 4 * g;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const f32x4_t v = o[qb][db] * inv;
+      uint2 w;
+      w.x = pack_bf16x2(v[0], v[1]);
+      w.y = pack_bf16x2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(op + db * 16) = w;
+    }
+    if (g == 0 && P.lse)
+      P.lse[static_cast<long long>(bh) * P.S + qrow] = l[qb] > 0.f ? m[qb] + __log2f(l[qb]) : -INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------ delta
+// delta[b*H+h][s] = sum_d dO * O ; one 8-lane group per (token, head).
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ o, long long ldo,
+                                                         const bf16_t* __restrict__ dout, long long lddo,
+                                                         float* __restrict__ delta, int B, int H, int S) {
+  const long long gid = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const long long pair = gid >> 3;  // (token, head)
+  const int c = gid & 7;
+  const long long ntok = static_cast<long long>(B) * S;
+  const bool ok = pair < ntok * H;
+  float acc = 0.f;
+  long long tok = 0;
+  int h = 0;
+  if (ok) {
+    tok = pair / H;
+    h = static_cast<int>(pair - tok * H);
+    float a[8], d[8];
+    unpack8(ldg16(o + tok * ldo + h * D + c * 8), a);
+    unpack8(ldg16(dout + tok * lddo + h * D + c * 8), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * d[j];
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (ok && c == 0) {
+    const long long b = tok / S, s = tok - b * S;
+    delta[(b * H + h) * S + s] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------ bwd dK, dV
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TILE_BYTES + 2 * KT * 4)];
+  constexpr int BUF = 2 * TILE_BYTES + 2 * KT * 4;
+  const int kblocks = P.S / QBLK;
+  const int t = tile::xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / kblocks, kblk = t - bh * kblocks;
+  const int b = bh / P.H, h = bh - b * P.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int k0 = kblk * QBLK + wave * 32;
+  const int len = P.seqlen ? min(P.seqlen[b], P.S) : P.S;
+  const long long tok0 = static_cast<long long>(b) * P.S;
+
+  f32x4_t dk[2][4], dv[2][4];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) dk[kb][db] = dv[kb][db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const bool any = kblk * QBLK < len;  // block-uniform: some key of this block is valid
+  if (any) {
+    bf16x8_t kf[2][2], vf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const long long row = tok0 + k0 + kb * 16 + i16;
+        kf[kb][ks] = ldg_frag(P.k + row * P.ldk + h * D + ks * 32 + g * 8);
+        vf[kb][ks] = ldg_frag(P.v + row * P.ldv + h * D + ks * 32 + g * 8);
+      }
+    TileLoader lq, ld;
+    lq.init(P.q + tok0 * P.ldq + h * D, P.ldq, tid);
+    ld.init(P.dout + tok0 * P.lddo + h * D, P.lddo, tid);
+    const float* lse_row = P.lse + static_cast<long long>(bh) * P.S;
+    const float* del_row = P.delta + static_cast<long long>(bh) * P.S;
+    const uint32_t key = DROP ? drop_key(P.rng, P.site) : 0u;
+    const int ntiles = P.S / KT;
+    auto stage_stats = [&](char* buf, int qt) {
+      float* st = reinterpret_cast<float*>(buf + 2 * TILE_BYTES);
+      if (tid < KT) st[tid] = lse_row[qt * KT + tid];
+      else if (tid < 2 * KT) st[tid] = del_row[qt * KT + tid - KT];
+    };
+    lq.load(0, P.S);
+    ld.load(0, P.S);
+    lq.store(smem);
+    ld.store(smem + TILE_BYTES);
+    stage_stats(smem, 0);
+    __syncthreads();
+    int cur = 0;
+    for (int qt = 0; qt < ntiles; ++qt) {
+      const bool nxt = qt + 1 < ntiles;
+      if (nxt) {
+        lq.load((qt + 1) * KT, P.S);
+        ld.load((qt + 1) * KT, P.S);
+      }
+      const char* sQ = smem + cur * BUF;
+      const char* sD = sQ + TILE_BYTES;
+      const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE_BYTES);
+      const float* sDel = sL + KT;
+      // S[q][key] and dP[q][key]: lane holds q = qb*16 + 4g + i, key = kb*16 + i16
+      f32x4_t sc[4][2], dp[4][2];
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) {
+        const bf16x8_t q0f = rd_row(sQ, qb * 16 + i16, g), q1f = rd_row(sQ, qb * 16 + i16, 4 + g);
+        const bf16x8_t d0f = rd_row(sD, qb * 16 + i16, g), d1f = rd_row(sD, qb * 16 + i16, 4 + g);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          sc[qb][kb] = mfma(q0f, kf[kb][0], f32x4_t{0.f, 0.f, 0.f, 0.f});
+          sc[qb][kb] = mfma(q1f, kf[kb][1], sc[qb][kb]);
+          dp[qb][kb] = mfma(d0f, vf[kb][0], f32x4_t{0.f, 0.f, 0.f, 0.f});
+          dp[qb][kb] = mfma(d1f, vf[kb][1], dp[qb][kb]);
+        }
+      }
+      // P, dS (in place: sc <- P*keep*scale, dp <- dS)
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ql = qb * 16 + 4 * g + i;
+          const float lse2 = sL[ql], del = sDel[ql];
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            const int kcol = k0 + kb * 16 + i16;
+            float p = kcol < len ? fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2) : 0.f;
+            float dpv = dp[qb][kb][i];
+            float pd = p;
+            if constexpr (DROP) {
+              const unsigned long long idx =
+                  (static_cast<unsigned long long>(bh) * P.S + (qt * KT + ql)) * P.S + kcol;
+              const bool kp = drop_keep(key, idx, P.drop_thr);
+              pd = kp ? p * P.drop_scale : 0.f;
+              dpv = kp ? dpv * P.drop_scale : 0.f;
+            }
+            sc[qb][kb][i] = pd;
+            dp[qb][kb][i] = p * (dpv - del);
+          }
+        }
+      // dV^T += dO^T P_d ; dK^T += Q^T dS   (contraction over the 64 queries in 2 chunks)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t pfr[2], sfr[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          pfr[kb] = pack_frag(sc[2 * ks][kb], sc[2 * ks + 1][kb]);
+          sfr[kb] = pack_frag(dp[2 * ks][kb], dp[2 * ks + 1][kb]);
+        }
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const bf16x8_t dof = rd_col(sD, ks * 32, ks * 32 + 16, db * 16, lane);
+          const bf16x8_t qcf = rd_col(sQ, ks * 32, ks * 32 + 16, db * 16, lane);
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            dv[kb][db] = mfma(dof, pfr[kb], dv[kb][db]);
+            dk[kb][db] = mfma(qcf, sfr[kb], dk[kb][db]);
+          }
+        }
+      }
+      if (nxt) {
+        char* nb = smem + (cur ^ 1) * BUF;
+        lq.store(nb);
+        ld.store(nb + TILE_BYTES);
+        stage_stats(nb, qt + 1);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  // store dK (scaled by 1/sqrt(D)) and dV: lane holds key kb*16 + i16, d = db*16 + 4g + i
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const long long row = tok0 + k0 + kb * 16 + i16;
+    bf16_t* pk = P.out + row * P.ld_out + h * D + 4 * g;
+    bf16_t* pv = P.out2 + row * P.ld_out2 + h * D + 4 * g;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const f32x4_t a = dk[kb][db] * P.scale, c = dv[kb][db];
+      *reinterpret_cast<uint2*>(pk + db * 16) = make_uint2(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]));
+      *reinterpret_cast<uint2*>(pv + db * 16) = make_uint2(pack_bf16x2(c[0], c[1]), pack_bf16x2(c[2], c[3]));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ bwd dQ
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
+  const int qblocks = P.S / QBLK;
+  const int t = tile::xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / qblocks, qblk = t - bh * qblocks;
+  const int b = bh / P.H, h = bh - b * P.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q0 = qblk * QBLK + wave * 32;
+  const int len = P.seqlen ? min(P.seqlen[b], P.S) : P.S;
+  const long long tok0 = static_cast<long long>(b) * P.S;
+
+  bf16x8_t qf[2][2], df[2][2];
+  float lse2[2], del[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const long long row = tok0 + q0 + qb * 16 + i16;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[qb][ks] = ldg_frag(P.q + row * P.ldq + h * D + ks * 32 + g * 8);
+      df[qb][ks] = ldg_frag(P.dout + row * P.lddo + h * D + ks * 32 + g * 8);
+    }
+    lse2[qb] = P.lse[static_cast<long long>(bh) * P.S + q0 + qb * 16 + i16];
+    del[qb] = P.delta[static_cast<long long>(bh) * P.S + q0 + qb * 16 + i16];
+  }
+  f32x4_t dq[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) dq[qb][db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  TileLoader lk, lv;
+  lk.init(P.k + tok0 * P.ldk + h * D, P.ldk, tid);
+  lv.init(P.v + tok0 * P.ldv + h * D, P.ldv, tid);
+  const uint32_t key = DROP ? drop_key(P.rng, P.site) : 0u;
+  const int ntiles = (len + KT - 1) / KT;
+  if (ntiles > 0) {
+    lk.load(0, len);
+    lv.load(0, len);
+    lk.store(smem);
+    lv.store(smem + TILE_BYTES);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const bool nxt = kt + 1 < ntiles;
+    if (nxt) {
+      lk.load((kt + 1) * KT, len);
+      lv.load((kt + 1) * KT, len);
+    }
+    const char* sK = smem + cur * 2 * TILE_BYTES;
+    const char* sV = sK + TILE_BYTES;
+    f32x4_t sc[2][4], dp[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bf16x8_t k0f = rd_row(sK, kb * 16 + i16, g), k1f = rd_row(sK, kb * 16 + i16, 4 + g);
+      const bf16x8_t v0f = rd_row(sV, kb * 16 + i16, g), v1f = rd_row(sV, kb * 16 + i16, 4 + g);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        sc[qb][kb] = mfma(k0f, qf[qb][0], f32x4_t{0.f, 0.f, 0.f, 0.f});
+        sc[qb][kb] = mfma(k1f, qf[qb][1], sc[qb][kb]);
+        dp[qb][kb] = mfma(v0f, df[qb][0], f32x4_t{0.f, 0.f, 0.f, 0.f});
+        dp[qb][kb] = mfma(v1f, df[qb][1], dp[qb][kb]);
+      }
+    }
+    const int kbase = kt * KT;
+    bf16x8_t sfr[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int qrow = q0 + qb * 16 + i16;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kcol = kbase + kb * 16 + 4 * g + i;
+          const float p = kcol < len ? fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2[qb]) : 0.f;
+          float dpv = dp[qb][kb][i];
+          if constexpr (DROP) {
+            const unsigned long long idx = (static_cast<unsigned long long>(bh) * P.S + qrow) * P.S + kcol;
+            dpv = drop_keep(key, idx, P.drop_thr) ? dpv * P.drop_scale : 0.f;
+          }
+          sc[qb][kb][i] = p * (dpv - del[qb]);
+        }
+      sfr[qb][0] = pack_frag(sc[qb][0], sc[qb][1]);
+      sfr[qb][1] = pack_frag(sc[qb][2], sc[qb][3]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8_t kc = rd_col(sK, ks * 32, ks * 32 + 16, db * 16, lane);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) dq[qb][db] = mfma(kc, sfr[qb][ks], dq[qb][db]);
+      }
+    if (nxt) {
+      lk.store(smem + (cur ^ 1) * 2 * TILE_BYTES);
+      lv.store(smem + (cur ^ 1) * 2 * TILE_BYTES + TILE_BYTES);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    bf16_t* op = P.out + (tok0 + q0 + qb * 16 + i16) * P.ld_out + h * D + 4 * g;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const f32x4_t v = dq[qb][db] * P.scale;
+      *reinterpret_cast<uint2*>(op + db * 16) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+  }
+}
+
+AttnParams make_params(int B, int H, int S, const int* seqlen, float p_drop, const long long* rng, uint32_t site) {
+  AttnParams P{};
+  P.B = B;
+  P.H = H;
+  P.S = S;
+  P.seqlen = seqlen;
+  P.scale = 0.125f;  // 1/sqrt(64)
+  P.scale_log2 = 0.125f * 1.4426950408889634f;
+  P.drop_thr = drop_threshold(p_drop);
+  P.drop_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  P.rng = rng;
+  P.site = site;
+  return P;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+}  // namespace ttdk
+
+using namespace ttdk;
+
+// Shapes: S % 128 == 0, head_dim 64, every ld % 8 == 0 and bases 16-B aligned (checked).
+// Returns hipErrorInvalidValue on violation (the Python wrapper raises).
+TTDK_EXPORT int ttdk_attn_fwd(const bf16_t* q, long long ldq, const bf16_t* k, long long ldk, const bf16_t* v,
+                              long long ldv, bf16_t* o, long long ldo, float* lse, const int* seqlen, int B, int H,
+                              int S, float p_drop, const long long* rng, unsigned site, hipStream_t st) {
+  if (S % QBLK || (ldq | ldk | ldv | ldo) & 7 || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) ||
+      (p_drop > 0.f && !rng))
+    return hipErrorInvalidValue;
+  AttnParams P = make_params(B, H, S, seqlen, p_drop, rng, site);
+  P.q = q; P.k = k; P.v = v; P.ldq = ldq; P.ldk = ldk; P.ldv = ldv;
+  P.out = o; P.ld_out = ldo; P.lse = lse;
+  dim3 grid(B * H * (S / QBLK)), block(256);
+  if (p_drop > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, block, 0, st, P);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, block, 0, st, P);
+  return hipGetLastError();
+}
+
+// dq/dk/dv may alias one fused [tokens, 3*H*64] buffer (different column offsets).
+TTDK_EXPORT int ttdk_attn_bwd(const bf16_t* q, long long ldq, const bf16_t* k, long long ldk, const bf16_t* v,
+                              long long ldv, const bf16_t* o, long long ldo, const bf16_t* dout, long long lddo,
+                              const float* lse, float* delta, bf16_t* dq, long long lddq, bf16_t* dk, long long lddk,
+                              bf16_t* dv, long long lddv, const int* seqlen, int B, int H, int S, float p_drop,
+                              const long long* rng, unsigned site, hipStream_t st) {
+  if (S % QBLK || (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) & 7 || !aligned16(q) || !aligned16(k) ||
+      !aligned16(v) || !aligned16(o) || !aligned16(dout) || (p_drop > 0.f && !rng))
+    return hipErrorInvalidValue;
+  const long long pairs = static_cast<long long>(B) * S * H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3(static_cast<unsigned>((pairs * 8 + 255) / 256)), dim3(256), 0, st, o, ldo,
+                     dout, lddo, delta, B, H, S);
+  AttnParams P = make_params(B, H, S, seqlen, p_drop, rng, site);
+  P.q = q; P.k = k; P.v = v; P.o = o; P.dout = dout;
+  P.ldq = ldq; P.ldk = ldk; P.ldv = ldv; P.ldo = ldo; P.lddo = lddo;
+  P.lse = const_cast<float*>(lse);
+  P.delta = delta;
+  dim3 grid(B * H * (S / QBLK)), block(256);
+  P.out = dk; P.ld_out = lddk; P.out2 = dv; P.ld_out2 = lddv;
+  if (p_drop > 0.f) hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, block, 0, st, P);
+  else hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, block, 0, st, P);
+  P.out = dq; P.ld_out = lddq; P.out2 = nullptr;
+  if (p_drop > 0.f) hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, block, 0, st, P);
+  else hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, block, 0, st, P);
+  return hipGetLastError();
+}

@@ -322,11 +322,19 @@ struct MNConvGather {
 };
 
 // ------------------------------------------------------------------ epilogues
-enum Act : int { kActNone = 0, kActRelu = 1, kActGelu = 2 };
+// kActDGelu: backward of the tanh-GELU: out = acc * gelu'(residual) (residual = the
+// pre-activation saved by the forward epilogue; not added).
+enum Act : int { kActNone = 0, kActRelu = 1, kActGelu = 2, kActTanh = 3, kActDGelu = 4 };
 
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float t = tanhf(k0 * (x + k1 * x * x * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
 struct EpiParams {
@@ -344,6 +352,7 @@ struct EpiParams {
   int rP, rQ, rOH, rOW, rs;
   float* stat;  // BN partial sums: [tiles_m][2][N] (sum, sumsq) or null
   float alpha;  // scale applied to acc
+  bf16_t* aux;  // optional: pre-activation copy (GELU backward input), row stride ldo
 };
 
 __device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
@@ -431,8 +440,13 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
 #pragma unroll
         for (int j = 0; j < 8; ++j) rv[j] = n + j < N ? bf2f(rp[j]) : 0.f;
       }
+      if (E.act == kActDGelu) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += rv[j];
+        for (int j = 0; j < 8; ++j) f[j] *= gelu_tanh_grad(rv[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += rv[j];
+      }
     }
     bf16_t* op = out + out_row(E, m) * E.ldo + n;
     if (E.beta) {
@@ -446,12 +460,27 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] += ov[j];
     }
+    if (E.aux) {
+      bf16_t* ap = E.aux + out_row(E, m) * E.ldo + n;
+      const uint4 pa = pack8(f);
+      if (vst) {
+        *reinterpret_cast<uint4*>(ap) = pa;
+      } else {
+        const uint32_t w[4] = {pa.x, pa.y, pa.z, pa.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n + j < N) ap[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+      }
+    }
     if (E.act == kActRelu) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
     } else if (E.act == kActGelu) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
+    } else if (E.act == kActTanh) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = tanhf(f[j]);
     }
     const uint4 packed = pack8(f);
     if (vst) {
@@ -689,6 +718,7 @@ struct TtdkEpilogue {
   int rP, rQ, rOH, rOW, rs;
   float* stat;
   float alpha;
+  bf16_t* aux;  // optional second bf16 output: the pre-activation value (same layout as out)
 };
 
 static EpiParams to_epi(const TtdkEpilogue* e) {
@@ -710,6 +740,7 @@ static EpiParams to_epi(const TtdkEpilogue* e) {
   p.rs = e->rs;
   p.stat = e->stat;
   p.alpha = e->alpha == 0.f ? 1.f : e->alpha;
+  p.aux = e->aux;
   return p;
 }
 

@@ -1,0 +1,454 @@
+"""BERT pre-training (masked-LM + next-sentence) on the gfx950 kernel library —
+BASELINE.json config 4 ("BERT-Large seq=512 bf16 MirroredStrategy"), SURVEY.md §2.6 [NS]
+BERT kernel list (embedding gather/scatter, LayerNorm, QKV/out-proj/FFN GEMMs, fused
+attention, GELU, dropout, Adam/LAMB).
+
+Execution model (MI355X-first, mirrors models/resnet.py):
+* activations are token-major bf16 [B*S, features]; the fused QKV projection writes
+  [tokens, 3H] and the attention kernels read Q/K/V as strided column slices of it and write
+  dQ/dK/dV back into one [tokens, 3H] gradient, so no head transposes exist;
+* dense kernels are stored [out, in] (the GEMM's K-major B operand; the checkpoint layer
+  exports TF's [in, out]); q/k/v kernels and biases are adjacent in the flat store so the
+  fused [3H, H] projection is a zero-copy view;
+* every sub-layer epilogue is fused: bias (+GELU, keeping the pre-activation for backward)
+  in the GEMM epilogue; residual add + hidden dropout + LayerNorm in one pass; GELU'
+  multiplies inside the dgrad GEMM epilogue;
+* dropout masks are counter hashes of a device-resident (seed, step) — nothing is stored,
+  backward regenerates them, and a hipGraph-captured step still draws fresh masks;
+* variables live in one FlatParams store in backward-completion order (heads, pooler,
+  layers L-1..0, embeddings; the tied word embedding last) so bucketed all-reduce
+  (parallel/collective.py) launches as soon as each layer's gradients are final;
+* the vocabulary is padded to a multiple of 64 (zero rows, masked out of the softmax and
+  sliced off in checkpoints) so the decoder GEMM and the vocab softmax stay vectorised.
+
+Variable names follow Google's TF BERT checkpoints (bert/encoder/layer_N/attention/self/
+query/kernel, cls/predictions/output_bias, ...).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..train.flat import FlatParams, ParamSpec
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden_size: int = 1024
+    num_hidden_layers: int = 24
+    num_attention_heads: int = 16
+    intermediate_size: int = 4096
+    max_position_embeddings: int = 512
+    type_vocab_size: int = 2
+    hidden_dropout_prob: float = 0.1
+    attention_probs_dropout_prob: float = 0.1
+    layer_norm_eps: float = 1e-12
+    initializer_range: float = 0.02
+
+    @property
+    def vocab_padded(self) -> int:
+        return (self.vocab_size + 63) // 64 * 64
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden_size // self.num_attention_heads
+
+    @staticmethod
+    def large(**kw) -> "BertConfig":
+        return BertConfig(**kw)
+
+    @staticmethod
+    def base(**kw) -> "BertConfig":
+        d = dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072)
+        d.update(kw)
+        return BertConfig(**d)
+
+
+def _trunc(std, rows=None):
+    def init(t, gen):
+        torch.nn.init.trunc_normal_(t, 0.0, std, -2 * std, 2 * std, generator=gen)
+        if rows is not None:
+            t[rows:] = 0.0
+    return init
+
+
+def _fill(v):
+    def init(t, gen):
+        t.fill_(v)
+    return init
+
+
+@dataclass
+class BertBatch:
+    input_ids: torch.Tensor          # int32 [B, S]
+    token_type_ids: torch.Tensor     # int32 [B, S]
+    masked_lm_positions: torch.Tensor  # int32 [B, P] positions within the sequence
+    masked_lm_ids: torch.Tensor      # int32 [B, P] (-1 = padding slot)
+    next_sentence_labels: torch.Tensor  # int32 [B]
+    seqlen: Optional[torch.Tensor] = None  # int32 [B] valid lengths (None = all S)
+
+
+def synthetic_batch(cfg: BertConfig, B: int, S: int, max_predictions: int = 80, device="cuda", seed: int = 0,
+                    full_length: bool = True) -> BertBatch:
+    """Random-token pre-training batch of the shape of BERT's seq-512 phase-2 data
+    (max_predictions_per_seq = 80): distinct masked positions, random targets."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    lo = min(1000, cfg.vocab_size // 2)  # skip BERT's [unused]/special-token id range
+    ids = torch.randint(lo, cfg.vocab_size, (B, S), generator=g, dtype=torch.int32)
+    tt = torch.zeros((B, S), dtype=torch.int32)
+    half = torch.randint(S // 4, 3 * S // 4, (B,), generator=g)
+    for b in range(B):
+        tt[b, int(half[b]):] = 1
+    pos = torch.stack([torch.randperm(S - 1, generator=g)[:max_predictions] + 1 for _ in range(B)]).sort(1).values
+    lab = torch.randint(lo, cfg.vocab_size, (B, max_predictions), generator=g, dtype=torch.int32)
+    nsp = torch.randint(0, 2, (B,), generator=g, dtype=torch.int32)
+    seqlen = None
+    if not full_length:
+        seqlen = torch.randint(S // 2, S + 1, (B,), generator=g, dtype=torch.int32)
+        for b in range(B):
+            L = int(seqlen[b])
+            keep = pos[b] < L
+            lab[b][~keep] = -1
+    return BertBatch(ids.to(device), tt.to(device), pos.to(torch.int32).to(device), lab.to(device), nsp.to(device),
+                     seqlen.to(device) if seqlen is not None else None)
+
+
+class BertPretraining:
+    """BERT encoder + masked-LM / NSP heads with a hand-scheduled forward/backward."""
+
+    def __init__(self, cfg: BertConfig, device="cuda", seed: int = 0, dropout: bool = True):
+        if cfg.head_dim != 64:
+            raise ValueError("the attention kernels are specialised for head_dim 64")
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dropout = dropout
+        self.params = FlatParams(self.build_specs(cfg), self.device, seed=seed)
+        P = self.params
+        H, I, L = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
+        for name_a, n, width in [("query/kernel", 3, H * H), ("query/bias", 3, H)]:
+            for l in range(L):
+                o = P.offsets[self._ln(l, "attention/self/" + name_a)]
+                for j, nm in enumerate(["query", "key", "value"]):
+                    o2 = P.offsets[self._ln(l, "attention/self/%s/%s" % (nm, name_a.split("/")[1]))]
+                    if o2 != o + j * width:
+                        raise AssertionError("q/k/v %s not contiguous" % name_a)
+        self.rng = None
+        if self.device.type == "cuda":
+            from ..ops.transformer import RngState
+            self.rng = RngState(seed * 7919 + 17, self.device)
+
+    # ------------------------------------------------------------------ variables
+    @staticmethod
+    def _ln(l, suffix):
+        return "bert/encoder/layer_%d/%s" % (l, suffix)
+
+    @staticmethod
+    def build_specs(cfg: BertConfig) -> List[ParamSpec]:
+        c = cfg
+        H, I, V, Vp = c.hidden_size, c.intermediate_size, c.vocab_size, c.vocab_padded
+        std = c.initializer_range
+        sp: List[ParamSpec] = []
+
+        def dense(name, n_out, n_in):
+            sp.append(ParamSpec(name + "/kernel", (n_out, n_in), _trunc(std),
+                                meta={"layout": "NK", "tf_shape": (n_in, n_out)}))
+
+        def bias(name, n):
+            sp.append(ParamSpec(name, (n,), _fill(0.0), weight_decay=False))
+
+        def ln(name):
+            sp.append(ParamSpec(name + "/gamma", (H,), _fill(1.0), weight_decay=False))
+            sp.append(ParamSpec(name + "/beta", (H,), _fill(0.0), weight_decay=False))
+
+        bias_spec = ParamSpec("cls/predictions/output_bias", (Vp,), _fill(0.0), weight_decay=False,
+                              meta={"rows": V})
+        sp.append(bias_spec)
+        ln("cls/predictions/transform/LayerNorm")
+        dense("cls/predictions/transform/dense", H, H)
+        bias("cls/predictions/transform/dense/bias", H)
+        # TF keeps output_weights as [2, H] = [out, in] already
+        sp.append(ParamSpec("cls/seq_relationship/output_weights", (2, H), _trunc(std)))
+        bias("cls/seq_relationship/output_bias", 2)
+        dense("bert/pooler/dense", H, H)
+        bias("bert/pooler/dense/bias", H)
+        for l in reversed(range(c.num_hidden_layers)):
+            p = lambda s, l=l: BertPretraining._ln(l, s)  # noqa: E731
+            ln(p("output/LayerNorm"))
+            dense(p("output/dense"), H, I)
+            bias(p("output/dense/bias"), H)
+            dense(p("intermediate/dense"), I, H)
+            bias(p("intermediate/dense/bias"), I)
+            ln(p("attention/output/LayerNorm"))
+            dense(p("attention/output/dense"), H, H)
+            bias(p("attention/output/dense/bias"), H)
+            for nm in ("query", "key", "value"):
+                dense(p("attention/self/" + nm), H, H)
+            for nm in ("query", "key", "value"):
+                bias(p("attention/self/%s/bias" % nm), H)
+        ln("bert/embeddings/LayerNorm")
+        sp.append(ParamSpec("bert/embeddings/token_type_embeddings", (c.type_vocab_size, H), _trunc(std)))
+        sp.append(ParamSpec("bert/embeddings/position_embeddings", (c.max_position_embeddings, H), _trunc(std)))
+        sp.append(ParamSpec("bert/embeddings/word_embeddings", (Vp, H), _trunc(std, rows=V), meta={"rows": V}))
+        return sp
+
+    @staticmethod
+    def count_parameters(cfg: BertConfig) -> int:
+        """Unpadded parameter count (what a TF checkpoint of this config holds)."""
+        n = 0
+        for s in BertPretraining.build_specs(cfg):
+            shape = list(s.shape)
+            if "rows" in s.meta:
+                shape[0] = s.meta["rows"]
+            n += int(np.prod(shape))
+        return n
+
+    def _fused(self, l, what):
+        """Zero-copy fused q/k/v views: what in {'w', 'b', 'gw', 'gb'}."""
+        P, H = self.params, self.cfg.hidden_size
+        if what in ("w", "gw"):
+            o = P.offsets[self._ln(l, "attention/self/query/kernel")]
+            buf = P.compute if what == "w" else P.grad
+            return buf[o:o + 3 * H * H].view(3 * H, H)
+        o = P.offsets[self._ln(l, "attention/self/query/bias")]
+        buf = P.master if what == "b" else P.grad
+        return buf[o:o + 3 * H]
+
+    # ------------------------------------------------------------------ training step
+    def forward_backward(self, batch: BertBatch, loss_scale: float = 1.0, grad_hook=None):
+        """One pre-training forward + backward on the GPU kernels. Gradients of
+        loss_scale * (mean MLM loss + mean NSP loss) land in params.grad (loss_scale =
+        1/replicas for data parallelism). Returns device fp32[4] =
+        (mlm loss, mlm accuracy, nsp loss, nsp accuracy)."""
+        from ..ops import gemm as G
+        from ..ops import kernels as K
+        from ..ops import transformer as T
+        c, P = self.cfg, self.params
+        dev = self.device
+        B, S = batch.input_ids.shape
+        H, NH, L = c.hidden_size, c.num_attention_heads, c.num_hidden_layers
+        V = c.vocab_size
+        Tk = B * S
+        hd = c.hidden_dropout_prob if self.dropout else 0.0
+        ad = c.attention_probs_dropout_prob if self.dropout else 0.0
+        eps = c.layer_norm_eps
+        rng = self.rng
+        if rng is not None and (hd > 0 or ad > 0):
+            rng.advance()
+        hook = grad_hook or (lambda name: None)
+        bf = torch.bfloat16
+
+        def site(l, k):
+            return (l + 1) * 8 + k
+
+        def wgrad(dy, x, out):
+            M, N, Kd = dy.shape[1], x.shape[1], dy.shape[0]
+            G.gemm(dy, x, trans_a=True, out=out, splits=G.gemm_wgrad_splits(M, N, Kd))
+
+        ids = batch.input_ids.reshape(-1)
+        tt = batch.token_type_ids.reshape(-1)
+        seqlen = batch.seqlen
+        offs = (torch.arange(B, device=dev, dtype=torch.int32) * S)
+        pos_idx = (batch.masked_lm_positions + offs[:, None]).reshape(-1).contiguous()
+        labels = batch.masked_lm_ids.reshape(-1).contiguous()
+        cls_idx = offs.contiguous()
+
+        # ---------------------------------------------------------------- forward
+        s0 = T.embed_fwd(ids, tt, P.c["bert/embeddings/word_embeddings"], P.c["bert/embeddings/position_embeddings"],
+                         P.c["bert/embeddings/token_type_embeddings"], S)
+        y, _, mean0, rstd0 = T.layernorm_fwd(s0, P.var["bert/embeddings/LayerNorm/gamma"],
+                                             P.var["bert/embeddings/LayerNorm/beta"], eps=eps, p_out=hd,
+                                             site_out=1, rng=rng)
+        ctx = []
+        for l in range(L):
+            x = y
+            qkv = G.gemm(x, self._fused(l, "w"), trans_b=True, bias=self._fused(l, "b"))
+            ao = torch.empty((Tk, H), dtype=bf, device=dev)
+            lse = torch.empty((B * NH, S), dtype=torch.float32, device=dev)
+            T.attention_fwd(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], ao, lse, B, NH, S, seqlen=seqlen,
+                            p_drop=ad, rng=rng, site=site(l, 0))
+            proj = G.gemm(ao, P.c[self._ln(l, "attention/output/dense/kernel")], trans_b=True,
+                          bias=P.var[self._ln(l, "attention/output/dense/bias")])
+            y1, s1, m1, r1 = T.layernorm_fwd(proj, P.var[self._ln(l, "attention/output/LayerNorm/gamma")],
+                                             P.var[self._ln(l, "attention/output/LayerNorm/beta")], res=x, eps=eps,
+                                             p_in=hd, site_in=site(l, 1), rng=rng)
+            del proj
+            pre = torch.empty((Tk, c.intermediate_size), dtype=bf, device=dev)
+            inter = G.gemm(y1, P.c[self._ln(l, "intermediate/dense/kernel")], trans_b=True,
+                           bias=P.var[self._ln(l, "intermediate/dense/bias")], act=G.ACT_GELU, aux=pre)
+            o2 = G.gemm(inter, P.c[self._ln(l, "output/dense/kernel")], trans_b=True,
+                        bias=P.var[self._ln(l, "output/dense/bias")])
+            y, s2, m2, r2 = T.layernorm_fwd(o2, P.var[self._ln(l, "output/LayerNorm/gamma")],
+                                            P.var[self._ln(l, "output/LayerNorm/beta")], res=y1, eps=eps, p_in=hd,
+                                            site_in=site(l, 2), rng=rng)
+            del o2
+            ctx.append((x, qkv, ao, lse, s1, m1, r1, y1, pre, inter, s2, m2, r2))
+
+        # masked-LM head
+        hm = T.gather_rows(y, pos_idx)
+        tpre = torch.empty_like(hm)
+        t = G.gemm(hm, P.c["cls/predictions/transform/dense/kernel"], trans_b=True,
+                   bias=P.var["cls/predictions/transform/dense/bias"], act=G.ACT_GELU, aux=tpre)
+        t2, _, mt, rt = T.layernorm_fwd(t, P.var["cls/predictions/transform/LayerNorm/gamma"],
+                                        P.var["cls/predictions/transform/LayerNorm/beta"], eps=eps)
+        logits = G.gemm(t2, P.c["bert/embeddings/word_embeddings"], trans_b=True,
+                        bias=P.var["cls/predictions/output_bias"])
+        sums = torch.zeros(4, dtype=torch.float32, device=dev)
+        inv_cnt = torch.empty(1, dtype=torch.float32, device=dev)
+        T.count_valid(labels, 1.0, inv_cnt)
+        gsc = inv_cnt * loss_scale
+        T.xent_vocab(logits, V, labels, gsc, dlogits=logits, sums=sums[0:2], mscale=inv_cnt)
+        dlog = logits  # gradient now, in place
+        # next-sentence head
+        cls = T.gather_rows(y, cls_idx)
+        pooled = G.gemm(cls, P.c["bert/pooler/dense/kernel"], trans_b=True, bias=P.var["bert/pooler/dense/bias"],
+                        act=G.ACT_TANH)
+        nsp = G.gemm(pooled, P.c["cls/seq_relationship/output_weights"], trans_b=True,
+                     bias=P.var["cls/seq_relationship/output_bias"])
+        nsums, dnsp, _, _ = K.sparse_xent(nsp, batch.next_sentence_labels, grad_scale=loss_scale / B)
+        sums[2:4].copy_(nsums)
+
+        # ---------------------------------------------------------------- backward: heads
+        g = P.g
+        wgrad(dlog, t2, g["bert/embeddings/word_embeddings"])  # tied decoder (write; embedding adds later)
+        K.colsum(dlog, out=g["cls/predictions/output_bias"])
+        hook("cls/predictions/output_bias")
+        dt2 = G.gemm(dlog, P.c["bert/embeddings/word_embeddings"])
+        del dlog, logits
+        dt, _ = T.layernorm_bwd(dt2, t, mt, rt, P.var["cls/predictions/transform/LayerNorm/gamma"],
+                                g["cls/predictions/transform/LayerNorm/gamma"],
+                                g["cls/predictions/transform/LayerNorm/beta"])
+        hook("cls/predictions/transform/LayerNorm/beta")
+        dtp = T.dact(dt, tpre, 0)
+        wgrad(dtp, hm, g["cls/predictions/transform/dense/kernel"])
+        K.colsum(dtp, out=g["cls/predictions/transform/dense/bias"])
+        dhm = G.gemm(dtp, P.c["cls/predictions/transform/dense/kernel"])
+        hook("cls/predictions/transform/dense/bias")
+        wgrad(dnsp, pooled, g["cls/seq_relationship/output_weights"])
+        K.colsum(dnsp, out=g["cls/seq_relationship/output_bias"])
+        dpooled = G.gemm(dnsp, P.c["cls/seq_relationship/output_weights"])
+        hook("cls/seq_relationship/output_bias")
+        dpp = T.dact(dpooled, pooled, 1)
+        wgrad(dpp, cls, g["bert/pooler/dense/kernel"])
+        K.colsum(dpp, out=g["bert/pooler/dense/bias"])
+        dcls = G.gemm(dpp, P.c["bert/pooler/dense/kernel"])
+        hook("bert/pooler/dense/bias")
+        dy = torch.zeros((Tk, H), dtype=bf, device=dev)
+        T.scatter_rows(dhm, pos_idx, dy)
+        T.scatter_rows(dcls, cls_idx, dy, accumulate=True)
+
+        # ---------------------------------------------------------------- backward: encoder
+        ln_work = T.ln_bwd_workspace(Tk, H, dev)
+        delta = torch.empty((B * NH, S), dtype=torch.float32, device=dev)
+        for l in reversed(range(L)):
+            x, qkv, ao, lse, s1, m1, r1, y1, pre, inter, s2, m2, r2 = ctx.pop()
+            G1 = torch.empty((Tk, H), dtype=bf, device=dev)
+            _, dout2 = T.layernorm_bwd(dy, s2, m2, r2, P.var[self._ln(l, "output/LayerNorm/gamma")],
+                                       g[self._ln(l, "output/LayerNorm/gamma")],
+                                       g[self._ln(l, "output/LayerNorm/beta")], ds_out=G1, want_dx=True, p_in=hd,
+                                       site_in=site(l, 2), rng=rng, work=ln_work)
+            del dy
+            wgrad(dout2, inter, g[self._ln(l, "output/dense/kernel")])
+            K.colsum(dout2, out=g[self._ln(l, "output/dense/bias")])
+            dpre = G.gemm(dout2, P.c[self._ln(l, "output/dense/kernel")], act=G.ACT_DGELU, residual=pre)
+            del dout2, inter, pre
+            wgrad(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")])
+            K.colsum(dpre, out=g[self._ln(l, "intermediate/dense/bias")])
+            G.gemm(dpre, P.c[self._ln(l, "intermediate/dense/kernel")], out=G1, beta=1)
+            del dpre
+            hook(self._ln(l, "intermediate/dense/bias"))
+            G0 = torch.empty((Tk, H), dtype=bf, device=dev)
+            _, dproj = T.layernorm_bwd(G1, s1, m1, r1, P.var[self._ln(l, "attention/output/LayerNorm/gamma")],
+                                       g[self._ln(l, "attention/output/LayerNorm/gamma")],
+                                       g[self._ln(l, "attention/output/LayerNorm/beta")], ds_out=G0, want_dx=True,
+                                       p_in=hd, site_in=site(l, 1), rng=rng, work=ln_work)
+            del G1
+            wgrad(dproj, ao, g[self._ln(l, "attention/output/dense/kernel")])
+            K.colsum(dproj, out=g[self._ln(l, "attention/output/dense/bias")])
+            dao = G.gemm(dproj, P.c[self._ln(l, "attention/output/dense/kernel")])
+            del dproj
+            dqkv = torch.empty((Tk, 3 * H), dtype=bf, device=dev)
+            T.attention_bwd(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], ao, dao, lse, dqkv[:, :H],
+                            dqkv[:, H:2 * H], dqkv[:, 2 * H:], B, NH, S, delta=delta, seqlen=seqlen, p_drop=ad,
+                            rng=rng, site=site(l, 0))
+            del dao, ao, qkv
+            wgrad(dqkv, x, self._fused(l, "gw"))
+            K.colsum(dqkv, out=self._fused(l, "gb"))
+            G.gemm(dqkv, self._fused(l, "w"), out=G0, beta=1)
+            del dqkv
+            hook(self._ln(l, "attention/self/value/bias"))
+            dy = G0
+
+        # ---------------------------------------------------------------- backward: embeddings
+        ds0, _ = T.layernorm_bwd(dy, s0, mean0, rstd0, P.var["bert/embeddings/LayerNorm/gamma"],
+                                 g["bert/embeddings/LayerNorm/gamma"], g["bert/embeddings/LayerNorm/beta"], p_out=hd,
+                                 site_out=1, rng=rng, work=ln_work)
+        dpos = g["bert/embeddings/position_embeddings"]
+        if S < dpos.shape[0]:
+            dpos[S:].zero_()
+        T.embed_bwd(ds0, ids, tt, g["bert/embeddings/word_embeddings"], dpos, g["bert/embeddings/token_type_embeddings"],
+                    B, S)
+        hook("bert/embeddings/word_embeddings")
+        return sums
+
+    # ------------------------------------------------------------------ fp32 reference (tests)
+    def reference_loss(self, batch: BertBatch, leaves: dict):
+        """Plain-PyTorch fp32 forward (dropout off) on `leaves` (name -> fp32 tensor with
+        requires_grad as wanted). Returns (mlm mean loss, nsp mean loss)."""
+        import torch.nn.functional as F
+        c = self.cfg
+        H, NH, L, V = c.hidden_size, c.num_attention_heads, c.num_hidden_layers, c.vocab_size
+        B, S = batch.input_ids.shape
+        W = leaves
+
+        def lin(x, name):
+            return x @ W[name + "/kernel"].t() + W[name + "/bias"]
+
+        def ln(x, name):
+            return F.layer_norm(x, (H,), W[name + "/gamma"], W[name + "/beta"], c.layer_norm_eps)
+
+        def gelu(x):
+            return 0.5 * x * (1 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
+
+        ids = batch.input_ids.long()
+        x = (W["bert/embeddings/word_embeddings"][ids] + W["bert/embeddings/position_embeddings"][:S][None]
+             + W["bert/embeddings/token_type_embeddings"][batch.token_type_ids.long()])
+        x = ln(x, "bert/embeddings/LayerNorm")
+        keymask = None
+        if batch.seqlen is not None:
+            ar = torch.arange(S, device=x.device)
+            keymask = ar[None, :] < batch.seqlen[:, None].long()
+        for l in range(L):
+            p = lambda s, l=l: self._ln(l, s)  # noqa: E731
+            q = lin(x, p("attention/self/query")).view(B, S, NH, 64).transpose(1, 2)
+            k = lin(x, p("attention/self/key")).view(B, S, NH, 64).transpose(1, 2)
+            v = lin(x, p("attention/self/value")).view(B, S, NH, 64).transpose(1, 2)
+            sc = q @ k.transpose(-1, -2) / 8.0
+            if keymask is not None:
+                sc = sc.masked_fill(~keymask[:, None, None, :], float("-inf"))
+            a = (sc.softmax(-1) @ v).transpose(1, 2).reshape(B, S, H)
+            x = ln(x + lin(a, p("attention/output/dense")), p("attention/output/LayerNorm"))
+            h = gelu(lin(x, p("intermediate/dense")))
+            x = ln(x + lin(h, p("output/dense")), p("output/LayerNorm"))
+        flat = x.reshape(B * S, H)
+        offs = torch.arange(B, device=x.device) * S
+        pos = (batch.masked_lm_positions.long() + offs[:, None]).reshape(-1)
+        t = ln(gelu(lin(flat[pos], "cls/predictions/transform/dense")), "cls/predictions/transform/LayerNorm")
+        logits = t @ W["bert/embeddings/word_embeddings"][:V].t() + W["cls/predictions/output_bias"][:V]
+        lab = batch.masked_lm_ids.reshape(-1).long()
+        mlm = F.cross_entropy(logits, lab.clamp(min=0), reduction="none")
+        valid = (lab >= 0).float()
+        mlm = (mlm * valid).sum() / valid.sum().clamp(min=1)
+        pooled = torch.tanh(lin(flat[offs], "bert/pooler/dense"))
+        nl = pooled @ W["cls/seq_relationship/output_weights"].t() + W["cls/seq_relationship/output_bias"]
+        nsp = F.cross_entropy(nl, batch.next_sentence_labels.long())
+        return mlm, nsp
+
+
+def bert_large(device="cuda", **kw) -> BertPretraining:
+    return BertPretraining(BertConfig.large(), device=device, **kw)

@@ -31,7 +31,7 @@ class Epilogue(ctypes.Structure):
         ("mode", c_int), ("out", c_void_p), ("ldo", c_longlong), ("slab_stride", c_longlong),
         ("bias", c_void_p), ("residual", c_void_p), ("ldr", c_longlong), ("act", c_int),
         ("beta", c_int), ("remap", c_int), ("rP", c_int), ("rQ", c_int), ("rOH", c_int),
-        ("rOW", c_int), ("rs", c_int), ("stat", c_void_p), ("alpha", c_float),
+        ("rOW", c_int), ("rs", c_int), ("stat", c_void_p), ("alpha", c_float), ("aux", c_void_p),
     ]
 
 

@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 
-ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_DGELU = 0, 1, 2, 3, 4
 
 # Optional launch log (kind, M, N, K, splits) for matching rocprofv3 dispatches to layer
 # shapes: enable with TTD_GEMM_LOG=1, read/reset via gemm_log().
@@ -33,19 +33,20 @@ def _log(kind, M, N, K, splits=1):
 
 
 def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,
-         slab_stride=0):
+         slab_stride=0, aux=None):
     e = _lib.Epilogue()
     e.mode = mode
     e.out = out.data_ptr()
-    e.ldo = ldo if ldo is not None else out.shape[-1]
+    e.ldo = ldo if ldo is not None else (out.stride(0) if out.dim() == 2 else out.shape[-1])
     e.slab_stride = slab_stride
     e.bias = bias.data_ptr() if bias is not None else None
     e.residual = residual.data_ptr() if residual is not None else None
-    e.ldr = residual.shape[-1] if residual is not None else 0
+    e.ldr = (residual.stride(0) if residual.dim() == 2 else residual.shape[-1]) if residual is not None else 0
     e.act = act
     e.beta = beta
     e.stat = stat.data_ptr() if stat is not None else None
     e.alpha = alpha
+    e.aux = aux.data_ptr() if aux is not None else None
     return e
 
 
@@ -63,26 +64,40 @@ def _check(t, dtype, name):
                          % (name, dtype, t.dtype, t.device, t.is_contiguous()))
 
 
+def _check2d(t, dtype, name):
+    """2-D operand whose rows may be strided (a column slice of a wider buffer)."""
+    if t.dtype != dtype or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("%s must be a row-major 2-D CUDA %s tensor (got %s %s shape %s strides %s)"
+                         % (name, dtype, t.dtype, t.device, tuple(t.shape), t.stride()))
+
+
 def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16, bias=None,
-         act=ACT_NONE, residual=None, beta=0, alpha=1.0, splits=1, tile=(0, 0)):
+         act=ACT_NONE, residual=None, beta=0, alpha=1.0, splits=1, tile=(0, 0), aux=None, stat=None):
     """C = alpha * op(a) @ op(b) (+bias) (+residual) (+C if beta) -> act.
 
-    a: [M, K] (or [K, M] with trans_a); b: [K, N] (or [N, K] with trans_b); bf16, contiguous.
+    a: [M, K] (or [K, M] with trans_a); b: [K, N] (or [N, K] with trans_b); bf16 2-D with unit
+    column stride (row stride = leading dimension, so column slices of fused buffers work).
     out_dtype bf16 (fused epilogue) or float32 (plain / split-K store).
+    aux: optional bf16 [M, N] receiving the pre-activation value (bias/residual applied).
+    stat: optional fp32 [ceil(M/BM), 2, N] per-tile column (sum, sumsq) of the stored output.
+    act=ACT_DGELU multiplies by gelu'(residual) instead of adding the residual.
     """
-    _check(a, torch.bfloat16, "a")
-    _check(b, torch.bfloat16, "b")
+    _check2d(a, torch.bfloat16, "a")
+    _check2d(b, torch.bfloat16, "b")
     M, K = (a.shape[1], a.shape[0]) if trans_a else a.shape
     Kb, N = (b.shape[1], b.shape[0]) if trans_b else b.shape
     if K != Kb:
         raise ValueError("gemm inner dims differ: %d vs %d" % (K, Kb))
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    elif tuple(out.shape) != (M, N) or out.stride(-1) != 1:
+        raise ValueError("gemm out must be [%d, %d] row-major (got %s strides %s)" % (M, N, tuple(out.shape),
+                                                                                   out.stride()))
     _log("gemm_%s%s" % ("t" if trans_a else "n", "t" if trans_b else "n"), M, N, K, splits)
     a_kmajor = 0 if trans_a else 1
-    lda = M if trans_a else K
+    lda = a.stride(0)
     b_kmajor = 1 if trans_b else 0
-    ldb = K if trans_b else N
+    ldb = b.stride(0)
     if out.dtype == torch.float32:
         splits = effective_splits(K, splits)
         if splits > 1:
@@ -90,14 +105,25 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
             e = _epi(ws, mode=1, ldo=N, slab_stride=M * N, alpha=alpha)
             _lib.call("ttdk_gemm_bf16", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K,
                       splits, tile[0], tile[1], ctypes.byref(e), _lib.stream())
+            if not out.is_contiguous():
+                raise ValueError("split-K output must be contiguous")
             _lib.call("ttdk_splitk_reduce", ws.data_ptr(), splits, M * N, out.data_ptr(), beta, _lib.stream())
             return out
-        e = _epi(out, mode=2, ldo=N, beta=beta, alpha=alpha)
+        e = _epi(out, mode=2, beta=beta, alpha=alpha)
     else:
-        e = _epi(out, bias=bias, residual=residual, act=act, beta=beta, alpha=alpha)
+        e = _epi(out, bias=bias, residual=residual, act=act, beta=beta, alpha=alpha, aux=aux, stat=stat)
     _lib.call("ttdk_gemm_bf16", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K, 1,
               tile[0], tile[1], ctypes.byref(e), _lib.stream())
     return out
+
+
+def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
+    """Split-K factor for a weight-gradient GEMM (long K = tokens, small M x N)."""
+    bm = 64 if M <= 64 else 128
+    bn = 64 if N <= 64 else 128
+    tiles = -(-M // bm) * -(-N // bn)
+    ktiles = -(-K // 64)
+    return max(1, min(ktiles // min_ktiles, -(-target_blocks // tiles)))
 
 
 def conv_geom(x_shape, w_shape, stride, padding, dilation=(1, 1)):

@@ -300,18 +300,30 @@ def load_variable(ckpt: str, name: str):
 # ------------------------------------------------------------------ TF-layout variable export
 def export_value(spec, t: torch.Tensor) -> np.ndarray:
     a = t.detach().float().cpu().numpy() if t.dtype != torch.int64 else t.detach().cpu().numpy()
-    if spec is not None and spec.meta.get("layout") == "KRSC":
+    lay = spec.meta.get("layout") if spec is not None else None
+    if lay == "KRSC":
         cin = spec.meta.get("cin", a.shape[-1])
         a = a[..., :cin].transpose(1, 2, 3, 0).copy(order="C")  # -> [R,S,C,K]
+    elif lay == "NK":  # dense kernel stored [out, in] (GEMM B operand) -> TF [in, out]
+        a = a.T.copy(order="C")
+    if spec is not None and "rows" in spec.meta:  # padded leading dim (e.g. vocabulary to a multiple of 64)
+        a = a[:spec.meta["rows"]].copy(order="C")
     return a if a.flags["C_CONTIGUOUS"] else a.copy(order="C")
 
 
 def import_value(spec, a: np.ndarray, target: torch.Tensor):
     a = np.asarray(a)
-    if spec is not None and spec.meta.get("layout") == "KRSC":
+    lay = spec.meta.get("layout") if spec is not None else None
+    if lay == "KRSC":
         w = np.zeros(tuple(target.shape), dtype=np.float32)
         cin = a.shape[2]
         w[..., :cin] = a.transpose(3, 0, 1, 2)
+        a = w
+    elif lay == "NK":
+        a = a.T
+    if spec is not None and "rows" in spec.meta and a.shape[0] != target.shape[0]:
+        w = np.zeros(tuple(target.shape), dtype=np.float32)
+        w[:a.shape[0]] = a
         a = w
     with torch.no_grad():
         target.copy_(torch.from_numpy(np.ascontiguousarray(a)).reshape(target.shape).to(target.dtype))
