@@ -652,6 +652,384 @@ hipError_t splitk_reduce(const float* ws, int splits, long long n, float* out, i
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ 256x256 LDS-DMA GEMM
+// Large-GEMM path (BERT projections/FFN, big 1x1 convs): 256x256x64 tile, 8 waves, ~1
+// workgroup per CU, operands streamed global -> LDS with global_load_lds_dwordx4 (no VGPR
+// staging; the XOR swizzle is applied on the per-lane SOURCE address so the LDS image stays
+// lane-linear). Each operand tile is split in two 128-row halves (A0/A1, B0/B1).
+//
+// Wave (wm, wn) owns rows {h*128 + wm*64 + [0,64)} and cols {h'*128 + wn*32 + [0,32)} for
+// h, h' in {0,1}: four 64x32 quadrants, one per phase, ordered (A0,B0) (A0,B1) (A1,B0)
+// (A1,B1) — so A0 is free after phase 1, B0 after phase 2, A1/B1 after phase 3, and each
+// phase can reload one freed half for the tile two K-steps ahead (2 glds per wave):
+//   phase q0 of tile T issues (T+1).A1, q1 (T+1).B1, q2 (T+2).A0, q3 (T+2).B0.
+// One raw s_barrier per phase; DMA completion is counted per wave with s_waitcnt vmcnt(N)
+// before the barrier (q0: N=8, q1: N=6 in steady state => 3-4 half-tiles stay in flight
+// across every barrier, never drained to 0 inside the loop). All LDS lives in one
+// __shared__ array. s_setprio(1) around each 16-MFMA cluster keeps hipcc from moving MFMAs
+// across the barriers. Requires K % 64 == 0, 16-B aligned operands, M, N >= 256.
+namespace big {
+constexpr int BM = 256, BN = 256, THR = 512;
+constexpr int HALF = 128 * 64 * 2;   // 16 KB
+constexpr int STAGE = 4 * HALF;      // A0 A1 B0 B1
+constexpr int PITCH = BN * 2 + 16;
+constexpr int EPI = BM * PITCH + 8 * 2 * BN * 4;
+constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// One operand (A or B): two 128-row halves per K-tile.
+template <bool KMAJ>
+struct Operand {
+  const bf16_t* src[2][2];  // [half][instruction]
+  long long kstep;
+  __device__ __forceinline__ void init(const bf16_t* p, long long ld, int row0, int rows, int tid) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = i * THR + tid;  // 16-B chunk of the half image (lane-linear per wave)
+        if constexpr (KMAJ) {
+          const int row = q >> 3, slot = q & 7;
+          const int chunk = slot ^ ((row >> 1) & 7);
+          const int r = min(row0 + h * 128 + row, rows - 1);
+          src[h][i] = p + static_cast<long long>(r) * ld + chunk * 8;
+        } else {
+          const int k = q >> 4, j = q & 15;
+          const int col = ((((j >> 1) ^ mn_swz<128>(k))) << 4) + (j & 1) * 8;
+          const int c = min(row0 + h * 128 + col, rows - 8);
+          src[h][i] = p + static_cast<long long>(k) * ld + c;
+        }
+      }
+    kstep = KMAJ ? 64 : 64 * ld;
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(char* half_lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(src[H][i] + kt * kstep),
+                                       (lds_void_t*)(half_lds + (i * THR + wave * 64) * 16), 16, 0, 0);
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* half_lds, int base, int ks, int lane) {
+    if constexpr (KMAJ)
+      return lds_read_b128(half_lds + kmaj_off(base + (lane & 15), ks * 4 + (lane >> 4)));
+    else
+      return mn_frag<128>(half_lds, base, ks, lane);
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restrict__ A, long long lda,
+                                                         const bf16_t* __restrict__ B, long long ldb, EpiParams E,
+                                                         int M, int N, int K, int tiles_m, int tiles_n,
+                                                         int kt_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int nblk = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  const int tile_n = t % tiles_n, tile_m = t / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  Operand<AK> la;
+  Operand<BKM> lb;
+  la.init(A, lda, m0, M, tid);
+  lb.init(B, ldb, n0, N, tid);
+
+  // acc[ha][hb][a][b]: rows ha*128 + wm*64 + a*16, cols hb*128 + wn*32 + b*16
+  f32x4_t acc[2][2][4][2];
+#pragma unroll
+  for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[ha][hb][a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ktiles = K / 64;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt1 = min(kt0 + kt_per_split, ktiles);
+  auto buf = [&](int kt) { return smem + ((kt - kt0) & 1) * STAGE; };
+  // half offsets inside a stage
+  constexpr int A0 = 0, A1 = HALF, B0 = 2 * HALF, B1 = 3 * HALF;
+
+  // Issue order per tile: A0, B1, A1, B0 (B0 last), so one counted wait retires a whole
+  // tile. Phase order q0 (A0,B0) q1 (A0,B1) q2 (A1,B1) q3 (A1,B0): every fragment is read
+  // from LDS once per tile and reused from registers; B1 is read behind q0's MFMAs, A1
+  // behind q1's, and the NEXT tile's A0/B0 behind q3's, so no phase waits on LDS latency.
+  // Reloads: q0 -> (T+1).A1, q1 -> (T+1).B0, q2 -> (T+2).A0, q3 -> (T+2).B1.
+  // Barriers only at q2 (WAR for A0 reloaded there) and q3 (after the counted wait that
+  // retires tile T+1: publishes its DMA to every wave; WAR for B1).
+  bf16x8_t fa[2][2][4], fb[2][2][2];  // [slot][ks][block]
+  auto read_a = [&](const char* sA, bf16x8_t (&f)[2][4]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) f[ks][a] = Operand<AK>::frag(sA, wm * 64 + a * 16, ks, lane);
+  };
+  auto read_b = [&](const char* sB, bf16x8_t (&f)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) f[ks][b] = Operand<BKM>::frag(sB, wn * 32 + b * 16, ks, lane);
+  };
+  auto mma = [&](const bf16x8_t (&x)[2][4], const bf16x8_t (&y)[2][2], f32x4_t (&c)[4][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y[ks][b], x[ks][a], c[a][b], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if (kt0 < kt1) {
+    char* b0 = buf(kt0);
+    la.template issue<0>(b0 + A0, kt0, wave);
+    lb.template issue<1>(b0 + B1, kt0, wave);
+    la.template issue<1>(b0 + A1, kt0, wave);
+    lb.template issue<0>(b0 + B0, kt0, wave);
+    if (kt0 + 1 < kt1) {
+      char* b1 = buf(kt0 + 1);
+      la.template issue<0>(b1 + A0, kt0 + 1, wave);
+      lb.template issue<1>(b1 + B1, kt0 + 1, wave);
+      wait_vm<4>();
+    } else {
+      wait_vm<0>();
+    }
+    barrier();
+    read_a(b0 + A0, fa[0]);
+    read_b(b0 + B0, fb[0]);
+  }
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const bool has1 = kt + 1 < kt1, has2 = kt + 2 < kt1;
+    char* cb = buf(kt);
+    // ---- q0: (A0, B0)
+    if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
+    mma(fa[0], fb[0], acc[0][0]);
+    read_b(cb + B1, fb[1]);
+    // ---- q1: (A0, B1)
+    if (has1) lb.template issue<0>(buf(kt + 1) + B0, kt + 1, wave);
+    mma(fa[0], fb[1], acc[0][1]);
+    read_a(cb + A1, fa[1]);
+    // ---- q2: (A1, B1)
+    barrier();
+    if (has2) la.template issue<0>(cb + A0, kt + 2, wave);
+    mma(fa[1], fb[1], acc[1][1]);
+    // ---- q3: (A1, B0); retire tile kt+1 and prefetch its A0/B0 fragments
+    if (has1) {
+      if (has2) wait_vm<2>(); else wait_vm<0>();
+    }
+    barrier();
+    if (has2) lb.template issue<1>(cb + B1, kt + 2, wave);
+    mma(fa[1], fb[0], acc[1][0]);
+    if (has1) {
+      char* nb = buf(kt + 1);
+      read_a(nb + A0, fa[0]);
+      read_b(nb + B0, fb[0]);
+    }
+  }
+  wait_vm<0>();
+  __syncthreads();
+
+  // ---------------------------------------------------------------- epilogue
+  const int g = lane >> 4, i16 = lane & 15;
+  if (E.mode != 0) {
+    float* out = static_cast<float*>(E.out) + (E.mode == 1 ? blockIdx.y * E.slab_stride : 0);
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int m = m0 + ha * 128 + wm * 64 + a * 16 + i16;
+        if (m >= M) continue;
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int n = n0 + hb * 128 + wn * 32 + b * 16 + 4 * g;
+            f32x4_t v = acc[ha][hb][a][b] * E.alpha;
+            float* o = out + static_cast<long long>(m) * E.ldo + n;
+            if (n + 3 < N && (E.ldo & 3) == 0) {
+              if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
+              *reinterpret_cast<f32x4_t*>(o) = v;
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (n + j < N) o[j] = v[j] + (E.beta ? o[j] : 0.f);
+            }
+          }
+      }
+    return;
+  }
+#pragma unroll
+  for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * 128 + wn * 32 + b * 16 + 4 * g;
+          const f32x4_t v = acc[ha][hb][a][b] * E.alpha;
+          *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+  __syncthreads();
+  constexpr int CPR = BN / 8;     // 32 chunks per row
+  constexpr int RPP = THR / CPR;  // 16 rows per pass
+  const int c = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + c * 8;
+  const bool nfull = n + 8 <= N;
+  const bool vst = nfull && (E.ldo & 7) == 0;
+  const bool vres = nfull && (E.ldr & 7) == 0;
+  bf16_t* out = static_cast<bf16_t*>(E.out);
+  float bias8[8], s8[8], q8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
+    s8[j] = q8[j] = 0.f;
+  }
+  for (int r = r0; r < BM; r += RPP) {
+    const int m = m0 + r;
+    if (m >= M || n >= N) break;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += bias8[j];
+    if (E.residual) {
+      const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
+      float rv[8];
+      if (vres) {
+        unpack8(*reinterpret_cast<const uint4*>(rp), rv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rv[j] = n + j < N ? bf2f(rp[j]) : 0.f;
+      }
+      if (E.act == kActDGelu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= gelu_tanh_grad(rv[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += rv[j];
+      }
+    }
+    bf16_t* op = out + static_cast<long long>(m) * E.ldo + n;
+    if (E.beta) {
+      float ov[8];
+      if (vst) {
+        unpack8(*reinterpret_cast<const uint4*>(op), ov);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ov[j] = n + j < N ? bf2f(op[j]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += ov[j];
+    }
+    if (E.aux) {
+      bf16_t* ap = E.aux + static_cast<long long>(m) * E.ldo + n;
+      const uint4 pa = pack8(f);
+      if (vst) {
+        *reinterpret_cast<uint4*>(ap) = pa;
+      } else {
+        const uint32_t w[4] = {pa.x, pa.y, pa.z, pa.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n + j < N) ap[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+      }
+    }
+    if (E.act == kActRelu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    } else if (E.act == kActGelu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
+    } else if (E.act == kActTanh) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = tanhf(f[j]);
+    }
+    const uint4 packed = pack8(f);
+    if (vst) {
+      *reinterpret_cast<uint4*>(op) = packed;
+    } else {
+      const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (n + j < N) op[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+    }
+    if (E.stat) {
+      float sv[8];
+      unpack8(packed, sv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s8[j] += sv[j];
+        q8[j] += sv[j] * sv[j];
+      }
+    }
+  }
+  if (E.stat) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s8[j] += __shfl_xor(s8[j], 32, 64);
+      q8[j] += __shfl_xor(q8[j], 32, 64);
+    }
+    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [8 waves][2][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wave * 2 + 0) * BN + c * 8 + j] = s8[j];
+        red[(wave * 2 + 1) * BN + c * 8 + j] = q8[j];
+      }
+    }
+    __syncthreads();
+    for (int t2 = tid; t2 < BN; t2 += THR) {
+      if (n0 + t2 < N) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ss += red[(k * 2 + 0) * BN + t2];
+          qq += red[(k * 2 + 1) * BN + t2];
+        }
+        E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t2] = ss;
+        E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t2] = qq;
+      }
+    }
+  }
+}
+
+template <bool AK, bool BKM>
+hipError_t launch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, const EpiParams& pe, int M, int N,
+                  int K, int splits, hipStream_t st) {
+  const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+  const int ktiles = K / 64;
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(tm * tn, splits), dim3(THR), 0, st, A, lda, B, ldb, pe, M, N, K, tm,
+                     tn, per);
+  return hipGetLastError();
+}
+
+}  // namespace big
+
 // ------------------------------------------------------------------ host-side dispatch
 template <int BM, int BN, class LA, class LB>
 hipError_t launch(const typename LA::Params& pa, const typename LB::Params& pb, const EpiParams& pe, int M, int N,
@@ -750,7 +1128,6 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
                                int b_kmajor, int M, int N, int K, int splits, int bm, int bn,
                                const TtdkEpilogue* epi, hipStream_t st) {
   EpiParams pe = to_epi(epi);
-  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   // 16-B vector operand loads need the contiguous dim and the leading dim to be multiples
   // of 8 elements and 16-B aligned bases; otherwise both operands use the masked scalar path.
@@ -758,6 +1135,17 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
                    (b_kmajor ? K % 8 == 0 : N % 8 == 0);
   DenseParams pa{A, lda, M, K};
   DenseParams pb{B, ldb, N, K};
+  // 256x256 LDS-DMA path for big GEMMs (explicit tile 256 forces it; 128/64 force the 4-wave kernel)
+  const bool big_ok = vec && K % 64 == 0 && M >= 256 && N >= 256 && pe.remap == 0 && pe.stat == nullptr &&
+                      (a_kmajor || M % 8 == 0) && (b_kmajor || N % 8 == 0);
+  if (big_ok && (bm == 256 || (bm == 0 && static_cast<long long>(M) * N >= (1LL << 20)))) {
+    if (a_kmajor && b_kmajor) return big::launch<true, true>(A, lda, B, ldb, pe, M, N, K, splits, st);
+    if (a_kmajor) return big::launch<true, false>(A, lda, B, ldb, pe, M, N, K, splits, st);
+    if (b_kmajor) return big::launch<false, true>(A, lda, B, ldb, pe, M, N, K, splits, st);
+    return big::launch<false, false>(A, lda, B, ldb, pe, M, N, K, splits, st);
+  }
+  if (bm == 256) bm = 0;
+  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
   if (vec) {
     if (a_kmajor && b_kmajor) return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
     if (a_kmajor) return dispatch<KDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);

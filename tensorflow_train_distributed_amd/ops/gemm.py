@@ -118,7 +118,13 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
 
 
 def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
-    """Split-K factor for a weight-gradient GEMM (long K = tokens, small M x N)."""
+    """Split-K factor for a weight-gradient GEMM (long K = tokens, small M x N). Mirrors the
+    launcher's kernel choice: the 256x256 LDS-DMA kernel (M, N >= 256, M*N >= 2^20, one
+    workgroup per CU -> aim for ~1-2 waves of 256 workgroups) or the 4-wave 128x128 kernel."""
+    if M >= 256 and N >= 256 and M * N >= (1 << 20) and K % 64 == 0:
+        tiles = -(-M // 256) * -(-N // 256)
+        ktiles = K // 64
+        return max(1, min(ktiles // min_ktiles, -(-256 // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)

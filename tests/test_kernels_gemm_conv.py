@@ -99,3 +99,28 @@ def test_conv_bn_stat_epilogue():
     yf = y.float().reshape(-1, 128)
     torch.testing.assert_close(s[0], yf.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (300, 520, 192)])
+def test_gemm256_lds_dma_path_all_layouts(ta, tb, M, N, K):
+    """The 256x256 global_load_lds kernel (forced with tile=(256, 256)) vs fp32 matmul, bf16
+    and split-K fp32 outputs, edge tiles included."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 2 * ta + tb)
+    a = torch.randn((K, M) if ta else (M, K), device="cuda").bfloat16()
+    b = torch.randn((N, K) if tb else (K, N), device="cuda").bfloat16()
+    ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda").bfloat16()
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    y = G.gemm(a, b, trans_a=ta, trans_b=tb, bias=bias, residual=res, act=G.ACT_GELU, aux=aux, tile=(256, 256))
+    pre = ref + bias + res.float()
+    torch.testing.assert_close(aux.float(), pre, atol=0.15, rtol=2e-2)
+    gel = 0.5 * pre * (1 + torch.tanh(0.7978845608028654 * (pre + 0.044715 * pre ** 3)))
+    torch.testing.assert_close(y.float(), gel, atol=0.15, rtol=2e-2)
+    for splits in (1, 3):
+        out = torch.full((M, N), 1.0, device="cuda")
+        G.gemm(a, b, trans_a=ta, trans_b=tb, out=out, splits=splits, beta=1, tile=(256, 256))
+        torch.testing.assert_close(out, ref + 1.0, atol=2e-2, rtol=1e-3)
