@@ -180,6 +180,49 @@ __global__ void colsum_kernel(const T* __restrict__ x, long long rows, int C, fl
   atomicAdd(&out[c], s);
 }
 
+// Vectorised bf16 column sum (C % 8 == 0): a 256-thread block covers 256 columns (32 threads
+// x 8 columns, 16-B loads, 512 contiguous bytes per row) x 8 row lanes over its row slice;
+// the 8 row lanes reduce through LDS and each block adds its 256 sums with one atomic each.
+__global__ __launch_bounds__(256) void colsum_bf16x8_kernel(const bf16_t* __restrict__ x, long long rows, int C,
+                                                            float* __restrict__ out, long long rows_per_slice) {
+  __shared__ float red[8][257];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 256 + cl * 8;
+  const long long r0 = blockIdx.y * rows_per_slice, r1 = min(rows, r0 + rows_per_slice);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    long long r = r0 + rl;
+    for (; r + 24 < r1; r += 32) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(x + (r + 8 * u) * C + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+    }
+    for (; r < r1; r += 8) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + r * C + c), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cl * 8 + j] = s[j];
+  __syncthreads();
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][threadIdx.x];
+    atomicAdd(&out[col], t);
+  }
+}
+
 __global__ void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
                                 long long n8, float alpha, float beta) {
   GRID_STRIDE(i, n8) {
@@ -293,6 +336,17 @@ TTDK_EXPORT int ttdk_colsum(const void* x, long long rows, int C, float* out, in
   if (!beta) {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * C, st);
     if (e != hipSuccess) return e;
+  }
+  if (dtype == 1 && C % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const int cblocks = (C + 255) / 256;
+    long long slices = (1024 + cblocks - 1) / cblocks;  // ~1024 blocks
+    const long long max_slices = (rows + 63) / 64;       // >= 64 rows per slice
+    if (slices > max_slices) slices = max_slices;
+    if (slices < 1) slices = 1;
+    const long long per = (rows + slices - 1) / slices;
+    hipLaunchKernelGGL(colsum_bf16x8_kernel, dim3(cblocks, static_cast<int>(slices)), dim3(256), 0, st,
+                       static_cast<const bf16_t*>(x), rows, C, out, per);
+    return hipGetLastError();
   }
   long long slices = (rows + 127) / 128;
   if (slices > 256) slices = 256;

@@ -77,10 +77,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c = (lane + 64 * v) * 8;
-    float o[8];
+    float o[8], gw[8], bw[8];
+    *reinterpret_cast<f32x4_t*>(gw) = *reinterpret_cast<const f32x4_t*>(gamma + c);
+    *reinterpret_cast<f32x4_t*>(gw + 4) = *reinterpret_cast<const f32x4_t*>(gamma + c + 4);
+    *reinterpret_cast<f32x4_t*>(bw) = *reinterpret_cast<const f32x4_t*>(beta + c);
+    *reinterpret_cast<f32x4_t*>(bw + 4) = *reinterpret_cast<const f32x4_t*>(beta + c + 4);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      o[j] = (f[v][j] - mean) * rstd * gamma[c + j] + beta[c + j];
+      o[j] = (f[v][j] - mean) * rstd * gw[j] + bw[j];
       if (dsp.thr_out)
         o[j] = drop_keep(kout, static_cast<unsigned long long>(row) * H + c + j, dsp.thr_out) ? o[j] * dsp.scale_out
                                                                                                : 0.f;
@@ -110,12 +114,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   const uint32_t kout = dsp.thr_out ? drop_key(dsp.rng, dsp.site_out) : 0u;
   float dg[NV][8], db[NV][8], gm[NV][8];
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
+  for (int v = 0; v < NV; ++v) {
+    *reinterpret_cast<f32x4_t*>(gm[v]) = *reinterpret_cast<const f32x4_t*>(gamma + (lane + 64 * v) * 8);
+    *reinterpret_cast<f32x4_t*>(gm[v] + 4) = *reinterpret_cast<const f32x4_t*>(gamma + (lane + 64 * v) * 8 + 4);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dg[v][j] = db[v][j] = 0.f;
-      gm[v][j] = gamma[(lane + 64 * v) * 8 + j];
-    }
+    for (int j = 0; j < 8; ++j) dg[v][j] = db[v][j] = 0.f;
+  }
   const long long r0 = static_cast<long long>(blockIdx.x) * rows_per_block;
   const long long r1 = min(static_cast<long long>(rows), r0 + rows_per_block);
   for (long long row = r0 + w; row < r1; row += 4) {
@@ -185,19 +189,33 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-// out[c] (+)= sum_b part[b * stride + c] for c < C; 64 columns per block.
+// out[c] (+)= sum_b part[b * stride + c] for c < C (C % 4 == 0, stride % 4 == 0): 64 columns
+// per block (16 threads x float4) x 16 row lanes, 4 independent loads in flight per thread.
 __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ part, int nb, int C, int stride,
                                                         float* __restrict__ out, int beta) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < C)
-    for (int b = w; b < nb; b += 4) s += part[static_cast<long long>(b) * stride + c];
-  red[w][threadIdx.x & 63] = s;
+  __shared__ f32x4_t red[16][17];
+  const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + cl * 4;
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int b = rl;
+    for (; b + 48 < nb; b += 64) {
+      f32x4_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(part + static_cast<long long>(b + 16 * u) * stride + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; b < nb; b += 16) s += *reinterpret_cast<const f32x4_t*>(part + static_cast<long long>(b) * stride + c);
+  }
+  red[rl][cl] = s;
   __syncthreads();
-  if (w == 0 && c < C) {
-    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    out[c] = beta ? out[c] + t : t;
+  if (rl == 0 && c < C) {
+    f32x4_t t = red[0][cl];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][cl];
+    f32x4_t* o = reinterpret_cast<f32x4_t*>(out + c);
+    *o = beta ? *o + t : t;
   }
 }
 
@@ -477,15 +495,22 @@ TTDK_EXPORT int ttdk_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean
   const int rpb = (rows + nb - 1) / nb;
   TTDK_LN_DISPATCH(ln_bwd_kernel, dim3(nb), dim3(256), 0, st, dy, s, mean, rstd, gamma, ds_out, dx_out, part, rows, rpb,
                    d);
-  // part rows are [dgamma(H) | dbeta(H)]
-  hipLaunchKernelGGL(colreduce_kernel, dim3((H + 63) / 64), dim3(256), 0, st, part, nb, H, 2 * H, dgamma, accumulate);
-  hipLaunchKernelGGL(colreduce_kernel, dim3((H + 63) / 64), dim3(256), 0, st, part + H, nb, H, 2 * H, dbeta,
-                     accumulate);
+  // part rows are [dgamma(H) | dbeta(H)]; one launch when the outputs are adjacent (flat store)
+  if (dbeta == dgamma + H) {
+    hipLaunchKernelGGL(colreduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, st, part, nb, 2 * H, 2 * H, dgamma,
+                       accumulate);
+  } else {
+    hipLaunchKernelGGL(colreduce_kernel, dim3((H + 63) / 64), dim3(256), 0, st, part, nb, H, 2 * H, dgamma, accumulate);
+    hipLaunchKernelGGL(colreduce_kernel, dim3((H + 63) / 64), dim3(256), 0, st, part + H, nb, H, 2 * H, dbeta,
+                       accumulate);
+  }
   return hipGetLastError();
 }
 
 // out[c] (+)= sum_b part[b * stride + c], c < C.
 TTDK_EXPORT int ttdk_colreduce(const float* part, int nb, int C, int stride, float* out, int beta, hipStream_t st) {
+  if (C % 4 || stride % 4 || (reinterpret_cast<uintptr_t>(part) & 15) || (reinterpret_cast<uintptr_t>(out) & 15))
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(colreduce_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, nb, C, stride, out, beta);
   return hipGetLastError();
 }
