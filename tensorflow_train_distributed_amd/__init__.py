@@ -13,7 +13,7 @@ tf.distribute/tf.train-shaped public API:
 """
 __version__ = "0.1.0"
 
-from . import data, distribute, models, parallel, summary, train  # noqa: E402
+from . import data, distribute, initializers, layers, models, nn, parallel, regularizers, summary, train  # noqa: E402
 from .parallel.ps import device  # noqa: E402
 from .utils import app, errors, flags  # noqa: E402
 from .train.graph import placeholder  # noqa: E402
