@@ -1046,6 +1046,11 @@ hipError_t launch(const typename LA::Params& pa, const typename LB::Params& pb, 
 }
 
 // Tile choice: prefer 128x128; shrink a dimension when it is small.
+// The 256x256 LDS-DMA kernel pays once both tile dims are full and the GEMM is large.
+inline bool big_fits(int M, int N, int K) {
+  return M >= 256 && N >= 256 && K % 64 == 0 && static_cast<long long>(M) * N >= (1LL << 20);
+}
+
 inline void pick_tile(int M, int N, int* bm, int* bn) {
   *bm = (M <= 64) ? 64 : 128;
   *bn = (N <= 64) ? 64 : 128;
@@ -1178,9 +1183,15 @@ TTDK_EXPORT int ttdk_conv_fwd(const bf16_t* x, const bf16_t* w, const TtdkConv* 
   if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
   DenseParams pb{w, K, N, K};
   if (is_pointwise(g)) {
+    // bm == 256 asks for the LDS-DMA kernel (the caller sized `stat` for 256-row tiles)
+    if (bm == 256) {
+      if (!big_fits(M, N, K) || pe.remap) return hipErrorInvalidValue;
+      return big::launch<true, true>(x, g->C, w, K, pe, M, N, K, 1, st);
+    }
     DenseParams pa{x, g->C, M, K};
     return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
   }
+  if (bm == 256) return hipErrorInvalidValue;
   GatherParams pa{x, g->H, g->W, g->C, g->P, g->Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};
   return dispatch<KConvFwd, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
 }
@@ -1199,6 +1210,9 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
     const int M = g->N * g->P * g->Q;
     if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
     DenseParams pa{dy, g->K, M, K};
+    if (g->sh == 1 && g->sw == 1 && (bm == 0 || bm == 256) && big_fits(M, N, K) && pe.stat == nullptr)
+      return big::launch<true, true>(dy, g->K, wt, K, pe, M, N, K, 1, st);
+    if (bm == 256) bm = bn = 0, pick_tile(M, N, &bm, &bn);
     if (g->sh != 1 || g->sw != 1) {
       if (g->sh != g->sw) return hipErrorInvalidValue;
       pe.remap = 1;
@@ -1211,7 +1225,7 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
     return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
   }
   const int M = g->N * g->H * g->W;
-  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
+  if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
   GatherParams pa{dy, g->P, g->Q, g->K, g->H, g->W, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};
   return dispatch<KConvDgrad, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
 }
@@ -1222,7 +1236,8 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
                                 int splits, int beta, int bm, int bn, hipStream_t st) {
   const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
   if (g->C % 8 || g->K % 8) return hipErrorInvalidValue;
-  if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
+  const bool use_big = is_pointwise(g) && (bm == 0 || bm == 256) && big_fits(M, N, K);
+  if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
   const int ktiles = ceil_div(K, BK);
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles;
@@ -1243,7 +1258,9 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
   }
   DenseParams pa{dy, g->K, M, K};
   hipError_t e;
-  if (is_pointwise(g)) {
+  if (use_big) {
+    e = big::launch<false, false>(dy, g->K, x, g->C, pe, M, N, K, splits, st);
+  } else if (is_pointwise(g)) {
     DenseParams pb{x, g->C, N, K};
     e = dispatch<MNDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
   } else {

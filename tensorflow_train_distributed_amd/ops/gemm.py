@@ -50,6 +50,11 @@ def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat
     return e
 
 
+def big_fits(M, N, K):
+    """Mirror of the C++ rule selecting the 256x256 LDS-DMA GEMM kernel."""
+    return M >= 256 and N >= 256 and K % 64 == 0 and M * N >= (1 << 20)
+
+
 def effective_splits(K, splits, bk=64):
     """Mirror of the kernel launcher's split-K clamping (every split gets >= 1 K-tile)."""
     kt = -(-K // bk)
@@ -190,6 +195,10 @@ def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
     """Split-K factor for the weight gradient: enough blocks to fill 256 CUs twice, but every
     split keeps >= min_ktiles K-steps (the slab write + reduce is pure overhead)."""
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
+    pointwise = g.R == 1 and g.S == 1 and g.sh == 1 and g.sw == 1 and g.ph == 0 and g.pw == 0
+    if pointwise and big_fits(M, N, K):  # mirrors ttdk_conv_wgrad's choice of the 256x256 kernel
+        tiles = -(-M // 256) * -(-N // 256)
+        return max(1, min((K // 64) // min_ktiles, -(-256 // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)

@@ -20,6 +20,16 @@ SHAPES = [  # (name, M, N, K, trans_a, trans_b)
     ("bert_ffn1_dgrad", T, 1024, 4096, False, False),
     ("bert_ffn1_wgrad", 4096, 1024, T, True, False),
     ("bert_qkv_wgrad", 3072, 1024, T, True, False),
+    # ResNet-50 batch-256 1x1 conv GEMMs (fwd: pixels x Cout x Cin)
+    ("r50_s2_c3_fwd", 802816, 256, 64, False, True),
+    ("r50_s2_c1_fwd", 802816, 64, 256, False, True),
+    ("r50_s3_c3_fwd", 200704, 512, 128, False, True),
+    ("r50_s3_c1_fwd", 200704, 128, 512, False, True),
+    ("r50_s4_c3_fwd", 50176, 1024, 256, False, True),
+    ("r50_s4_c1_fwd", 50176, 256, 1024, False, True),
+    ("r50_s5_c3_fwd", 12544, 2048, 512, False, True),
+    ("r50_s4_c3_wgrad", 1024, 256, 50176, True, False),
+    ("r50_s3_c3_wgrad", 512, 128, 200704, True, False),
 ]
 
 
@@ -44,6 +54,9 @@ def main():
         res = []
         wgrad = ta
         for tile in ((128, 128), (256, 256)):
+            if tile[0] == 256 and (M < 256 or N < 256):
+                res.append("256 n/a")
+                continue
             if wgrad:
                 out = torch.empty(M, N, device="cuda")
                 sp = G.gemm_wgrad_splits(M, N, K) if tile[0] == 128 else max(1, 256 // ((M // 256) * (N // 256)))
@@ -59,7 +72,7 @@ def main():
         res.append("torch %.3f ms %.0f TF/s" % (ms, fl / ms / 1e9))
         # correctness spot check of the 256 path
         out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-        G.gemm(a, b, trans_a=ta, trans_b=tb, out=out, tile=(256, 256))
+        G.gemm(a, b, trans_a=ta, trans_b=tb, out=out, tile=(256, 256) if min(M, N) >= 256 else (128, 128))
         ref = torch.matmul(at, bt)
         err = float((out.float() - ref.float()).abs().max())
         print("%-16s M=%5d N=%5d K=%5d | %s | maxerr %.3g" % (name, M, N, K, " | ".join(res), err), flush=True)
