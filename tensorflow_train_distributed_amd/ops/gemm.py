@@ -129,7 +129,7 @@ def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
     if M >= 256 and N >= 256 and M * N >= (1 << 20) and K % 64 == 0:
         tiles = -(-M // 256) * -(-N // 256)
         ktiles = K // 64
-        return max(1, min(ktiles // min_ktiles, -(-256 // tiles)))
+        return max(1, min(ktiles // 32, -(-256 // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
@@ -197,8 +197,10 @@ def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
     pointwise = g.R == 1 and g.S == 1 and g.sh == 1 and g.sw == 1 and g.ph == 0 and g.pw == 0
     if pointwise and big_fits(M, N, K):  # mirrors ttdk_conv_wgrad's choice of the 256x256 kernel
+        # ~1 wave of 256 workgroups, but >= 32 K-tiles per split: fp32 slabs cost 8 B per output
+        # element per split (write + reduce read)
         tiles = -(-M // 256) * -(-N // 256)
-        return max(1, min((K // 64) // min_ktiles, -(-256 // tiles)))
+        return max(1, min((K // 64) // 32, -(-256 // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
