@@ -24,6 +24,8 @@
 //    strided output-row remap (stride-2 1x1 dgrad), per-tile BatchNorm partial sums.
 #include "common.h"
 
+#include <type_traits>
+
 namespace ttdk {
 namespace {
 
@@ -652,80 +654,270 @@ hipError_t splitk_reduce(const float* ws, int splits, long long n, float* out, i
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------------ 256x256 LDS-DMA GEMM
-// Large-GEMM path (BERT projections/FFN, big 1x1 convs): 256x256x64 tile, 8 waves, ~1
-// workgroup per CU, operands streamed global -> LDS with global_load_lds_dwordx4 (no VGPR
-// staging; the XOR swizzle is applied on the per-lane SOURCE address so the LDS image stays
-// lane-linear). Each operand tile is split in two 128-row halves (A0/A1, B0/B1).
+// ------------------------------------------------------------------ 256-row LDS-DMA GEMM
+// Large-GEMM / large-conv path: 256 x BN x (128 B of K) tile, BN in {256, 128}, 8 waves,
+// ~1 workgroup per CU. Operand tiles stream global -> LDS with global_load_lds_dwordx4 (no
+// VGPR staging, no ds_write pass); the XOR swizzle is applied on the per-lane SOURCE address
+// so the LDS image stays lane-linear. Operand policies (A: rows = M, B: rows = N):
+//   OpDenseK   element (row, k) at p[row*ld + k]        (bf16, or fp8 e4m3/e5m2)
+//   OpDenseMN  element (k, row) at p[k*ld + row]        (bf16)
+//   OpConvK    implicit-GEMM conv row gather (fwd: x patch, dgrad: dy patch; C % (64|128))
+//   OpWgradMN  implicit-GEMM im2col columns for the weight gradient (bf16)
+// Padding / out-of-range rows read a zero page (DMA cannot zero-fill), so convolutions need
+// no masking in the MFMA loop.
 //
-// Wave (wm, wn) owns rows {h*128 + wm*64 + [0,64)} and cols {h'*128 + wn*32 + [0,32)} for
-// h, h' in {0,1}: four 64x32 quadrants, one per phase, ordered (A0,B0) (A0,B1) (A1,B0)
-// (A1,B1) — so A0 is free after phase 1, B0 after phase 2, A1/B1 after phase 3, and each
-// phase can reload one freed half for the tile two K-steps ahead (2 glds per wave):
-//   phase q0 of tile T issues (T+1).A1, q1 (T+1).B1, q2 (T+2).A0, q3 (T+2).B0.
-// One raw s_barrier per phase; DMA completion is counted per wave with s_waitcnt vmcnt(N)
-// before the barrier (q0: N=8, q1: N=6 in steady state => 3-4 half-tiles stay in flight
-// across every barrier, never drained to 0 inside the loop). All LDS lives in one
-// __shared__ array. s_setprio(1) around each 16-MFMA cluster keeps hipcc from moving MFMAs
-// across the barriers. Requires K % 64 == 0, 16-B aligned operands, M, N >= 256.
+// Each operand tile is split in two halves (A0/A1: 128 rows each, B0/B1: BN/2 rows). Wave
+// (wm, wn) owns rows {h*128 + wm*64 + [0,64)} and cols {h'*BN/2 + wn*BN/8 + [0,BN/8)}:
+// four quadrants, one per phase, ordered (A0,B0) (A0,B1) (A1,B1) (A1,B0) so every fragment
+// is read from LDS once per K-tile (B1 behind q0's MFMAs, A1 behind q1's, the next tile's
+// A0/B0 behind q3's) and each phase reloads one half no wave reads any more:
+//   q0 -> (T+1).A1, q1 -> (T+1).B0, q2 -> (T+2).A0, q3 -> (T+2).B1.
+// Barriers only at q2 (WAR for A0) and q3 (after a counted s_waitcnt vmcnt that retires
+// tile T+1 but leaves (T+2).A0 in flight; publishes T+1's DMA to every wave). All LDS lives
+// in one __shared__ array; s_setprio(1) brackets each MFMA cluster.
+// fp8: K-tile = 128 elements, v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales
+// (2x the bf16 MFMA rate); A and B fragments take the same 32 contiguous k per lane group,
+// so the product is independent of the instruction's internal k order.
 namespace big {
-constexpr int BM = 256, BN = 256, THR = 512;
-constexpr int HALF = 128 * 64 * 2;   // 16 KB
-constexpr int STAGE = 4 * HALF;      // A0 A1 B0 B1
-constexpr int PITCH = BN * 2 + 16;
-constexpr int EPI = BM * PITCH + 8 * 2 * BN * 4;
-constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+constexpr int BM = 256, THR = 512;
+
+// zero page for padded / out-of-range DMA sources (static device memory is zero-filled)
+__device__ __attribute__((aligned(16))) unsigned char g_zero[256];
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
-// One operand (A or B): two 128-row halves per K-tile.
-template <bool KMAJ>
-struct Operand {
-  const bf16_t* src[2][2];  // [half][instruction]
-  long long kstep;
-  __device__ __forceinline__ void init(const bf16_t* p, long long ld, int row0, int rows, int tid) {
+template <int HROWS>
+__device__ __forceinline__ int swz_mn(int k) {
+  if constexpr (HROWS == 128)
+    return (k & 3) | ((k >> 1) & 4);
+  else
+    return ((k >> 1) & 1) | ((k >> 2) & 2);
+}
+
+__device__ __forceinline__ void glds(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(lds), 16, 0, 0);
+}
+
+struct DenseP {
+  const void* p;
+  long long ld;   // elements
+  int rows;
+};
+
+struct ConvP {  // implicit-GEMM geometry: source tensor [Nimg, Hs, Ws, Cs]; GEMM rows on the (P, Q) grid
+  const void* x;
+  int Hs, Ws, Cs;
+  int P, Q;
+  int R, S;
+  int sh, sw, ph, pw, dh, dw;
+  int rows;
+};
+
+// ---- dense K-major: half = HROWS rows x 128 B
+template <int HROWS, int ESZ>
+struct OpDenseK {
+  using Params = DenseP;
+  static constexpr int G = HROWS / 64;  // glds per wave per half
+  const char* src[2][G];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int q = i * THR + tid;  // 16-B chunk of the half image (lane-linear per wave)
-        if constexpr (KMAJ) {
-          const int row = q >> 3, slot = q & 7;
-          const int chunk = slot ^ ((row >> 1) & 7);
-          const int r = min(row0 + h * 128 + row, rows - 1);
-          src[h][i] = p + static_cast<long long>(r) * ld + chunk * 8;
-        } else {
-          const int k = q >> 4, j = q & 15;
-          const int col = ((((j >> 1) ^ mn_swz<128>(k))) << 4) + (j & 1) * 8;
-          const int c = min(row0 + h * 128 + col, rows - 8);
-          src[h][i] = p + static_cast<long long>(k) * ld + c;
-        }
+      for (int i = 0; i < G; ++i) {
+        const int q = i * THR + tid;
+        const int row = q >> 3, slot = q & 7;
+        const int chunk = slot ^ ((row >> 1) & 7);
+        const int r = min(row0 + h * HROWS + row, P.rows - 1);
+        src[h][i] = static_cast<const char*>(P.p) + (static_cast<long long>(r) * P.ld) * ESZ + chunk * 16;
       }
-    kstep = KMAJ ? 64 : 64 * ld;
   }
   template <int H>
-  __device__ __forceinline__ void issue(char* half_lds, int kt, int wave) const {
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(src[H][i] + kt * kstep),
-                                       (lds_void_t*)(half_lds + (i * THR + wave * 64) * 16), 16, 0, 0);
-  }
-  static __device__ __forceinline__ bf16x8_t frag(const char* half_lds, int base, int ks, int lane) {
-    if constexpr (KMAJ)
-      return lds_read_b128(half_lds + kmaj_off(base + (lane & 15), ks * 4 + (lane >> 4)));
-    else
-      return mn_frag<128>(half_lds, base, ks, lane);
+    for (int i = 0; i < G; ++i) glds(src[H][i] + static_cast<long long>(kt) * 128, lds + (i * THR + wave * 64) * 16);
   }
 };
+
+// ---- dense MN-major (bf16): half = HROWS cols x 64 k
+template <int HROWS>
+struct OpDenseMN {
+  using Params = DenseP;
+  static constexpr int G = HROWS / 64;
+  static constexpr int CPR = HROWS / 8;  // 16-B chunks per k-row
+  const char* src[2][G];
+  long long kstep;
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int q = i * THR + tid;
+        const int k = q / CPR, j = q % CPR;
+        const int col = ((((j >> 1) ^ swz_mn<HROWS>(k))) << 4) + (j & 1) * 8;
+        const int c = min(row0 + h * HROWS + col, P.rows - 8);
+        src[h][i] = static_cast<const char*>(P.p) + (static_cast<long long>(k) * P.ld + c) * 2;
+      }
+    kstep = 64 * P.ld * 2;
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < G; ++i) glds(src[H][i] + kt * kstep, lds + (i * THR + wave * 64) * 16);
+  }
+};
+
+// ---- implicit-GEMM conv rows (K-major): row = output pixel of the (P, Q) grid, k = (r, s, c);
+// one K-tile (128 B) lies inside one tap (requires Cs*ESZ % 128 == 0).
+template <int HROWS, int ESZ, bool DGRAD, bool UNIT_STRIDE = false>
+struct OpConvK {
+  using Params = ConvP;
+  static constexpr int G = HROWS / 64;
+  static constexpr int KT = 128 / ESZ;  // elements per K-tile
+  const char* x;
+  int Hs, Ws, Cs, S, sh, sw, dh, dw, tid;
+  int img[2][G], hb[2][G], wb[2][G];  // img < 0: row beyond M (reads the zero page)
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid_) {
+    x = static_cast<const char*>(P.x);
+    Hs = P.Hs; Ws = P.Ws; Cs = P.Cs; S = P.S; sh = P.sh; sw = P.sw; dh = P.dh; dw = P.dw;
+    tid = tid_;
+    const int pq = P.P * P.Q;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int row = (i * THR + tid) >> 3;
+        const int m = row0 + h * HROWS + row;
+        const bool ok = m < P.rows;
+        const int mm = ok ? m : 0;
+        const int n = mm / pq, rem = mm - n * pq;
+        const int p = rem / P.Q, qq = rem - p * P.Q;
+        img[h][i] = ok ? n * P.Hs : -1;
+        if (DGRAD) {
+          hb[h][i] = p + P.ph;
+          wb[h][i] = qq + P.pw;
+        } else {
+          hb[h][i] = p * P.sh - P.ph;
+          wb[h][i] = qq * P.sw - P.pw;
+        }
+      }
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+    const int k0 = kt * KT;
+    const int tap = k0 / Cs, c0 = k0 - tap * Cs;
+    const int rr = tap / S, ss = tap - rr * S;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int row = (i * THR + tid) >> 3;
+      const int coff = (((tid & 7) ^ ((row >> 1) & 7))) * 16;
+      int hh, ww;
+      bool v = img[H][i] >= 0;
+      if (DGRAD && UNIT_STRIDE) {
+        hh = hb[H][i] - rr * dh;
+        ww = wb[H][i] - ss * dw;
+        v = v && hh >= 0 && ww >= 0;
+      } else if (DGRAD) {
+        const int hn = hb[H][i] - rr * dh, wn = wb[H][i] - ss * dw;
+        hh = hn / sh;
+        ww = wn / sw;
+        v = v && hn >= 0 && wn >= 0 && hh * sh == hn && ww * sw == wn;
+      } else {
+        hh = hb[H][i] + rr * dh;
+        ww = wb[H][i] + ss * dw;
+        v = v && hh >= 0 && ww >= 0;
+      }
+      v = v && hh < Hs && ww < Ws;
+      const char* s = v ? x + ((static_cast<long long>(img[H][i] + hh) * Ws + ww) * Cs + c0) * ESZ + coff
+                        : reinterpret_cast<const char*>(g_zero) + coff;
+      glds(s, lds + (i * THR + wave * 64) * 16);
+    }
+  }
+};
+
+// ---- weight-gradient im2col columns (MN-major, bf16): k = output pixel, column = (r, s, c)
+template <int HROWS>
+struct OpWgradMN {
+  using Params = ConvP;
+  static constexpr int G = HROWS / 64;
+  static constexpr int CPR = HROWS / 8;
+  const char* x;
+  int H, W, C, pq, Q, sh, sw;
+  int krow[2][G], roff[2][G], soff[2][G], cc[2][G];
+  bool cok[2][G];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    x = static_cast<const char*>(P.x);
+    H = P.Hs; W = P.Ws; C = P.Cs; pq = P.P * P.Q; Q = P.Q; sh = P.sh; sw = P.sw;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int q = i * THR + tid;
+        const int k = q / CPR, j = q % CPR;
+        const int col = row0 + h * HROWS + ((((j >> 1) ^ swz_mn<HROWS>(k))) << 4) + (j & 1) * 8;
+        krow[h][i] = k;
+        cok[h][i] = col < P.rows;
+        const int cl = cok[h][i] ? col : 0;
+        const int tap = cl / C, c = cl - tap * C;
+        const int rr = tap / P.S, ss = tap - rr * P.S;
+        roff[h][i] = rr * P.dh - P.ph;
+        soff[h][i] = ss * P.dw - P.pw;
+        cc[h][i] = c;
+      }
+  }
+  template <int HH>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int k = kt * 64 + krow[HH][i];
+      const int n = k / pq, rem = k - n * pq;
+      const int p = rem / Q, qq = rem - p * Q;
+      const int hh = p * sh + roff[HH][i], ww = qq * sw + soff[HH][i];
+      const bool v = cok[HH][i] && hh >= 0 && ww >= 0 && hh < H && ww < W;
+      const char* s = v ? x + ((static_cast<long long>(n * H + hh) * W + ww) * C + cc[HH][i]) * 2
+                        : reinterpret_cast<const char*>(g_zero);
+      glds(s, lds + (i * THR + wave * 64) * 16);
+    }
+  }
+};
+
+template <class OP>
+struct Traits {
+  static constexpr bool kmaj = true;
+};
+template <int HR>
+struct Traits<OpDenseMN<HR>> {
+  static constexpr bool kmaj = false;
+};
+template <int HR>
+struct Traits<OpWgradMN<HR>> {
+  static constexpr bool kmaj = false;
+};
+
+// fragment readers
+__device__ __forceinline__ bf16x8_t frag_k(const char* lds, int base, int ks, int lane) {
+  return lds_read_b128(lds + kmaj_off(base + (lane & 15), ks * 4 + (lane >> 4)));
+}
+__device__ __forceinline__ i32x8_t frag_k8(const char* lds, int base, int lane) {
+  const int row = base + (lane & 15), g = lane >> 4;
+  const uint4 lo = *reinterpret_cast<const uint4*>(lds + kmaj_off(row, 2 * g));
+  const uint4 hi = *reinterpret_cast<const uint4*>(lds + kmaj_off(row, 2 * g + 1));
+  i32x8_t v = {static_cast<int>(lo.x), static_cast<int>(lo.y), static_cast<int>(lo.z), static_cast<int>(lo.w),
+               static_cast<int>(hi.x), static_cast<int>(hi.y), static_cast<int>(hi.z), static_cast<int>(hi.w)};
+  return v;
+}
+template <int HROWS>
+__device__ __forceinline__ bf16x8_t frag_mn(const char* lds, int colbase, int ks, int lane) {
+  return mn_frag<HROWS>(lds, colbase, ks, lane);
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
 }
 
 __device__ __forceinline__ void barrier() {
@@ -734,12 +926,28 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool AK, bool BKM>
-__global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restrict__ A, long long lda,
-                                                         const bf16_t* __restrict__ B, long long ldb, EpiParams E,
+template <int BN>
+struct Geo {
+  static constexpr int BNH = BN / 2;          // B half rows
+  static constexpr int AH = 128 * 128;        // A half bytes
+  static constexpr int BH = BNH * 128;        // B half bytes
+  static constexpr int STAGE = 2 * AH + 2 * BH;
+  static constexpr int NB = BNH / 64;         // 16-col blocks per wave per B half
+  static constexpr int PITCH = BN * 2 + 16;
+  static constexpr int EPI = BM * PITCH + 8 * 2 * BN * 4;
+  static constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+};
+
+// F8: 0 = bf16, 1 = fp8 e4m3 x e4m3, 2 = e5m2 (A) x e4m3 (B)  (dgrad: gradients in e5m2)
+template <int BN, class OA, class OB, int F8>
+__global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa, typename OB::Params pb, EpiParams E,
                                                          int M, int N, int K, int tiles_m, int tiles_n,
                                                          int kt_per_split) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  using Gm = Geo<BN>;
+  constexpr int BNH = Gm::BNH, NB = Gm::NB, GA = 2, GB = BNH / 64;
+  constexpr bool AK = Traits<OA>::kmaj, BKM = Traits<OB>::kmaj;
+  static_assert(F8 == 0 || (AK && BKM), "fp8 operands must be K-major");
+  __shared__ __attribute__((aligned(16))) char smem[Gm::SMEM];
   const int nblk = tiles_m * tiles_n;
   const int t = xcd_remap(blockIdx.x, nblk);
   const int tile_n = t % tiles_n, tile_m = t / tiles_n;
@@ -747,13 +955,13 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
 
-  Operand<AK> la;
-  Operand<BKM> lb;
-  la.init(A, lda, m0, M, tid);
-  lb.init(B, ldb, n0, N, tid);
+  OA la;
+  OB lb;
+  la.init(pa, m0, tid);
+  lb.init(pb, n0, tid);
 
-  // acc[ha][hb][a][b]: rows ha*128 + wm*64 + a*16, cols hb*128 + wn*32 + b*16
-  f32x4_t acc[2][2][4][2];
+  // acc[ha][hb][a][b]: rows ha*128 + wm*64 + a*16, cols hb*BNH + wn*(BNH/4) + b*16
+  f32x4_t acc[2][2][4][NB];
 #pragma unroll
   for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
@@ -761,46 +969,57 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[ha][hb][a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < NB; ++b) acc[ha][hb][a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int ktiles = K / 64;
+  const int ktiles = K / (F8 ? 128 : 64);
   const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(kt0 + kt_per_split, ktiles);
-  auto buf = [&](int kt) { return smem + ((kt - kt0) & 1) * STAGE; };
-  // half offsets inside a stage
-  constexpr int A0 = 0, A1 = HALF, B0 = 2 * HALF, B1 = 3 * HALF;
+  auto buf = [&](int kt) { return smem + ((kt - kt0) & 1) * Gm::STAGE; };
+  constexpr int A0 = 0, A1 = Gm::AH, B0 = 2 * Gm::AH, B1 = 2 * Gm::AH + Gm::BH;
 
-  // Issue order per tile: A0, B1, A1, B0 (B0 last), so one counted wait retires a whole
-  // tile. Phase order q0 (A0,B0) q1 (A0,B1) q2 (A1,B1) q3 (A1,B0): every fragment is read
-  // from LDS once per tile and reused from registers; B1 is read behind q0's MFMAs, A1
-  // behind q1's, and the NEXT tile's A0/B0 behind q3's, so no phase waits on LDS latency.
-  // Reloads: q0 -> (T+1).A1, q1 -> (T+1).B0, q2 -> (T+2).A0, q3 -> (T+2).B1.
-  // Barriers only at q2 (WAR for A0 reloaded there) and q3 (after the counted wait that
-  // retires tile T+1: publishes its DMA to every wave; WAR for B1).
-  bf16x8_t fa[2][2][4], fb[2][2][2];  // [slot][ks][block]
-  auto read_a = [&](const char* sA, bf16x8_t (&f)[2][4]) {
+  // fragments: [slot][ks][block]; fp8 uses one "ks" of K = 128
+  constexpr int KS = F8 ? 1 : 2;
+  typedef typename std::conditional<F8 != 0, i32x8_t, bf16x8_t>::type frag_t;
+  frag_t fa[2][KS][4], fb[2][KS][NB];
+  auto read_a = [&](const char* sA, frag_t (&f)[KS][4]) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int a = 0; a < 4; ++a) f[ks][a] = Operand<AK>::frag(sA, wm * 64 + a * 16, ks, lane);
+      for (int a = 0; a < 4; ++a) {
+        if constexpr (F8 != 0) f[ks][a] = frag_k8(sA, wm * 64 + a * 16, lane);
+        else if constexpr (AK) f[ks][a] = frag_k(sA, wm * 64 + a * 16, ks, lane);
+        else f[ks][a] = frag_mn<128>(sA, wm * 64 + a * 16, ks, lane);
+      }
   };
-  auto read_b = [&](const char* sB, bf16x8_t (&f)[2][2]) {
+  auto read_b = [&](const char* sB, frag_t (&f)[KS][NB]) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) f[ks][b] = Operand<BKM>::frag(sB, wn * 32 + b * 16, ks, lane);
+      for (int b = 0; b < NB; ++b) {
+        if constexpr (F8 != 0) f[ks][b] = frag_k8(sB, wn * (BNH / 4) + b * 16, lane);
+        else if constexpr (BKM) f[ks][b] = frag_k(sB, wn * (BNH / 4) + b * 16, ks, lane);
+        else f[ks][b] = frag_mn<BNH>(sB, wn * (BNH / 4) + b * 16, ks, lane);
+      }
   };
-  auto mma = [&](const bf16x8_t (&x)[2][4], const bf16x8_t (&y)[2][2], f32x4_t (&c)[4][2]) {
+  auto mma = [&](const frag_t (&x)[KS][4], const frag_t (&y)[KS][NB], f32x4_t (&c)[4][NB]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y[ks][b], x[ks][a], c[a][b], 0, 0, 0);
+        for (int b = 0; b < NB; ++b) {
+          if constexpr (F8 == 1)
+            c[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(y[ks][b], x[ks][a], c[a][b], 0, 0, 0, 127, 0, 127);
+          else if constexpr (F8 == 2)  // A (x operand, second arg) in e5m2: blgp = 1
+            c[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(y[ks][b], x[ks][a], c[a][b], 0, 1, 0, 127, 0, 127);
+          else
+            c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y[ks][b], x[ks][a], c[a][b], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
   };
 
+  // issue order per tile: A0, B1, A1, B0 (B0 last) => one counted wait retires a whole tile
   if (kt0 < kt1) {
     char* b0 = buf(kt0);
     la.template issue<0>(b0 + A0, kt0, wave);
@@ -811,7 +1030,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
       char* b1 = buf(kt0 + 1);
       la.template issue<0>(b1 + A0, kt0 + 1, wave);
       lb.template issue<1>(b1 + B1, kt0 + 1, wave);
-      wait_vm<4>();
+      wait_vm<GA + GB>();
     } else {
       wait_vm<0>();
     }
@@ -822,21 +1041,21 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
   for (int kt = kt0; kt < kt1; ++kt) {
     const bool has1 = kt + 1 < kt1, has2 = kt + 2 < kt1;
     char* cb = buf(kt);
-    // ---- q0: (A0, B0)
+    // q0: (A0, B0)
     if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
     mma(fa[0], fb[0], acc[0][0]);
     read_b(cb + B1, fb[1]);
-    // ---- q1: (A0, B1)
+    // q1: (A0, B1)
     if (has1) lb.template issue<0>(buf(kt + 1) + B0, kt + 1, wave);
     mma(fa[0], fb[1], acc[0][1]);
     read_a(cb + A1, fa[1]);
-    // ---- q2: (A1, B1)
+    // q2: (A1, B1)
     barrier();
     if (has2) la.template issue<0>(cb + A0, kt + 2, wave);
     mma(fa[1], fb[1], acc[1][1]);
-    // ---- q3: (A1, B0); retire tile kt+1 and prefetch its A0/B0 fragments
+    // q3: (A1, B0); retire tile kt+1 ((kt+2).A0 may stay in flight), prefetch its A0/B0
     if (has1) {
-      if (has2) wait_vm<2>(); else wait_vm<0>();
+      if (has2) wait_vm<GA>(); else wait_vm<0>();
     }
     barrier();
     if (has2) lb.template issue<1>(cb + B1, kt + 2, wave);
@@ -863,8 +1082,8 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
 #pragma unroll
         for (int hb = 0; hb < 2; ++hb)
 #pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int n = n0 + hb * 128 + wn * 32 + b * 16 + 4 * g;
+          for (int b = 0; b < NB; ++b) {
+            const int n = n0 + hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
             f32x4_t v = acc[ha][hb][a][b] * E.alpha;
             float* o = out + static_cast<long long>(m) * E.ldo + n;
             if (n + 3 < N && (E.ldo & 3) == 0) {
@@ -879,6 +1098,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
       }
     return;
   }
+  constexpr int PITCH = Gm::PITCH;
 #pragma unroll
   for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
@@ -886,15 +1106,15 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * 128 + wn * 32 + b * 16 + 4 * g;
+        for (int b = 0; b < NB; ++b) {
+          const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
           const f32x4_t v = acc[ha][hb][a][b] * E.alpha;
           *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) =
               make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         }
   __syncthreads();
-  constexpr int CPR = BN / 8;     // 32 chunks per row
-  constexpr int RPP = THR / CPR;  // 16 rows per pass
+  constexpr int CPR = BN / 8;     // 16-B chunks per row
+  constexpr int RPP = THR / CPR;  // rows per pass
   const int c = tid % CPR, r0 = tid / CPR;
   const int n = n0 + c * 8;
   const bool nfull = n + 8 <= N;
@@ -945,11 +1165,11 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
     }
     if (E.aux) {
       bf16_t* ap = E.aux + static_cast<long long>(m) * E.ldo + n;
-      const uint4 pa = pack8(f);
+      const uint4 pa8 = pack8(f);
       if (vst) {
-        *reinterpret_cast<uint4*>(ap) = pa;
+        *reinterpret_cast<uint4*>(ap) = pa8;
       } else {
-        const uint32_t w[4] = {pa.x, pa.y, pa.z, pa.w};
+        const uint32_t w[4] = {pa8.x, pa8.y, pa8.z, pa8.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (n + j < N) ap[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
@@ -985,10 +1205,14 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
     }
   }
   if (E.stat) {
+    // threads sharing a chunk column c: tid % CPR equal -> within a wave lanes c, c+CPR, ...
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      s8[j] += __shfl_xor(s8[j], 32, 64);
-      q8[j] += __shfl_xor(q8[j], 32, 64);
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        s8[j] += __shfl_xor(s8[j], o, 64);
+        q8[j] += __shfl_xor(q8[j], o, 64);
+      }
     }
     float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [8 waves][2][BN]
     if (lane < CPR) {
@@ -1014,18 +1238,30 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(const bf16_t* __restric
   }
 }
 
-template <bool AK, bool BKM>
-hipError_t launch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, const EpiParams& pe, int M, int N,
+template <int BN, class OA, class OB, int F8 = 0>
+hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, const EpiParams& pe, int M, int N,
                   int K, int splits, hipStream_t st) {
   const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
-  const int ktiles = K / 64;
+  const int ktiles = K / (F8 ? 128 : 64);
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles;
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(tm * tn, splits), dim3(THR), 0, st, A, lda, B, ldb, pe, M, N, K, tm,
-                     tn, per);
+  hipLaunchKernelGGL((gemm256_kernel<BN, OA, OB, F8>), dim3(tm * tn, splits), dim3(THR), 0, st, pa, pb, pe, M, N, K,
+                     tm, tn, per);
   return hipGetLastError();
+}
+
+// dense GEMM entry: A (M rows) and B (N rows), each K-major or MN-major, bf16
+template <int BN>
+hipError_t dense(const bf16_t* A, long long lda, bool ak, const bf16_t* B, long long ldb, bool bk,
+                 const EpiParams& pe, int M, int N, int K, int splits, hipStream_t st) {
+  DenseP pa{A, lda, M}, pb{B, ldb, N};
+  constexpr int BH = BN / 2;
+  if (ak && bk) return launch<BN, OpDenseK<128, 2>, OpDenseK<BH, 2>>(pa, pb, pe, M, N, K, splits, st);
+  if (ak) return launch<BN, OpDenseK<128, 2>, OpDenseMN<BH>>(pa, pb, pe, M, N, K, splits, st);
+  if (bk) return launch<BN, OpDenseMN<128>, OpDenseK<BH, 2>>(pa, pb, pe, M, N, K, splits, st);
+  return launch<BN, OpDenseMN<128>, OpDenseMN<BH>>(pa, pb, pe, M, N, K, splits, st);
 }
 
 }  // namespace big
@@ -1046,10 +1282,13 @@ hipError_t launch(const typename LA::Params& pa, const typename LB::Params& pb, 
 }
 
 // Tile choice: prefer 128x128; shrink a dimension when it is small.
-// The 256x256 LDS-DMA kernel pays once both tile dims are full and the GEMM is large.
-inline bool big_fits(int M, int N, int K) {
-  return M >= 256 && N >= 256 && K % 64 == 0 && static_cast<long long>(M) * N >= (1LL << 20);
+// Tile width of the 256-row LDS-DMA kernel for an M x N x K GEMM, or 0 when the 4-wave
+// kernel is the better fit (small tiles / small GEMMs). Mirrored by ops/gemm.py big_bn().
+inline int big_bn(int M, int N, int K) {
+  if (M < 256 || N < 128 || K % 64 || N % 8 || static_cast<long long>(M) * N < (1LL << 20)) return 0;
+  return N >= 256 ? 256 : 128;
 }
+inline bool big_fits(int M, int N, int K) { return big_bn(M, N, K) != 0; }
 
 inline void pick_tile(int M, int N, int* bm, int* bn) {
   *bm = (M <= 64) ? 64 : 128;
@@ -1140,14 +1379,12 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
                    (b_kmajor ? K % 8 == 0 : N % 8 == 0);
   DenseParams pa{A, lda, M, K};
   DenseParams pb{B, ldb, N, K};
-  // 256x256 LDS-DMA path for big GEMMs (explicit tile 256 forces it; 128/64 force the 4-wave kernel)
-  const bool big_ok = vec && K % 64 == 0 && M >= 256 && N >= 256 && pe.remap == 0 && pe.stat == nullptr &&
-                      (a_kmajor || M % 8 == 0) && (b_kmajor || N % 8 == 0);
-  if (big_ok && (bm == 256 || (bm == 0 && static_cast<long long>(M) * N >= (1LL << 20)))) {
-    if (a_kmajor && b_kmajor) return big::launch<true, true>(A, lda, B, ldb, pe, M, N, K, splits, st);
-    if (a_kmajor) return big::launch<true, false>(A, lda, B, ldb, pe, M, N, K, splits, st);
-    if (b_kmajor) return big::launch<false, true>(A, lda, B, ldb, pe, M, N, K, splits, st);
-    return big::launch<false, false>(A, lda, B, ldb, pe, M, N, K, splits, st);
+  // 256-row LDS-DMA path for big GEMMs (explicit tile 256 forces it; 128/64 force the 4-wave kernel)
+  const int bbn = big_bn(M, N, K);
+  const bool big_ok = vec && bbn && pe.remap == 0 && pe.stat == nullptr && (a_kmajor || M % 8 == 0);
+  if (big_ok && (bm == 256 || bm == 0)) {
+    if (bbn == 256) return big::dense<256>(A, lda, a_kmajor, B, ldb, b_kmajor, pe, M, N, K, splits, st);
+    return big::dense<128>(A, lda, a_kmajor, B, ldb, b_kmajor, pe, M, N, K, splits, st);
   }
   if (bm == 256) bm = 0;
   if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
@@ -1175,25 +1412,74 @@ static bool is_pointwise(const TtdkConv* g) {
 }
 
 // y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]).
+static big::ConvP conv_params(const void* src, int Hs, int Ws, int Cs, int P, int Q, const TtdkConv* g, int rows) {
+  return big::ConvP{src, Hs, Ws, Cs, P, Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, rows};
+}
+
+// bm == 256 requests the LDS-DMA kernel (bn = its tile width 256 or 128; the caller sized
+// `stat` for 256-row tiles); the request fails loudly when the conv is not eligible.
 TTDK_EXPORT int ttdk_conv_fwd(const bf16_t* x, const bf16_t* w, const TtdkConv* g, int bm, int bn,
                               const TtdkEpilogue* epi, hipStream_t st) {
   if (g->C % 8) return hipErrorInvalidValue;
   EpiParams pe = to_epi(epi);
   const int M = g->N * g->P * g->Q, N = g->K, K = g->R * g->S * g->C;
+  if (bm == 256) {
+    const int bbn = big_bn(M, N, K);
+    if (!bbn || bbn != bn || pe.remap || g->C % 64) return hipErrorInvalidValue;
+    if (is_pointwise(g)) return bbn == 256 ? big::dense<256>(x, g->C, true, w, K, true, pe, M, N, K, 1, st)
+                                           : big::dense<128>(x, g->C, true, w, K, true, pe, M, N, K, 1, st);
+    const big::ConvP pa = conv_params(x, g->H, g->W, g->C, g->P, g->Q, g, M);
+    const big::DenseP pb{w, K, N};
+    if (bbn == 256)
+      return big::launch<256, big::OpConvK<128, 2, false>, big::OpDenseK<128, 2>>(pa, pb, pe, M, N, K, 1, st);
+    return big::launch<128, big::OpConvK<128, 2, false>, big::OpDenseK<64, 2>>(pa, pb, pe, M, N, K, 1, st);
+  }
   if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
   DenseParams pb{w, K, N, K};
   if (is_pointwise(g)) {
-    // bm == 256 asks for the LDS-DMA kernel (the caller sized `stat` for 256-row tiles)
-    if (bm == 256) {
-      if (!big_fits(M, N, K) || pe.remap) return hipErrorInvalidValue;
-      return big::launch<true, true>(x, g->C, w, K, pe, M, N, K, 1, st);
-    }
     DenseParams pa{x, g->C, M, K};
     return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
   }
-  if (bm == 256) return hipErrorInvalidValue;
   GatherParams pa{x, g->H, g->W, g->C, g->P, g->Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};
   return dispatch<KConvFwd, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
+}
+
+// fp8 forward conv / GEMM on the block-scaled MFMA: x8 [N,H,W,C] and w8 [K][R][S][C] in fp8
+// e4m3 (per-tensor scales folded into epi->alpha by the caller). C % 128 == 0, 256-row tiles.
+TTDK_EXPORT int ttdk_conv_fwd_fp8(const uint8_t* x8, const uint8_t* w8, const TtdkConv* g, int bn,
+                                  const TtdkEpilogue* epi, hipStream_t st) {
+  EpiParams pe = to_epi(epi);
+  const int M = g->N * g->P * g->Q, N = g->K, K = g->R * g->S * g->C;
+  const int bbn = N >= 256 ? 256 : 128;  // fp8 always runs the LDS-DMA kernel (edges are clamped)
+  if (bbn != bn || g->C % 128 || pe.remap || M < 1) return hipErrorInvalidValue;
+  const big::DenseP pb{w8, K, N};
+  if (is_pointwise(g)) {
+    const big::DenseP pa{x8, g->C, M};
+    if (bbn == 256) return big::launch<256, big::OpDenseK<128, 1>, big::OpDenseK<128, 1>, 1>(pa, pb, pe, M, N, K, 1, st);
+    return big::launch<128, big::OpDenseK<128, 1>, big::OpDenseK<64, 1>, 1>(pa, pb, pe, M, N, K, 1, st);
+  }
+  const big::ConvP pa = conv_params(x8, g->H, g->W, g->C, g->P, g->Q, g, M);
+  if (bbn == 256) return big::launch<256, big::OpConvK<128, 1, false>, big::OpDenseK<128, 1>, 1>(pa, pb, pe, M, N, K, 1, st);
+  return big::launch<128, big::OpConvK<128, 1, false>, big::OpDenseK<64, 1>, 1>(pa, pb, pe, M, N, K, 1, st);
+}
+
+// fp8 GEMM C[M,N] = A[M,K] . B[N,K]^T (both K-major fp8; a_fmt 0 = e4m3, 1 = e5m2; B e4m3),
+// K % 128 == 0, fused bf16 epilogue or fp32 (split-K slab) output like ttdk_gemm_bf16.
+TTDK_EXPORT int ttdk_gemm_fp8(const uint8_t* A, long long lda, const uint8_t* B, long long ldb, int a_fmt, int M,
+                              int N, int K, int splits, const TtdkEpilogue* epi, hipStream_t st) {
+  EpiParams pe = to_epi(epi);
+  const int bbn = N >= 256 ? 256 : 128;  // fp8 always runs the LDS-DMA kernel (edges are clamped)
+  if (M < 1 || N < 1 || K % 128 || lda % 16 || ldb % 16 || pe.remap) return hipErrorInvalidValue;
+  const big::DenseP pa{A, lda, M}, pb{B, ldb, N};
+#define TTDK_F8(BN_, BH_, F_) \
+  return big::launch<BN_, big::OpDenseK<128, 1>, big::OpDenseK<BH_, 1>, F_>(pa, pb, pe, M, N, K, splits, st)
+  if (bbn == 256) {
+    if (a_fmt) TTDK_F8(256, 128, 2);
+    TTDK_F8(256, 128, 1);
+  }
+  if (a_fmt) TTDK_F8(128, 64, 2);
+  TTDK_F8(128, 64, 1);
+#undef TTDK_F8
 }
 
 // dx[N,H,W,C] = conv_transpose(dy[N,P,Q,K], w): wt must hold w transposed to [C][R][S][K]
@@ -1210,8 +1496,10 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
     const int M = g->N * g->P * g->Q;
     if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
     DenseParams pa{dy, g->K, M, K};
-    if (g->sh == 1 && g->sw == 1 && (bm == 0 || bm == 256) && big_fits(M, N, K) && pe.stat == nullptr)
-      return big::launch<true, true>(dy, g->K, wt, K, pe, M, N, K, 1, st);
+    const int bbn = big_bn(M, N, K);
+    if (g->sh == 1 && g->sw == 1 && (bm == 0 || bm == 256) && bbn && pe.stat == nullptr)
+      return bbn == 256 ? big::dense<256>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st)
+                        : big::dense<128>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st);
     if (bm == 256) bm = bn = 0, pick_tile(M, N, &bm, &bn);
     if (g->sh != 1 || g->sw != 1) {
       if (g->sh != g->sw) return hipErrorInvalidValue;
@@ -1225,6 +1513,17 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
     return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
   }
   const int M = g->N * g->H * g->W;
+  const int bbn = big_bn(M, N, K);
+  // unit-stride dgrad gathers on the LDS-DMA kernel (strided ones keep the 4-wave kernel: the
+  // divisibility test costs registers the 256-row tile does not have)
+  if ((bm == 0 || bm == 256) && bbn && g->K % 64 == 0 && pe.stat == nullptr && !pe.remap && g->sh == 1 &&
+      g->sw == 1) {
+    const big::ConvP pa = conv_params(dy, g->P, g->Q, g->K, g->H, g->W, g, M);
+    const big::DenseP pb2{wt, K, N};
+    if (bbn == 256)
+      return big::launch<256, big::OpConvK<128, 2, true, true>, big::OpDenseK<128, 2>>(pa, pb2, pe, M, N, K, 1, st);
+    return big::launch<128, big::OpConvK<128, 2, true, true>, big::OpDenseK<64, 2>>(pa, pb2, pe, M, N, K, 1, st);
+  }
   if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
   GatherParams pa{dy, g->P, g->Q, g->K, g->H, g->W, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};
   return dispatch<KConvDgrad, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
@@ -1236,7 +1535,7 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
                                 int splits, int beta, int bm, int bn, hipStream_t st) {
   const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
   if (g->C % 8 || g->K % 8) return hipErrorInvalidValue;
-  const bool use_big = is_pointwise(g) && (bm == 0 || bm == 256) && big_fits(M, N, K);
+  const int bbn = (bm == 0 || bm == 256) ? big_bn(M, N, K) : 0;
   if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
   const int ktiles = ceil_div(K, BK);
   if (splits < 1) splits = 1;
@@ -1258,8 +1557,14 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
   }
   DenseParams pa{dy, g->K, M, K};
   hipError_t e;
-  if (use_big) {
-    e = big::launch<false, false>(dy, g->K, x, g->C, pe, M, N, K, splits, st);
+  if (bbn && is_pointwise(g)) {
+    e = bbn == 256 ? big::dense<256>(dy, g->K, false, x, g->C, false, pe, M, N, K, splits, st)
+                   : big::dense<128>(dy, g->K, false, x, g->C, false, pe, M, N, K, splits, st);
+  } else if (bbn) {
+    const big::DenseP pa2{dy, g->K, M};
+    const big::ConvP pb2 = conv_params(x, g->H, g->W, g->C, g->P, g->Q, g, N);
+    e = bbn == 256 ? big::launch<256, big::OpDenseMN<128>, big::OpWgradMN<128>>(pa2, pb2, pe, M, N, K, splits, st)
+                   : big::launch<128, big::OpDenseMN<128>, big::OpWgradMN<64>>(pa2, pb2, pe, M, N, K, splits, st);
   } else if (is_pointwise(g)) {
     DenseParams pb{x, g->C, N, K};
     e = dispatch<MNDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);

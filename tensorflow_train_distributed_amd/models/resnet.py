@@ -142,8 +142,9 @@ class ResNet:
         M = N * Pp * Q
         bm = 128 if M > 64 else 64
         bn = 128 if c.cout > 64 else 64
-        if c.k == 1 and c.stride == 1 and G.big_fits(M, c.cout, c.cin_store):
-            bm = bn = 256  # 1x1 conv on the 256x256 LDS-DMA GEMM (stat rows per 256-pixel tile)
+        big = G.big_bn(M, c.cout, c.k * c.k * c.cin_store)
+        if big and c.cin_store % 64 == 0:
+            bm, bn = 256, big  # 256-row LDS-DMA kernel (BN stat rows per 256-pixel tile)
         T = -(-M // bm)
         partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
         y = G.conv_fwd(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad), stat=partial,

@@ -50,9 +50,16 @@ def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat
     return e
 
 
+def big_bn(M, N, K):
+    """Mirror of the C++ big_bn(): tile width (256 / 128) of the 256-row LDS-DMA kernel for an
+    M x N x K GEMM, or 0 when the 4-wave kernel is used."""
+    if M < 256 or N < 128 or K % 64 or N % 8 or M * N < (1 << 20):
+        return 0
+    return 256 if N >= 256 else 128
+
+
 def big_fits(M, N, K):
-    """Mirror of the C++ rule selecting the 256x256 LDS-DMA GEMM kernel."""
-    return M >= 256 and N >= 256 and K % 64 == 0 and M * N >= (1 << 20)
+    return big_bn(M, N, K) != 0
 
 
 def effective_splits(K, splits, bk=64):
@@ -126,10 +133,10 @@ def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
     """Split-K factor for a weight-gradient GEMM (long K = tokens, small M x N). Mirrors the
     launcher's kernel choice: the 256x256 LDS-DMA kernel (M, N >= 256, M*N >= 2^20, one
     workgroup per CU -> aim for ~1-2 waves of 256 workgroups) or the 4-wave 128x128 kernel."""
-    if M >= 256 and N >= 256 and M * N >= (1 << 20) and K % 64 == 0:
-        tiles = -(-M // 256) * -(-N // 256)
-        ktiles = K // 64
-        return max(1, min(ktiles // 32, -(-256 // tiles)))
+    bbn = big_bn(M, N, K)
+    if bbn:
+        tiles = -(-M // 256) * -(-N // bbn)
+        return max(1, min((K // 64) // 32, -(-256 // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
@@ -195,11 +202,11 @@ def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
     """Split-K factor for the weight gradient: enough blocks to fill 256 CUs twice, but every
     split keeps >= min_ktiles K-steps (the slab write + reduce is pure overhead)."""
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
-    pointwise = g.R == 1 and g.S == 1 and g.sh == 1 and g.sw == 1 and g.ph == 0 and g.pw == 0
-    if pointwise and big_fits(M, N, K):  # mirrors ttdk_conv_wgrad's choice of the 256x256 kernel
+    bbn = big_bn(M, N, K)
+    if bbn:  # mirrors ttdk_conv_wgrad's choice of the 256-row LDS-DMA kernel
         # ~1 wave of 256 workgroups, but >= 32 K-tiles per split: fp32 slabs cost 8 B per output
         # element per split (write + reduce read)
-        tiles = -(-M // 256) * -(-N // 256)
+        tiles = -(-M // 256) * -(-N // bbn)
         return max(1, min((K // 64) // 32, -(-256 // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
@@ -225,4 +232,53 @@ def conv_wgrad(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=
         ws = torch.empty((splits,) + tuple(w_shape), dtype=torch.float32, device=x.device)
     _lib.call("ttdk_conv_wgrad", x.data_ptr(), dy.data_ptr(), ctypes.byref(g), out.data_ptr(),
               ws.data_ptr() if ws is not None else None, splits, beta, tile[0], tile[1], _lib.stream())
+    return out
+
+
+# ------------------------------------------------------------------ fp8 (gfx950 block-scaled MFMA)
+_lib.register({
+    "ttdk_conv_fwd_fp8": [_lib.P, _lib.P, _lib.G, _lib.I, _lib.E, _lib.P],
+    "ttdk_gemm_fp8": [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.I, _lib.I, _lib.E, _lib.P],
+})
+
+
+def gemm_fp8(a8, b8, *, alpha=1.0, out=None, out_dtype=torch.bfloat16, bias=None, act=ACT_NONE, residual=None,
+             beta=0, splits=1, a_e5m2=False, aux=None):
+    """C[M, N] = alpha * A[M, K] . B[N, K]^T with fp8 operands (uint8 storage: OCP e4m3, or
+    e5m2 for A when a_e5m2); alpha carries the per-tensor dequantisation scales."""
+    M, K = a8.shape
+    N, Kb = b8.shape
+    if K != Kb or a8.dtype != torch.uint8 or b8.dtype != torch.uint8:
+        raise ValueError("gemm_fp8 wants uint8 [M,K] x [N,K]")
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=a8.device)
+    if out.dtype == torch.float32:
+        splits = effective_splits(K, splits, bk=128)
+        if splits > 1:
+            ws = torch.empty((splits, M, N), dtype=torch.float32, device=a8.device)
+            e = _epi(ws, mode=1, ldo=N, slab_stride=M * N, alpha=alpha)
+            _lib.call("ttdk_gemm_fp8", a8.data_ptr(), a8.stride(0), b8.data_ptr(), b8.stride(0), int(a_e5m2), M, N, K,
+                      splits, ctypes.byref(e), _lib.stream())
+            _lib.call("ttdk_splitk_reduce", ws.data_ptr(), splits, M * N, out.data_ptr(), beta, _lib.stream())
+            return out
+        e = _epi(out, mode=2, beta=beta, alpha=alpha)
+    else:
+        e = _epi(out, bias=bias, residual=residual, act=act, beta=beta, alpha=alpha, aux=aux)
+    _lib.call("ttdk_gemm_fp8", a8.data_ptr(), a8.stride(0), b8.data_ptr(), b8.stride(0), int(a_e5m2), M, N, K, 1,
+              ctypes.byref(e), _lib.stream())
+    return out
+
+
+def conv_fwd_fp8(x8, w8, stride=(1, 1), padding=(0, 0), *, alpha=1.0, out=None, stat=None, residual=None,
+                 act=ACT_NONE):
+    """fp8 e4m3 implicit-GEMM conv: x8 [N,H,W,C] uint8, w8 [K,R,S,C] uint8, C % 128 == 0; bf16
+    output with the fused epilogue (stat rows per 256-pixel tile)."""
+    g = conv_geom(x8.shape, w8.shape, stride, padding)
+    if out is None:
+        out = torch.empty((g.N, g.P, g.Q, g.K), dtype=torch.bfloat16, device=x8.device)
+    M, N, K = g.N * g.P * g.Q, g.K, g.R * g.S * g.C
+    bn = 256 if N >= 256 else 128
+    _log("fwd8_%dx%d_s%d" % (g.R, g.S, g.sh), M, N, K)
+    e = _epi(out, ldo=g.K, residual=residual, act=act, stat=stat, alpha=alpha)
+    _lib.call("ttdk_conv_fwd_fp8", x8.data_ptr(), w8.data_ptr(), ctypes.byref(g), bn, ctypes.byref(e), _lib.stream())
     return out

@@ -52,6 +52,12 @@ CONVS = [
     (2, 14, 14, 64, 128, 1, 2, 0),
     (2, 32, 32, 8, 64, 7, 2, 3),
     (3, 7, 7, 512, 512, 3, 1, 1),
+    # 256-row LDS-DMA paths (fwd BN=128 gather; fwd/dgrad/wgrad BN=256 gathers; strided gathers)
+    (8, 32, 32, 64, 128, 3, 1, 1),
+    (16, 16, 16, 256, 256, 3, 1, 1),
+    (16, 32, 32, 128, 256, 3, 2, 1),
+    (16, 32, 32, 256, 512, 1, 2, 0),
+    (16, 16, 16, 128, 256, 1, 1, 0),
 ]
 
 
@@ -85,6 +91,62 @@ def test_conv_fwd_dgrad_wgrad(cfg):
     assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 1e-2
     dw1 = G.conv_wgrad(x, dy, w.shape, (s, s), (p, p), splits=1)
     assert _rel(dw1, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_conv_bn_stat_epilogue_big_tile():
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(4)
+    x = torch.randn(16, 16, 16, 128, device="cuda").bfloat16()
+    w = (torch.randn(256, 3, 3, 128, device="cuda") / 34).bfloat16()
+    M = 16 * 16 * 16
+    assert G.big_bn(M, 256, 9 * 128) == 256
+    stat = torch.zeros((M + 255) // 256, 2, 256, device="cuda")
+    y = G.conv_fwd(x, w, (1, 1), (1, 1), stat=stat, tile=(256, 256))
+    ref = F.conv2d(_nchw(x.float()), w.float().permute(0, 3, 1, 2), padding=1)
+    assert _rel(y, _nhwc(ref)) < 1e-2
+    s = stat.sum(0)
+    yf = y.float().reshape(-1, 256)
+    torch.testing.assert_close(s[0], yf.sum(0), rtol=1e-3, atol=2e-2)
+    torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=1e-3, atol=2e-2)
+
+
+def _q8(t, e5m2=False):
+    """Per-tensor scaled fp8 quantisation; returns (uint8 codes, dequantised fp32, inv scale)."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    fmax = 57344.0 if e5m2 else 448.0
+    amax = float(t.float().abs().max())
+    scale = torch.tensor([fmax / amax], device="cuda")
+    q = K.quant_fp8(t.bfloat16().contiguous(), scale, e5m2=e5m2)
+    deq = K.dequant_fp8(q, scale, e5m2=e5m2).float()  # dequant divides by the quant scale
+    return q, deq, 1.0 / float(scale)
+
+
+@pytest.mark.parametrize("M,N,K,e5m2", [(512, 768, 512, False), (1024, 128, 256, False), (300, 520, 384, True)])
+def test_gemm_fp8_block_scaled_mfma(M, N, K, e5m2):
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(M + N)
+    a, b = torch.randn(M, K, device="cuda"), torch.randn(N, K, device="cuda")
+    a8, ad, sa = _q8(a, e5m2)
+    b8, bd, sb = _q8(b)
+    ref = ad @ bd.t()
+    y = G.gemm_fp8(a8, b8, alpha=sa * sb, a_e5m2=e5m2)
+    assert _rel(y, ref) < 1e-2
+    y32 = G.gemm_fp8(a8, b8, alpha=sa * sb, a_e5m2=e5m2, out_dtype=torch.float32, splits=2)
+    assert _rel(y32, ref) < 5e-3  # reference operands are bf16-rounded dequantisations
+
+
+@pytest.mark.parametrize("cfg", [(16, 16, 16, 128, 256, 3, 1, 1), (16, 32, 32, 256, 128, 1, 1, 0)])
+def test_conv_fwd_fp8(cfg):
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    N, H, W, C, K, R, s, p = cfg
+    torch.manual_seed(5)
+    x = torch.randn(N, H, W, C, device="cuda")
+    w = torch.randn(K, R, R, C, device="cuda") / (R * R * C) ** 0.5
+    x8, xd, sx = _q8(x)
+    w8, wd, sw = _q8(w)
+    ref = F.conv2d(_nchw(xd), wd.permute(0, 3, 1, 2), stride=s, padding=p)
+    y = G.conv_fwd_fp8(x8, w8, (s, s), (p, p), alpha=sx * sw)
+    assert _rel(y, _nhwc(ref)) < 1e-2
 
 
 def test_conv_bn_stat_epilogue():
