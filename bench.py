@@ -31,7 +31,7 @@ def build_resnet(args, dev, rank, world):
     from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer, broadcast_flat_
     from tensorflow_train_distributed_amd.train.flat import FlatSGD, Schedule
 
-    B = args.batch or 256
+    B = args.batch or 512  # per-GPU batch sized for 288 GB HBM3E (larger tiles, fewer launches per image)
     model = resnet50(device=dev, seed=1234)
     broadcast_flat_(model.params)
     opt = FlatSGD(model.params, Schedule(kind=2, base_lr=0.1 * B * world / 256, warmup_steps=5, end_lr=0.0,
@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert"])
-    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = model default: 256 / 32)")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = model default: 512 / 32)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--graph", type=int, default=-1, help="hipGraph-capture the step (1/0, -1 = auto)")

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(kThreads) void stats_partial_kernel(const bf16_t* _
 // Backward partial sums: g = dy * [out > 0] (relu) ; sums of g and g*y. Optionally writes g.
 __global__ __launch_bounds__(kThreads) void bwd_partial_kernel(const bf16_t* __restrict__ dy,
                                                                const bf16_t* __restrict__ out,
+                                                               const uint8_t* __restrict__ mask,
                                                                const bf16_t* __restrict__ y, long long M, int C,
                                                                float* __restrict__ partial, long long rows_per_block,
                                                                bf16_t* __restrict__ g_out) {
@@ -90,7 +91,12 @@ __global__ __launch_bounds__(kThreads) void bwd_partial_kernel(const bf16_t* __r
         float g[8], yv[8];
         uint4 graw = *reinterpret_cast<const uint4*>(dy + off);
         unpack8(graw, g);
-        if (out) {
+        if (mask) {
+          const uint32_t mb = mask[off >> 3];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
+          if (g_out) *reinterpret_cast<uint4*>(g_out + off) = pack8(g);
+        } else if (out) {
           float o[8];
           unpack8(*reinterpret_cast<const uint4*>(out + off), o);
 #pragma unroll
@@ -189,7 +195,7 @@ __global__ void bwd_finalize_kernel(const float* __restrict__ sums, float count,
 __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
                                                          const bf16_t* __restrict__ residual, bf16_t* __restrict__ out,
-                                                         long long n8, int C, int relu) {
+                                                         uint8_t* __restrict__ mask, long long n8, int C, int relu) {
   const int cg = C >> 3;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n8;
        i += static_cast<long long>(gridDim.x) * blockDim.x) {
@@ -213,13 +219,25 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
     }
-    reinterpret_cast<uint4*>(out)[i] = pack8(f);
+    const uint4 packed = pack8(f);
+    reinterpret_cast<uint4*>(out)[i] = packed;
+    if (mask) {  // 1 bit per element of [stored bf16 > 0]: the ReLU mask backward reads instead of `out`
+      const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
+      uint32_t mb = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+        mb |= ((h & 0x7fffu) != 0 && !(h & 0x8000u) ? 1u : 0u) << j;
+      }
+      mask[i] = static_cast<uint8_t>(mb);
+    }
   }
 }
 
 // dz = a*g + b*y + c, g = dy * [out > 0] if out given.
 __global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ out,
+                                                             const uint8_t* __restrict__ mask,
                                                              const bf16_t* __restrict__ y,
                                                              const float* __restrict__ coef, bf16_t* __restrict__ dz,
                                                              long long n8, int C) {
@@ -229,7 +247,11 @@ __global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __res
     const int c0 = static_cast<int>(i % cg) * 8;
     float g[8], yv[8];
     unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
-    if (out) {
+    if (mask) {
+      const uint32_t mb = mask[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
+    } else if (out) {
       float o[8];
       unpack8(reinterpret_cast<const uint4*>(out)[i], o);
 #pragma unroll
@@ -273,11 +295,13 @@ TTDK_EXPORT int ttdk_bn_stats_partial(const bf16_t* x, long long M, int C, float
   return hipGetLastError();
 }
 
-TTDK_EXPORT int ttdk_bn_bwd_partial(const bf16_t* dy, const bf16_t* out, const bf16_t* y, long long M, int C,
-                                    float* partial, int nblocks, bf16_t* g_out, hipStream_t st) {
+// ReLU mask source: `mask` (1 bit per element, written by ttdk_bn_apply) if given, else `out`.
+TTDK_EXPORT int ttdk_bn_bwd_partial(const bf16_t* dy, const bf16_t* out, const uint8_t* mask, const bf16_t* y,
+                                    long long M, int C, float* partial, int nblocks, bf16_t* g_out, hipStream_t st) {
   if (C % 8) return hipErrorInvalidValue;
   const long long rpb = (M + nblocks - 1) / nblocks;
-  hipLaunchKernelGGL(bwd_partial_kernel, dim3(nblocks), dim3(kThreads), 0, st, dy, out, y, M, C, partial, rpb, g_out);
+  hipLaunchKernelGGL(bwd_partial_kernel, dim3(nblocks), dim3(kThreads), 0, st, dy, out, mask, y, M, C, partial, rpb,
+                     g_out);
   return hipGetLastError();
 }
 
@@ -311,18 +335,18 @@ TTDK_EXPORT int ttdk_bn_bwd_finalize(const float* sums, float count, int C, cons
 }
 
 TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* shift, const bf16_t* residual,
-                              bf16_t* out, long long n, int C, int relu, hipStream_t st) {
+                              bf16_t* out, uint8_t* mask, long long n, int C, int relu, hipStream_t st) {
   if (C % 8 || n % 8) return hipErrorInvalidValue;
   const long long n8 = n / 8;
-  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, y, scale, shift, residual, out, n8, C,
-                     relu);
+  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, n8,
+                     C, relu);
   return hipGetLastError();
 }
 
-TTDK_EXPORT int ttdk_bn_bwd_apply(const bf16_t* dy, const bf16_t* out, const bf16_t* y, const float* coef, bf16_t* dz,
-                                  long long n, int C, hipStream_t st) {
+TTDK_EXPORT int ttdk_bn_bwd_apply(const bf16_t* dy, const bf16_t* out, const uint8_t* mask, const bf16_t* y,
+                                  const float* coef, bf16_t* dz, long long n, int C, hipStream_t st) {
   if (C % 8 || n % 8) return hipErrorInvalidValue;
   const long long n8 = n / 8;
-  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, dy, out, y, coef, dz, n8, C);
+  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, n8, C);
   return hipGetLastError();
 }

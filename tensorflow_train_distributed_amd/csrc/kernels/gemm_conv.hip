@@ -1289,6 +1289,12 @@ inline int big_bn(int M, int N, int K) {
   return N >= 256 ? 256 : 128;
 }
 inline bool big_fits(int M, int N, int K) { return big_bn(M, N, K) != 0; }
+// Weight gradients have a long K (pixels) and split-K fills the machine, so only the tile
+// shape (not M*N) decides.
+inline int big_bn_wgrad(int M, int N, int K) {
+  if (M < 256 || N < 128 || K % 64 || N % 8) return 0;
+  return N >= 256 ? 256 : 128;
+}
 
 inline void pick_tile(int M, int N, int* bm, int* bn) {
   *bm = (M <= 64) ? 64 : 128;
@@ -1535,7 +1541,7 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
                                 int splits, int beta, int bm, int bn, hipStream_t st) {
   const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
   if (g->C % 8 || g->K % 8) return hipErrorInvalidValue;
-  const int bbn = (bm == 0 || bm == 256) ? big_bn(M, N, K) : 0;
+  const int bbn = (bm == 0 || bm == 256) ? big_bn_wgrad(M, N, K) : 0;
   if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
   const int ktiles = ceil_div(K, BK);
   if (splits < 1) splits = 1;

@@ -155,21 +155,22 @@ class ResNet:
         K.bn_fwd_finalize(sums, M, P.var[pre + "gamma"], P.var[pre + "beta"], self.bn_eps, self.bn_momentum,
                           P.var[pre + "moving_mean"], P.var[pre + "moving_variance"], st)
         y2 = y.view(M, c.cout)
+        mask = torch.empty(M * c.cout // 8, dtype=torch.uint8, device=x.device) if relu else None
         out = K.bn_apply(y2, st.scale, st.shift, residual=None if residual is None else residual.view(M, c.cout),
-                         relu=relu).view(N, Pp, Q, c.cout)
-        return out, (x, y, out if relu else None, st)
+                         relu=relu, mask=mask).view(N, Pp, Q, c.cout)
+        return out, (x, y, mask, st)
 
     def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0):
         from ..ops import gemm as G
         from ..ops import kernels as K
         P = self.params
-        x, y, out, st = ctx
+        x, y, mask, st = ctx
         N, Pp, Q, Kc = y.shape
         M = N * Pp * Q
         pre = c.name + "_bn/"
-        dz = K.bn_backward(dout.view(M, Kc), None if out is None else out.view(M, Kc), y.view(M, Kc),
-                           P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
-                           g_out=None if g_out is None else g_out.view(M, Kc)).view(N, Pp, Q, Kc)
+        dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
+                           P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
+                           mask=mask).view(N, Pp, Q, Kc)
         wname = c.name + "_conv/kernel"
         G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
         self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group

@@ -55,12 +55,12 @@ _SIGS = {
     # batchnorm.hip
     "ttdk_bn_num_partials": [L, I],
     "ttdk_bn_stats_partial": [P, L, I, P, I, P],
-    "ttdk_bn_bwd_partial": [P, P, P, L, I, P, I, P, P],
+    "ttdk_bn_bwd_partial": [P, P, P, P, L, I, P, I, P, P],
     "ttdk_bn_reduce_partials": [P, I, I, P, P],
     "ttdk_bn_fwd_finalize": [P, F, I, P, P, F, F, P, P, P, P, P, P, P],
     "ttdk_bn_bwd_finalize": [P, F, I, P, P, P, P, P, P, I, P],
-    "ttdk_bn_apply": [P, P, P, P, P, L, I, I, P],
-    "ttdk_bn_bwd_apply": [P, P, P, P, P, L, I, P],
+    "ttdk_bn_apply": [P, P, P, P, P, P, L, I, I, P],
+    "ttdk_bn_bwd_apply": [P, P, P, P, P, P, L, I, P],
     # pool.hip
     "ttdk_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "ttdk_maxpool_bwd": [P, P, P] + [I] * 12 + [P],

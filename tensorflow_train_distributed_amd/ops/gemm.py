@@ -62,6 +62,13 @@ def big_fits(M, N, K):
     return big_bn(M, N, K) != 0
 
 
+def big_bn_wgrad(M, N, K):
+    """Mirror of the C++ big_bn_wgrad() (conv weight gradients: long K, split-K)."""
+    if M < 256 or N < 128 or K % 64 or N % 8:
+        return 0
+    return 256 if N >= 256 else 128
+
+
 def effective_splits(K, splits, bk=64):
     """Mirror of the kernel launcher's split-K clamping (every split gets >= 1 K-tile)."""
     kt = -(-K // bk)
@@ -202,7 +209,7 @@ def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
     """Split-K factor for the weight gradient: enough blocks to fill 256 CUs twice, but every
     split keeps >= min_ktiles K-steps (the slab write + reduce is pure overhead)."""
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
-    bbn = big_bn(M, N, K)
+    bbn = big_bn_wgrad(M, N, K)
     if bbn:  # mirrors ttdk_conv_wgrad's choice of the 256-row LDS-DMA kernel
         # ~1 wave of 256 workgroups, but >= 32 K-tiles per split: fp32 slabs cost 8 B per output
         # element per split (write + reduce read)

@@ -59,31 +59,35 @@ def bn_fwd_finalize(sums, count, gamma, beta, eps, momentum, running_mean, runni
               state.scale.data_ptr(), state.shift.data_ptr(), _s())
 
 
-def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None):
+def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None, mask=None):
+    """out = act(y*scale + shift (+ residual)); `mask` (uint8 [M*C/8]) optionally receives the
+    ReLU mask as bits so the backward need not re-read `out`."""
     M, C = y2d.shape
     if out is None:
         out = torch.empty_like(y2d)
     _lib.call("ttdk_bn_apply", y2d.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(residual), out.data_ptr(),
-              M * C, C, int(relu), _s())
+              _p(mask), M * C, C, int(relu), _s())
     return out
 
 
-def bn_backward(dout, out_for_relu, y, gamma, state, dgamma, dbeta, *, g_out=None, dz=None, accumulate=False):
+def bn_backward(dout, out_for_relu, y, gamma, state, dgamma, dbeta, *, g_out=None, dz=None, accumulate=False,
+                mask=None):
     """dz = BN-backward(relu-mask(dout)). Writes dgamma/dbeta (fp32 [C]) and optionally the
-    relu-masked gradient g_out (needed by residual shortcuts)."""
+    relu-masked gradient g_out (needed by residual shortcuts). The ReLU mask comes from the
+    bit mask written by bn_apply (if given) or from `out_for_relu > 0`."""
     M, C = y.shape
     T = bn_num_partials(M, C)
     partial = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
-    _lib.call("ttdk_bn_bwd_partial", dout.data_ptr(), _p(out_for_relu), y.data_ptr(), M, C, partial.data_ptr(), T,
-              _p(g_out), _s())
+    _lib.call("ttdk_bn_bwd_partial", dout.data_ptr(), _p(out_for_relu), _p(mask), y.data_ptr(), M, C,
+              partial.data_ptr(), T, _p(g_out), _s())
     sums = bn_reduce_partials(partial, T, C)
     coef = torch.empty((3, C), dtype=torch.float32, device=y.device)
     _lib.call("ttdk_bn_bwd_finalize", sums.data_ptr(), float(M), C, _p(gamma), state.mean.data_ptr(),
               state.rstd.data_ptr(), _p(dgamma), _p(dbeta), coef.data_ptr(), int(accumulate), _s())
     if dz is None:
         dz = torch.empty_like(y)
-    _lib.call("ttdk_bn_bwd_apply", dout.data_ptr(), _p(out_for_relu), y.data_ptr(), coef.data_ptr(), dz.data_ptr(),
-              M * C, C, _s())
+    _lib.call("ttdk_bn_bwd_apply", dout.data_ptr(), _p(out_for_relu), _p(mask), y.data_ptr(), coef.data_ptr(),
+              dz.data_ptr(), M * C, C, _s())
     return dz
 
 

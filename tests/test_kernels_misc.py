@@ -43,6 +43,16 @@ def test_batchnorm_fwd_bwd_relu_residual():
     assert _rel(dg, g_r.grad) < 1e-2
     assert _rel(db, b_r.grad) < 1e-2
     assert _rel(g_sc, dout.float() * (out.float() > 0)) < 1e-6
+    # bit-mask ReLU path (what the ResNet engine uses): identical results without re-reading out
+    mask = torch.empty(M * C // 8, dtype=torch.uint8, device="cuda")
+    out2 = K.bn_apply(y, st.scale, st.shift, residual=res, relu=True, mask=mask)
+    assert torch.equal(out2, out)
+    bits = ((mask[:, None].int() >> torch.arange(8, device="cuda")) & 1).reshape(M, C)
+    assert torch.equal(bits.bool(), out.float() > 0)
+    dg2, db2, g_sc2 = torch.empty_like(dg), torch.empty_like(db), torch.empty_like(dout)
+    dz2 = K.bn_backward(dout, None, y, gamma, st, dg2, db2, g_out=g_sc2, mask=mask)
+    assert torch.equal(dz2, dz) and torch.equal(g_sc2, g_sc)
+    torch.testing.assert_close(dg2, dg) and torch.testing.assert_close(db2, db)
 
 
 def test_maxpool_avgpool():

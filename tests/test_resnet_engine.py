@@ -83,8 +83,11 @@ def test_convbn_unit_backward_oracle(which):
     dout = torch.randn_like(out)
     m._grad_hook = None
     dx = m._convbn_bwd(c, dout, ctx, need_dx=which != "stem")
-    _, y, o, st = ctx
-    g = dout.float() * (o.float() > 0) if relu else dout.float()
+    _, y, mask, st = ctx
+    g = dout.float() * (out.float() > 0) if relu else dout.float()
+    if relu:  # the saved bit mask is exactly [out > 0]
+        bits = ((mask[:, None].int() >> torch.arange(8, device="cuda")) & 1).reshape(out.shape)
+        assert torch.equal(bits.bool(), out > 0)
     yf = y.float()
     xhat = (yf - st.mean) * st.rstd
     gamma = P.var[c.name + "_bn/gamma"]

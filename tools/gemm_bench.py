@@ -70,6 +70,13 @@ def main():
         bt = b.t() if tb else b
         ms = timeit(lambda: torch.matmul(at, bt))
         res.append("torch %.3f ms %.0f TF/s" % (ms, fl / ms / 1e9))
+        if not ta and tb and K % 128 == 0:  # fp8 e4m3 on the block-scaled MFMA (same NT layout)
+            from tensorflow_train_distributed_amd.ops import kernels as KK
+            one = torch.ones(1, device="cuda")
+            a8, b8 = KK.quant_fp8(a, one), KK.quant_fp8(b, one)
+            o8 = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+            ms = timeit(lambda: G.gemm_fp8(a8, b8, out=o8))
+            res.append("fp8 %.3f ms %.0f TF/s" % (ms, fl / ms / 1e9))
         # correctness spot check of the 256 path
         out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
         G.gemm(a, b, trans_a=ta, trans_b=tb, out=out, tile=(256, 256) if min(M, N) >= 256 else (128, 128))
