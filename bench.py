@@ -29,13 +29,17 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 def build_resnet(args, dev, rank, world):
     from tensorflow_train_distributed_amd.models.resnet import resnet50
     from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer, broadcast_flat_
-    from tensorflow_train_distributed_amd.train.flat import FlatSGD, Schedule
+    from tensorflow_train_distributed_amd.train.flat import FlatLAMB, FlatSGD, Schedule
 
     B = args.batch or 512  # per-GPU batch sized for 288 GB HBM3E (larger tiles, fewer launches per image)
-    model = resnet50(device=dev, seed=1234)
+    model = resnet50(device=dev, seed=1234, precision=args.precision)
     broadcast_flat_(model.params)
-    opt = FlatSGD(model.params, Schedule(kind=2, base_lr=0.1 * B * world / 256, warmup_steps=5, end_lr=0.0,
-                                         power=2.0, total_steps=10000), momentum=0.9, weight_decay=5e-5)
+    if args.optimizer == "lamb":  # large-batch recipe (BASELINE config 5)
+        opt = FlatLAMB(model.params, Schedule(kind=2, base_lr=0.01 * (B * world / 1024) ** 0.5, warmup_steps=5,
+                                              end_lr=0.0, power=2.0, total_steps=10000), weight_decay=5e-5)
+    else:
+        opt = FlatSGD(model.params, Schedule(kind=2, base_lr=0.1 * B * world / 256, warmup_steps=5, end_lr=0.0,
+                                             power=2.0, total_steps=10000), momentum=0.9, weight_decay=5e-5)
     reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb)
     g = torch.Generator(device=dev)
     g.manual_seed(rank)
@@ -52,12 +56,15 @@ def build_resnet(args, dev, rank, world):
         return sums
 
     info = {
-        "metric": "images/sec (whole node) ResNet-50 bf16 MirroredStrategy",
+        "metric": "images/sec (whole node) ResNet-50 %s MirroredStrategy" % args.precision,
         "unit": "images/sec",
         "data": "synthetic (random NHWC images + labels resident on GPU; random-init weights)",
         "config": {"model": "ResNet-50 v1.5", "global_batch": B * world, "per_gpu_batch": B, "image_size": S,
                    "seq_len": None, "parallelism": "dp%d" % world,
-                   "optimizer": "momentum-SGD 0.9, wd 5e-5, fp32 master"},
+                   "optimizer": ("LAMB wd 5e-5" if args.optimizer == "lamb" else "momentum-SGD 0.9, wd 5e-5")
+                   + ", fp32 master",
+                   "precision": "fp8 e4m3 forward convs (delayed scaling), bf16 backward" if args.precision == "fp8"
+                   else "bf16"},
     }
     return step, B, info
 
@@ -107,6 +114,8 @@ def main():
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--graph", type=int, default=-1, help="hipGraph-capture the step (1/0, -1 = auto)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"], help="ResNet conv forward precision")
+    ap.add_argument("--optimizer", default="momentum", choices=["momentum", "lamb"], help="ResNet optimizer")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -174,7 +183,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp8+bf16" if args.precision == "fp8" else "bf16",
             "data": info["data"],
             "config": cfg,
         }), flush=True)

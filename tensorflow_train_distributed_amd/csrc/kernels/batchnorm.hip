@@ -195,8 +195,12 @@ __global__ void bwd_finalize_kernel(const float* __restrict__ sums, float count,
 __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
                                                          const bf16_t* __restrict__ residual, bf16_t* __restrict__ out,
-                                                         uint8_t* __restrict__ mask, long long n8, int C, int relu) {
+                                                         uint8_t* __restrict__ mask, uint8_t* __restrict__ q8,
+                                                         float* __restrict__ q8_slot, long long n8, int C, int relu) {
   const int cg = C >> 3;
+  // fp8 e4m3 copy with the slot's delayed scale; this step's amax goes to q8_slot[1]
+  const float qs = q8 ? q8_slot[2] : 1.f;
+  float qmax = 0.f;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n8;
        i += static_cast<long long>(gridDim.x) * blockDim.x) {
     const int c0 = static_cast<int>(i % cg) * 8;
@@ -231,6 +235,24 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
       }
       mask[i] = static_cast<uint8_t>(mb);
     }
+    if (q8) {
+      float fq[8];
+      unpack8(packed, fq);
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        qmax = fmaxf(qmax, fabsf(fq[j]));
+        const float v = fminf(fmaxf(fq[j] * qs, -448.f), 448.f);
+        const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false) & 0xff);
+        if (j < 4) lo |= b << (8 * j);
+        else hi |= b << (8 * (j - 4));
+      }
+      reinterpret_cast<uint2*>(q8)[i] = make_uint2(lo, hi);
+    }
+  }
+  if (q8) {
+    qmax = wave_max(qmax);
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(q8_slot + 1), __float_as_uint(qmax));
   }
 }
 
@@ -334,12 +356,14 @@ TTDK_EXPORT int ttdk_bn_bwd_finalize(const float* sums, float count, int C, cons
   return hipGetLastError();
 }
 
+// q8/q8_slot (optional): also write an fp8 e4m3 copy of `out` (delayed scaling, see fp8.hip).
 TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* shift, const bf16_t* residual,
-                              bf16_t* out, uint8_t* mask, long long n, int C, int relu, hipStream_t st) {
-  if (C % 8 || n % 8) return hipErrorInvalidValue;
+                              bf16_t* out, uint8_t* mask, uint8_t* q8, float* q8_slot, long long n, int C, int relu,
+                              hipStream_t st) {
+  if (C % 8 || n % 8 || (q8 && !q8_slot)) return hipErrorInvalidValue;
   const long long n8 = n / 8;
-  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, n8,
-                     C, relu);
+  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, q8,
+                     q8_slot, n8, C, relu);
   return hipGetLastError();
 }
 

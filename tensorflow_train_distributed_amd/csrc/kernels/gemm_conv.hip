@@ -355,7 +355,16 @@ struct EpiParams {
   float* stat;  // BN partial sums: [tiles_m][2][N] (sum, sumsq) or null
   float alpha;  // scale applied to acc
   bf16_t* aux;  // optional: pre-activation copy (GELU backward input), row stride ldo
+  const float* ascale0;  // optional device scalars multiplied into alpha (fp8 dequant scales)
+  const float* ascale1;
 };
+
+__device__ __forceinline__ float epi_alpha(const EpiParams& E) {
+  float a = E.alpha;
+  if (E.ascale0) a *= *E.ascale0;
+  if (E.ascale1) a *= *E.ascale1;
+  return a;
+}
 
 __device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
   if (!E.remap) return m;
@@ -372,6 +381,7 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
   static_assert(BM * (BN * 2 + 16) + 4 * 2 * BN * 4 <= 2 * (BM + BN) * BK * 2, "staged epilogue must fit in LDS");
   constexpr int TM = BM / 32, TN = BN / 32;
   const int g = lane >> 4, i16 = lane & 15;
+  const float alpha_e = epi_alpha(E);
   if (E.mode != 0) {
     float* out = static_cast<float*>(E.out) + (E.mode == 1 ? split * E.slab_stride : 0);
 #pragma unroll
@@ -381,7 +391,7 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int n = nwave + tn * 16 + 4 * g;
-        f32x4_t v = acc[tm][tn] * E.alpha;
+        f32x4_t v = acc[tm][tn] * alpha_e;
         float* o = out + static_cast<long long>(m) * E.ldo + n;
         if (n + 3 < N && (E.ldo & 3) == 0) {
           if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
@@ -405,7 +415,7 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const int r = mwave - m0 + tm * 16 + i16, c = nwave - n0 + tn * 16 + 4 * g;
-      const f32x4_t v = acc[tm][tn] * E.alpha;
+      const f32x4_t v = acc[tm][tn] * alpha_e;
       uint2 w;
       w.x = pack_bf16x2(v[0], v[1]);
       w.y = pack_bf16x2(v[2], v[3]);
@@ -1071,6 +1081,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
 
   // ---------------------------------------------------------------- epilogue
   const int g = lane >> 4, i16 = lane & 15;
+  const float alpha_e = epi_alpha(E);
   if (E.mode != 0) {
     float* out = static_cast<float*>(E.out) + (E.mode == 1 ? blockIdx.y * E.slab_stride : 0);
 #pragma unroll
@@ -1084,7 +1095,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
 #pragma unroll
           for (int b = 0; b < NB; ++b) {
             const int n = n0 + hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
-            f32x4_t v = acc[ha][hb][a][b] * E.alpha;
+            f32x4_t v = acc[ha][hb][a][b] * alpha_e;
             float* o = out + static_cast<long long>(m) * E.ldo + n;
             if (n + 3 < N && (E.ldo & 3) == 0) {
               if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
@@ -1108,7 +1119,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
-          const f32x4_t v = acc[ha][hb][a][b] * E.alpha;
+          const f32x4_t v = acc[ha][hb][a][b] * alpha_e;
           *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) =
               make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         }
@@ -1347,6 +1358,8 @@ struct TtdkEpilogue {
   float* stat;
   float alpha;
   bf16_t* aux;  // optional second bf16 output: the pre-activation value (same layout as out)
+  const float* ascale0;  // optional device scalars multiplied into alpha (fp8 dequant scales)
+  const float* ascale1;
 };
 
 static EpiParams to_epi(const TtdkEpilogue* e) {
@@ -1369,6 +1382,8 @@ static EpiParams to_epi(const TtdkEpilogue* e) {
   p.stat = e->stat;
   p.alpha = e->alpha == 0.f ? 1.f : e->alpha;
   p.aux = e->aux;
+  p.ascale0 = e->ascale0;
+  p.ascale1 = e->ascale1;
   return p;
 }
 

@@ -66,8 +66,19 @@ class ConvSpec:
 
 
 class ResNet:
+    """precision="fp8" (BASELINE.json config 5): every conv whose input has a multiple of 128
+    channels runs its forward GEMM in fp8 e4m3 on the block-scaled MFMA
+    (ops.gemm.conv_fwd_fp8): the producing BN-apply pass writes an fp8 copy of its output
+    with a delayed per-tensor scale (device-side amax history, ops/fp8.hip), the conv weights
+    are re-quantised once per step with current per-tensor scaling, and the dequantisation
+    scales reach the GEMM epilogue as device pointers (no host sync, graph-capturable).
+    Backward (dgrad/wgrad) stays bf16 on the same saved bf16 activations."""
+
     def __init__(self, stages=STAGES_50, num_classes=1000, in_channels=3, device="cuda", seed=0,
-                 bn_momentum=0.9, bn_eps=1e-5, width=64):
+                 bn_momentum=0.9, bn_eps=1e-5, width=64, precision="bf16"):
+        if precision not in ("bf16", "fp8"):
+            raise ValueError("precision must be bf16 or fp8")
+        self.precision = precision
         self.device = torch.device(device)
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -91,6 +102,51 @@ class ResNet:
                 cin = mid * 4
         self.feat = cin
         self.params = FlatParams(self._specs(), self.device, seed=seed)
+        self._fp8 = None
+        if precision == "fp8" and self.device.type == "cuda":
+            self._init_fp8()
+
+    # ----------------------------------------------------------------- fp8 state
+    def _fp8_conv(self, c: ConvSpec) -> bool:
+        return self.precision == "fp8" and c.cin_store % 128 == 0
+
+    def _init_fp8(self):
+        P = self.params
+        convs = [c for c in self.conv_list() if self._fp8_conv(c)]
+        rows = []
+        self._w8_slot = {}
+        for i, c in enumerate(convs):
+            name = c.name + "_conv/kernel"
+            rows.append((P.offsets[name], int(np.prod(P.spec(name).shape)), i))
+            self._w8_slot[c.name] = i
+        arr = np.zeros(len(rows), dtype=np.dtype([("off", "<i8"), ("len", "<i4"), ("slot", "<i4")]))
+        for i, r in enumerate(rows):
+            arr[i] = r
+        self._w8_table = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
+        self._w8_n = len(rows)
+        self._w8_max = max(r[1] for r in rows)
+        self._w8_flat = torch.zeros(P.numel, dtype=torch.uint8, device=self.device)
+        self._w8_slots = torch.zeros((len(rows), 4), dtype=torch.float32, device=self.device)
+        self._w8 = {c.name: self._w8_flat[P.offsets[c.name + "_conv/kernel"]:P.offsets[c.name + "_conv/kernel"]
+                                          + int(np.prod(P.spec(c.name + "_conv/kernel").shape))]
+                    .view(P.spec(c.name + "_conv/kernel").shape) for c in convs}
+        # activation slots: one per fp8-consumed tensor, assigned in forward order
+        self._a_slots = torch.zeros((4 * len(self.blocks) + 4, 4), dtype=torch.float32, device=self.device)
+        self._a_slots[:, 2] = 1.0
+        self._a_slots[:, 3] = 1.0
+        self._fp8 = True
+
+    def _fp8_step_begin(self):
+        from ..ops import kernels as K
+        K.fp8_rollover(self._a_slots, margin=0.9)
+        K.fp8_quant_weights(self.params.compute, self._w8_flat, self._w8_table, self._w8_n, self._w8_max,
+                            self._w8_slots)
+        self._a_next = 0
+
+    def _new_a_slot(self):
+        i = self._a_next
+        self._a_next += 1
+        return self._a_slots[i]
 
     # ----------------------------------------------------------------- variables
     def _conv_specs(self, c: ConvSpec):
@@ -132,7 +188,10 @@ class ResNet:
         return out
 
     # ----------------------------------------------------------------- GPU engine
-    def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None):
+    def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False):
+        """conv + BN (+residual) (+ReLU). x8 = (fp8 copy of x, its scale slot) selects the fp8
+        forward GEMM; want8 makes the BN-apply pass also emit an fp8 copy of the output.
+        Returns (out, ctx) or (out, ctx, out8) when want8."""
         from ..ops import gemm as G
         from ..ops import kernels as K
         P = self.params
@@ -143,12 +202,21 @@ class ResNet:
         bm = 128 if M > 64 else 64
         bn = 128 if c.cout > 64 else 64
         big = G.big_bn(M, c.cout, c.k * c.k * c.cin_store)
-        if big and c.cin_store % 64 == 0:
+        use8 = x8 is not None and self._fp8_conv(c)
+        if use8:
+            bm, bn = 256, (256 if c.cout >= 256 else 128)
+        elif big and c.cin_store % 64 == 0:
             bm, bn = 256, big  # 256-row LDS-DMA kernel (BN stat rows per 256-pixel tile)
         T = -(-M // bm)
         partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
-        y = G.conv_fwd(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
-                       tile=(bm, bn))
+        if use8:
+            xq, xslot = x8
+            ws = self._w8_slots[self._w8_slot[c.name]]
+            y = G.conv_fwd_fp8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
+                               ascale=(xslot[3:4], ws[3:4]))
+        else:
+            y = G.conv_fwd(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
+                           tile=(bm, bn))
         sums = K.bn_reduce_partials(partial, T, c.cout)
         st = K.BNState(c.cout, x.device)
         pre = c.name + "_bn/"
@@ -156,8 +224,14 @@ class ResNet:
                           P.var[pre + "moving_mean"], P.var[pre + "moving_variance"], st)
         y2 = y.view(M, c.cout)
         mask = torch.empty(M * c.cout // 8, dtype=torch.uint8, device=x.device) if relu else None
+        q8 = slot = None
+        if want8:
+            q8 = torch.empty((N, Pp, Q, c.cout), dtype=torch.uint8, device=x.device)
+            slot = self._new_a_slot()
         out = K.bn_apply(y2, st.scale, st.shift, residual=None if residual is None else residual.view(M, c.cout),
-                         relu=relu, mask=mask).view(N, Pp, Q, c.cout)
+                         relu=relu, mask=mask, q8=q8, q8_slot=slot).view(N, Pp, Q, c.cout)
+        if want8:
+            return out, (x, y, mask, st), (q8, slot)
         return out, (x, y, mask, st)
 
     def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0):
@@ -199,18 +273,29 @@ class ResNet:
         if grad_scale is None:
             grad_scale = 1.0 / N
         x = images if images.shape[-1] == self.in_store else K.pad_channels(images.contiguous(), self.in_store)
+        fp8 = self._fp8 is not None
+        if fp8:
+            self._fp8_step_begin()
+
+        def unit(c, inp, relu, residual=None, inp8=None, want8=False):
+            r = self._convbn_fwd(c, inp, relu, residual=residual, x8=inp8, want8=want8)
+            return r if want8 else (r[0], r[1], None)
+
         # ---- forward
         s_out, s_ctx = self._convbn_fwd(self.stem, x, relu=True)
         h, arg = K.maxpool_fwd(s_out, 3, 2, 1)
+        h8 = None
         ctxs = []
-        for blk in self.blocks:
-            o1, c1 = self._convbn_fwd(blk["c1"], h, True)
-            o2, c2 = self._convbn_fwd(blk["c2"], o1, True)
+        for i, blk in enumerate(self.blocks):
+            nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]))
+            o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]))
             if blk["cd"] is not None:
-                sc, cd = self._convbn_fwd(blk["cd"], h, False)
+                sc, cd, _ = unit(blk["cd"], h, False, inp8=h8)
             else:
                 sc, cd = h, None
-            o3, c3 = self._convbn_fwd(blk["c3"], o2, True, residual=sc)
+            o3, c3, h8 = unit(blk["c3"], o2, True, residual=sc, inp8=o2_8,
+                              want8=fp8 and nxt is not None and self._fp8_conv(nxt["c1"]))
             ctxs.append((c1, c2, c3, cd))
             h = o3
         feat_shape = h.shape
@@ -292,4 +377,5 @@ class ResNet:
 
 
 def resnet50(num_classes=1000, device="cuda", **kw) -> ResNet:
+    """ResNet-50 v1.5; precision="fp8" for the fp8 forward path (config 5)."""
     return ResNet(STAGES_50, num_classes=num_classes, device=device, **kw)

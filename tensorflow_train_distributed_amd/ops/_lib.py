@@ -32,6 +32,7 @@ class Epilogue(ctypes.Structure):
         ("bias", c_void_p), ("residual", c_void_p), ("ldr", c_longlong), ("act", c_int),
         ("beta", c_int), ("remap", c_int), ("rP", c_int), ("rQ", c_int), ("rOH", c_int),
         ("rOW", c_int), ("rs", c_int), ("stat", c_void_p), ("alpha", c_float), ("aux", c_void_p),
+        ("ascale0", c_void_p), ("ascale1", c_void_p),
     ]
 
 
@@ -59,7 +60,7 @@ _SIGS = {
     "ttdk_bn_reduce_partials": [P, I, I, P, P],
     "ttdk_bn_fwd_finalize": [P, F, I, P, P, F, F, P, P, P, P, P, P, P],
     "ttdk_bn_bwd_finalize": [P, F, I, P, P, P, P, P, P, I, P],
-    "ttdk_bn_apply": [P, P, P, P, P, P, L, I, I, P],
+    "ttdk_bn_apply": [P, P, P, P, P, P, P, P, L, I, I, P],
     "ttdk_bn_bwd_apply": [P, P, P, P, P, P, L, I, P],
     # pool.hip
     "ttdk_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
@@ -88,6 +89,9 @@ _SIGS = {
     "ttdk_amax_bf16": [P, L, P, I, P],
     "ttdk_quant_fp8": [P, P, L, P, I, P],
     "ttdk_dequant_fp8": [P, P, L, P, I, P],
+    # fp8.hip
+    "ttdk_fp8_rollover": [P, I, F, F, P],
+    "ttdk_fp8_quant_weights": [P, P, P, I, I, P, I, P],
 }
 
 _fns = {}

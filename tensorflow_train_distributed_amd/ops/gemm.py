@@ -33,7 +33,7 @@ def _log(kind, M, N, K, splits=1):
 
 
 def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,
-         slab_stride=0, aux=None):
+         slab_stride=0, aux=None, ascale=(None, None)):
     e = _lib.Epilogue()
     e.mode = mode
     e.out = out.data_ptr()
@@ -47,6 +47,8 @@ def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat
     e.stat = stat.data_ptr() if stat is not None else None
     e.alpha = alpha
     e.aux = aux.data_ptr() if aux is not None else None
+    e.ascale0 = ascale[0].data_ptr() if ascale[0] is not None else None
+    e.ascale1 = ascale[1].data_ptr() if ascale[1] is not None else None
     return e
 
 
@@ -277,7 +279,7 @@ def gemm_fp8(a8, b8, *, alpha=1.0, out=None, out_dtype=torch.bfloat16, bias=None
 
 
 def conv_fwd_fp8(x8, w8, stride=(1, 1), padding=(0, 0), *, alpha=1.0, out=None, stat=None, residual=None,
-                 act=ACT_NONE):
+                 act=ACT_NONE, ascale=(None, None)):
     """fp8 e4m3 implicit-GEMM conv: x8 [N,H,W,C] uint8, w8 [K,R,S,C] uint8, C % 128 == 0; bf16
     output with the fused epilogue (stat rows per 256-pixel tile)."""
     g = conv_geom(x8.shape, w8.shape, stride, padding)
@@ -286,6 +288,6 @@ def conv_fwd_fp8(x8, w8, stride=(1, 1), padding=(0, 0), *, alpha=1.0, out=None, 
     M, N, K = g.N * g.P * g.Q, g.K, g.R * g.S * g.C
     bn = 256 if N >= 256 else 128
     _log("fwd8_%dx%d_s%d" % (g.R, g.S, g.sh), M, N, K)
-    e = _epi(out, ldo=g.K, residual=residual, act=act, stat=stat, alpha=alpha)
+    e = _epi(out, ldo=g.K, residual=residual, act=act, stat=stat, alpha=alpha, ascale=ascale)
     _lib.call("ttdk_conv_fwd_fp8", x8.data_ptr(), w8.data_ptr(), ctypes.byref(g), bn, ctypes.byref(e), _lib.stream())
     return out

@@ -59,15 +59,26 @@ def bn_fwd_finalize(sums, count, gamma, beta, eps, momentum, running_mean, runni
               state.scale.data_ptr(), state.shift.data_ptr(), _s())
 
 
-def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None, mask=None):
+def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None, mask=None, q8=None, q8_slot=None):
     """out = act(y*scale + shift (+ residual)); `mask` (uint8 [M*C/8]) optionally receives the
-    ReLU mask as bits so the backward need not re-read `out`."""
+    ReLU mask as bits so the backward need not re-read `out`; `q8` (uint8 like out) an fp8
+    e4m3 copy quantised with the delayed scale of `q8_slot` (fp32[4], see fp8.hip)."""
     M, C = y2d.shape
     if out is None:
         out = torch.empty_like(y2d)
     _lib.call("ttdk_bn_apply", y2d.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(residual), out.data_ptr(),
-              _p(mask), M * C, C, int(relu), _s())
+              _p(mask), _p(q8), _p(q8_slot), M * C, C, int(relu), _s())
     return out
+
+
+def fp8_rollover(slots, margin=1.0):
+    """Delayed scaling step for fp8 activation slots [n, 4] (see fp8.hip)."""
+    _lib.call("ttdk_fp8_rollover", slots.data_ptr(), slots.shape[0], 448.0, float(margin), _s())
+
+
+def fp8_quant_weights(src, dst, table, n_tensors, max_len, slots):
+    _lib.call("ttdk_fp8_quant_weights", src.data_ptr(), dst.data_ptr(), table.data_ptr(), n_tensors, max_len,
+              slots.data_ptr(), slots.shape[0], _s())
 
 
 def bn_backward(dout, out_for_relu, y, gamma, state, dgamma, dbeta, *, g_out=None, dz=None, accumulate=False,

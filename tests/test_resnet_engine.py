@@ -145,3 +145,30 @@ def test_resnet_step_hipgraph_replay_matches_eager():
     d = (m1.params.master - m2.params.master).abs().max()
     assert float(d) < 1e-3 * float(m1.params.master.abs().max()), float(d)
     assert int(o1.step_t) == int(o2.step_t) == 4
+
+
+@pytest.mark.gpu
+def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
+    """precision="fp8": 128-channel-input convs run the fp8 block-scaled MFMA forward with
+    delayed activation scaling; the step must track the bf16 engine and train with LAMB."""
+    from tensorflow_train_distributed_amd.train.flat import FlatLAMB, Schedule
+    torch.manual_seed(0)
+    stages = ((64, 2, 1), (128, 2, 2))
+    x = torch.randn(16, 64, 64, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (16,), device="cuda", dtype=torch.int32)
+    ref = ResNet(stages, num_classes=10, device="cuda", seed=7)
+    f8 = ResNet(stages, num_classes=10, device="cuda", seed=7, precision="fp8")
+    assert sum(f8._fp8_conv(c) for c in f8.conv_list()) >= 5
+    s_ref = ref.forward_backward(x, y).clone()
+    f8.forward_backward(x, y)  # step 1 calibrates the delayed activation scales
+    s8 = f8.forward_backward(x, y).clone()
+    assert abs(float(s8[0]) - float(s_ref[0])) < 0.05 * float(s_ref[0])
+    a, b = f8.params.grad, ref.params.grad
+    cos = float(torch.dot(a, b) / (a.norm() * b.norm()))
+    assert cos > 0.9, cos
+    opt = FlatLAMB(f8.params, Schedule(kind=0, base_lr=0.02), weight_decay=1e-4)
+    losses = []
+    for _ in range(12):
+        losses.append(float(f8.forward_backward(x, y)[0]))
+        opt.step()
+    assert losses[-1] < losses[0] - 0.5, losses
