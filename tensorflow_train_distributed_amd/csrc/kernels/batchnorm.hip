@@ -250,9 +250,16 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
       reinterpret_cast<uint2*>(q8)[i] = make_uint2(lo, hi);
     }
   }
-  if (q8) {
+  if (q8) {  // block max, then one atomic per block spread over the slot's 64 amax lanes
+    __shared__ float red[kThreads / 64];
     qmax = wave_max(qmax);
-    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(q8_slot + 1), __float_as_uint(qmax));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = qmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = red[0];
+      for (int w = 1; w < kThreads / 64; ++w) m = fmaxf(m, red[w]);
+      atomicMax(reinterpret_cast<unsigned int*>(q8_slot + 8 + (blockIdx.x & 63)), __float_as_uint(m));
+    }
   }
 }
 

@@ -1,6 +1,8 @@
 // fp8 (OCP e4m3fn) scaling state for the fp8 training path (BASELINE.json config 5).
 //
-// Every fp8 tensor stream owns a slot float[4] = {amax_prev, amax_cur, scale, inv_scale}:
+// Every fp8 tensor stream owns a slot float[SLOT] = {amax_prev, amax_cur, scale, inv_scale, -, -, -, -,
+// 64 amax lanes}; producers with many workgroups (BN apply) spread their atomicMax over the 64
+// lanes (blockIdx % 64) so they do not serialise on one address; rollover folds the lanes.
 //   * activations use DELAYED scaling: the producer (BN apply) quantises with `scale` derived
 //     from the previous step's amax and accumulates this step's amax into amax_cur;
 //     ttdk_fp8_rollover (once per step, graph-capturable) moves amax_cur -> amax_prev and
@@ -14,11 +16,17 @@
 namespace ttdk {
 namespace {
 
+constexpr int SLOT = 72;
+
 __global__ void rollover_kernel(float* __restrict__ slots, int n, float fmax, float margin) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float* s = slots + 4 * i;
-  const float cur = s[1];
+  float* s = slots + SLOT * i;
+  float cur = s[1];
+  for (int l = 0; l < 64; ++l) {
+    cur = fmaxf(cur, s[8 + l]);
+    s[8 + l] = 0.f;
+  }
   const float prev = cur > 0.f ? cur : s[0];
   s[0] = prev;
   s[1] = 0.f;
@@ -49,14 +57,14 @@ __global__ __launch_bounds__(256) void multi_amax_kernel(const bf16_t* __restric
     }
   }
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(slots + 4 * e.slot + 1), __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(slots + SLOT * e.slot + 1), __float_as_uint(m));
 }
 
 __global__ __launch_bounds__(256) void multi_quant_kernel(const bf16_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                           const QEntry* __restrict__ tab, float* __restrict__ slots,
                                                           float fmax) {
   const QEntry e = tab[blockIdx.y];
-  float* s = slots + 4 * e.slot;
+  float* s = slots + SLOT * e.slot;
   const float amax = s[1];
   const float sc = amax > 0.f ? fmax / amax : 1.f;
   if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -126,12 +126,13 @@ class ResNet:
         self._w8_n = len(rows)
         self._w8_max = max(r[1] for r in rows)
         self._w8_flat = torch.zeros(P.numel, dtype=torch.uint8, device=self.device)
-        self._w8_slots = torch.zeros((len(rows), 4), dtype=torch.float32, device=self.device)
+        from ..ops.kernels import FP8_SLOT
+        self._w8_slots = torch.zeros((len(rows), FP8_SLOT), dtype=torch.float32, device=self.device)
         self._w8 = {c.name: self._w8_flat[P.offsets[c.name + "_conv/kernel"]:P.offsets[c.name + "_conv/kernel"]
                                           + int(np.prod(P.spec(c.name + "_conv/kernel").shape))]
                     .view(P.spec(c.name + "_conv/kernel").shape) for c in convs}
         # activation slots: one per fp8-consumed tensor, assigned in forward order
-        self._a_slots = torch.zeros((4 * len(self.blocks) + 4, 4), dtype=torch.float32, device=self.device)
+        self._a_slots = torch.zeros((4 * len(self.blocks) + 4, FP8_SLOT), dtype=torch.float32, device=self.device)
         self._a_slots[:, 2] = 1.0
         self._a_slots[:, 3] = 1.0
         self._fp8 = True

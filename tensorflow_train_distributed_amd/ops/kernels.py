@@ -62,7 +62,7 @@ def bn_fwd_finalize(sums, count, gamma, beta, eps, momentum, running_mean, runni
 def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None, mask=None, q8=None, q8_slot=None):
     """out = act(y*scale + shift (+ residual)); `mask` (uint8 [M*C/8]) optionally receives the
     ReLU mask as bits so the backward need not re-read `out`; `q8` (uint8 like out) an fp8
-    e4m3 copy quantised with the delayed scale of `q8_slot` (fp32[4], see fp8.hip)."""
+    e4m3 copy quantised with the delayed scale of `q8_slot` (fp32[FP8_SLOT], see fp8.hip)."""
     M, C = y2d.shape
     if out is None:
         out = torch.empty_like(y2d)
@@ -71,8 +71,11 @@ def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None, mask=Non
     return out
 
 
+FP8_SLOT = 72  # floats per fp8 scaling slot (see fp8.hip)
+
+
 def fp8_rollover(slots, margin=1.0):
-    """Delayed scaling step for fp8 activation slots [n, 4] (see fp8.hip)."""
+    """Delayed scaling step for fp8 activation slots [n, FP8_SLOT] (see fp8.hip)."""
     _lib.call("ttdk_fp8_rollover", slots.data_ptr(), slots.shape[0], 448.0, float(margin), _s())
 
 
