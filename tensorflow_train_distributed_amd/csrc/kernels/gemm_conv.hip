@@ -24,6 +24,7 @@
 //    strided output-row remap (stride-2 1x1 dgrad), per-tile BatchNorm partial sums.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace ttdk {
@@ -1096,7 +1097,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
           for (int b = 0; b < NB; ++b) {
             const int n = n0 + hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
             f32x4_t v = acc[ha][hb][a][b] * alpha_e;
-            float* o = out + static_cast<long long>(m) * E.ldo + n;
+            float* o = out + out_row(E, m) * E.ldo + n;
             if (n + 3 < N && (E.ldo & 3) == 0) {
               if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
               *reinterpret_cast<f32x4_t*>(o) = v;
@@ -1162,7 +1163,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
         for (int j = 0; j < 8; ++j) f[j] += rv[j];
       }
     }
-    bf16_t* op = out + static_cast<long long>(m) * E.ldo + n;
+    bf16_t* op = out + out_row(E, m) * E.ldo + n;
     if (E.beta) {
       float ov[8];
       if (vst) {
@@ -1175,7 +1176,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
       for (int j = 0; j < 8; ++j) f[j] += ov[j];
     }
     if (E.aux) {
-      bf16_t* ap = E.aux + static_cast<long long>(m) * E.ldo + n;
+      bf16_t* ap = E.aux + out_row(E, m) * E.ldo + n;
       const uint4 pa8 = pack8(f);
       if (vst) {
         *reinterpret_cast<uint4*>(ap) = pa8;
@@ -1515,13 +1516,7 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
   DenseParams pb{wt, K, N, K};
   if (g->R == 1 && g->S == 1 && g->ph == 0 && g->pw == 0) {
     const int M = g->N * g->P * g->Q;
-    if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
     DenseParams pa{dy, g->K, M, K};
-    const int bbn = big_bn(M, N, K);
-    if (g->sh == 1 && g->sw == 1 && (bm == 0 || bm == 256) && bbn && pe.stat == nullptr)
-      return bbn == 256 ? big::dense<256>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st)
-                        : big::dense<128>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st);
-    if (bm == 256) bm = bn = 0, pick_tile(M, N, &bm, &bn);
     if (g->sh != 1 || g->sw != 1) {
       if (g->sh != g->sw) return hipErrorInvalidValue;
       pe.remap = 1;
@@ -1531,19 +1526,33 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
       pe.rOW = g->W;
       pe.rs = g->sh;
     }
+    const int bbn = big_bn(M, N, K);
+    if ((bm == 0 || bm == 256) && bbn && pe.stat == nullptr)  // the big epilogue honours the row remap
+      return bbn == 256 ? big::dense<256>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st)
+                        : big::dense<128>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st);
+    if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
     return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
   }
   const int M = g->N * g->H * g->W;
   const int bbn = big_bn(M, N, K);
   // unit-stride dgrad gathers on the LDS-DMA kernel (strided ones keep the 4-wave kernel: the
   // divisibility test costs registers the 256-row tile does not have)
-  if ((bm == 0 || bm == 256) && bbn && g->K % 64 == 0 && pe.stat == nullptr && !pe.remap && g->sh == 1 &&
-      g->sw == 1) {
+  static const bool strided_big = [] {
+    const char* e = getenv("TTD_BIG_STRIDED_DGRAD");
+    return e != nullptr && e[0] == '1';
+  }();
+  const bool unit = g->sh == 1 && g->sw == 1;
+  if ((bm == 0 || bm == 256) && bbn && g->K % 64 == 0 && pe.stat == nullptr && !pe.remap && (unit || strided_big)) {
     const big::ConvP pa = conv_params(dy, g->P, g->Q, g->K, g->H, g->W, g, M);
     const big::DenseP pb2{wt, K, N};
+    if (unit) {
+      if (bbn == 256)
+        return big::launch<256, big::OpConvK<128, 2, true, true>, big::OpDenseK<128, 2>>(pa, pb2, pe, M, N, K, 1, st);
+      return big::launch<128, big::OpConvK<128, 2, true, true>, big::OpDenseK<64, 2>>(pa, pb2, pe, M, N, K, 1, st);
+    }
     if (bbn == 256)
-      return big::launch<256, big::OpConvK<128, 2, true, true>, big::OpDenseK<128, 2>>(pa, pb2, pe, M, N, K, 1, st);
-    return big::launch<128, big::OpConvK<128, 2, true, true>, big::OpDenseK<64, 2>>(pa, pb2, pe, M, N, K, 1, st);
+      return big::launch<256, big::OpConvK<128, 2, true>, big::OpDenseK<128, 2>>(pa, pb2, pe, M, N, K, 1, st);
+    return big::launch<128, big::OpConvK<128, 2, true>, big::OpDenseK<64, 2>>(pa, pb2, pe, M, N, K, 1, st);
   }
   if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
   GatherParams pa{dy, g->P, g->Q, g->K, g->H, g->W, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};

@@ -34,7 +34,8 @@ def run(batch):
 def report(trace_csv, log_json):
     import csv
     log = json.load(open(log_json))
-    rows = [r for r in csv.DictReader(open(trace_csv)) if "gemm_kernel" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(trace_csv))
+            if "gemm_kernel" in r["Kernel_Name"] or "gemm256_kernel" in r["Kernel_Name"]]
     # the last len(log) gemm dispatches belong to the logged step
     rows = rows[-len(log):]
     agg = {}
@@ -43,14 +44,17 @@ def report(trace_csv, log_json):
         t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         tot += t
         fl = 2.0 * M * N * K
-        key = (kind, M, N, K)
+        kn = r["Kernel_Name"]
+        kern = ("big" + kn.split("gemm256_kernel<")[1].split(",")[0]) if "gemm256" in kn else \
+            ("4w" + kn.split("gemm_kernel<")[1].split(",")[0] + "x" + kn.split("gemm_kernel<")[1].split(",")[1].strip())
+        key = (kind, M, N, K, kern)
         a = agg.setdefault(key, [0, 0.0, fl])
         a[0] += 1
         a[1] += t
     print("total gemm us %.1f" % tot)
-    print("%-16s %8s %6s %6s %5s %9s %8s" % ("kind", "M", "N", "K", "n", "us(each)", "TF/s"))
-    for (kind, M, N, K), (n, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        print("%-16s %8d %6d %6d %5d %9.1f %8.1f" % (kind, M, N, K, n, t / n, fl / (t / n) / 1e6))
+    print("%-16s %8s %6s %6s %5s %9s %8s %8s" % ("kind", "M", "N", "K", "n", "us(each)", "TF/s", "kernel"))
+    for (kind, M, N, K, kern), (n, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print("%-16s %8d %6d %6d %5d %9.1f %8.1f %8s" % (kind, M, N, K, n, t / n, fl / (t / n) / 1e6, kern))
 
 
 if __name__ == "__main__":
