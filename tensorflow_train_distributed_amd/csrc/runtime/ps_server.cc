@@ -91,14 +91,46 @@ struct Accumulator {
   int64_t dropped = 0;
 };
 
+// Variable storage. Workers read (Pull) and update (ApplyGD) without locking, exactly as
+// TF1's Hogwild `use_locking=False` kernels; to keep that well-defined under the C++
+// memory model (and clean under ThreadSanitizer) every element access is a relaxed 32-bit
+// atomic (a plain mov on x86: lost updates are allowed, torn words are not).
 struct Var {
   int dtype = kDtFloat;
   std::vector<int64_t> shape;
-  std::vector<char> data;  // raw bytes (float32 or int64)
+  std::vector<uint32_t> words;  // float32 or int64 payload as 32-bit words
   Accumulator acc;
-  float* f() { return reinterpret_cast<float*>(data.data()); }
-  size_t numel() const { return data.size() / (dtype == kDtInt64 ? 8 : 4); }
+  size_t nbytes() const { return words.size() * 4; }
+  size_t numel() const { return nbytes() / (dtype == kDtInt64 ? 8 : 4); }
+  void load(char* dst) const {  // relaxed snapshot
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    for (size_t i = 0; i < words.size(); ++i) {
+      uint32_t w = __atomic_load_n(&words[i], __ATOMIC_RELAXED);
+      std::memcpy(d + i, &w, 4);
+    }
+  }
+  void store(const char* src) {
+    for (size_t i = 0; i < words.size(); ++i) {
+      uint32_t w;
+      std::memcpy(&w, src + 4 * i, 4);
+      __atomic_store_n(&words[i], w, __ATOMIC_RELAXED);
+    }
+  }
+  // w += a * g, elementwise-atomic, not RMW-atomic. `g` may be unaligned (request body).
+  void axpy(float a, const void* gp) {
+    const char* g = static_cast<const char*>(gp);
+    for (size_t i = 0; i < words.size(); ++i) {
+      uint32_t u = __atomic_load_n(&words[i], __ATOMIC_RELAXED);
+      float w, gi;
+      std::memcpy(&w, &u, 4);
+      std::memcpy(&gi, g + 4 * i, 4);
+      w += a * gi;
+      std::memcpy(&u, &w, 4);
+      __atomic_store_n(&words[i], u, __ATOMIC_RELAXED);
+    }
+  }
 };
+using VarPtr = std::shared_ptr<Var>;  // a Pull racing a re-init keeps its Var alive
 
 // Cursor over a request body.
 struct Body {
@@ -233,11 +265,19 @@ class Server {
     }
     for (auto& t : ts)
       if (t.joinable()) t.join();
+    std::lock_guard<std::mutex> lk(stop_mu_);
+    stopped_ = true;
+    stop_cv_.notify_all();  // under the lock: a waiter may destroy the server once it returns
+  }
+
+  ~Server() {
+    stop();
+    std::thread t;
     {
       std::lock_guard<std::mutex> lk(stop_mu_);
-      stopped_ = true;
+      t.swap(shutdown_thread_);
     }
-    stop_cv_.notify_all();
+    if (t.joinable()) t.join();
   }
 
   bool stopping() const { return stopping_.load(); }
@@ -280,7 +320,10 @@ class Server {
       uint64_t rl = resp.size();
       if (!send_all(fd, &st, 4) || !send_all(fd, &rl, 8) || (rl && !send_all(fd, resp.data(), rl))) break;
       if (hdr[1] == kShutdown) {
-        std::thread([this] { stop(); }).detach();
+        // Tear down off this connection thread (stop() joins it); the destructor joins this
+        // thread, so a Shutdown racing ttd_ps_server_destroy never touches a freed server.
+        std::lock_guard<std::mutex> lk(stop_mu_);
+        if (!shutdown_thread_.joinable()) shutdown_thread_ = std::thread([this] { stop(); });
         break;
       }
     }
@@ -295,10 +338,10 @@ class Server {
     }
   }
 
-  Var* find(const std::string& name) {
+  VarPtr find(const std::string& name) {
     std::lock_guard<std::mutex> lk(vars_mu_);
     auto it = vars_.find(name);
-    return it == vars_.end() ? nullptr : it->second.get();
+    return it == vars_.end() ? nullptr : it->second;
   }
 
   void close_queue() {
@@ -328,16 +371,17 @@ class Server {
           for (uint32_t d = 0; d < nd; ++d) shape[d] = b.get<int64_t>();
           uint64_t nb = b.get<uint64_t>();
           const char* data = b.bytes(nb);
-          if (!b.ok) break;
-          auto v = std::make_unique<Var>();
-          v->dtype = dt;
-          v->shape = shape;
-          v->data.assign(data, data + nb);
+          if (!b.ok || nb % 4) break;
           std::lock_guard<std::mutex> lk(vars_mu_);
           auto it = vars_.find(name);
-          if (it != vars_.end() && it->second->data.size() == nb) {
-            std::memcpy(it->second->data.data(), data, nb);  // keep accumulator state / pointers
+          if (it != vars_.end() && it->second->nbytes() == nb) {
+            it->second->store(data);  // keep accumulator state
           } else {
+            auto v = std::make_shared<Var>();
+            v->dtype = dt;
+            v->shape = shape;
+            v->words.resize(nb / 4);
+            std::memcpy(v->words.data(), data, nb);
             vars_[name] = std::move(v);
           }
         }
@@ -355,13 +399,15 @@ class Server {
         uint32_t n = b.get<uint32_t>();
         for (uint32_t i = 0; i < n && b.ok; ++i) {
           std::string name = b.str();
-          Var* v = find(name);
+          VarPtr v = find(name);
           if (!v) {
             out->assign(name);
             return kNotFound;
           }
-          put<uint64_t>(out, v->data.size());
-          out->append(v->data.data(), v->data.size());  // Hogwild read, as TF1 (no locking)
+          put<uint64_t>(out, v->nbytes());
+          const size_t at = out->size();
+          out->resize(at + v->nbytes());
+          v->load(&(*out)[at]);  // Hogwild read, as TF1 (no locking)
         }
         return b.ok ? kOk : kErr;
       }
@@ -372,16 +418,14 @@ class Server {
         for (uint32_t i = 0; i < n && b.ok; ++i) {
           std::string name = b.str();
           uint64_t nb = b.get<uint64_t>();
-          const float* g = reinterpret_cast<const float*>(b.bytes(nb));
+          const char* g = b.bytes(nb);  // unaligned: read with memcpy
           if (!b.ok) break;
-          Var* v = find(name);
-          if (!v || v->dtype != kDtFloat || v->data.size() != nb) {
+          VarPtr v = find(name);
+          if (!v || v->dtype != kDtFloat || v->nbytes() != nb) {
             out->assign(name);
             return kNotFound;
           }
-          float* w = v->f();
-          const size_t m = nb / 4;
-          for (size_t k = 0; k < m; ++k) w[k] -= lr * g[k];  // ApplyGradientDescent, use_locking=False
+          v->axpy(-lr, g);  // ApplyGradientDescent, use_locking=False
         }
         int64_t gs = inc ? global_step_.fetch_add(1) + 1 : global_step_.load();
         put<int64_t>(out, gs);
@@ -394,10 +438,10 @@ class Server {
         for (uint32_t i = 0; i < n && b.ok; ++i) {
           std::string name = b.str();
           uint64_t nb = b.get<uint64_t>();
-          const float* g = reinterpret_cast<const float*>(b.bytes(nb));
+          const char* g = b.bytes(nb);  // unaligned: read with memcpy
           if (!b.ok) break;
-          Var* v = find(name);
-          if (!v || v->data.size() != nb) {
+          VarPtr v = find(name);
+          if (!v || v->nbytes() != nb) {
             out->assign(name);
             return kNotFound;
           }
@@ -409,7 +453,11 @@ class Server {
           }
           const size_t m = nb / 4;
           if (a.sum.size() != m) a.sum.assign(m, 0.f);
-          for (size_t k = 0; k < m; ++k) a.sum[k] += g[k];
+          for (size_t k = 0; k < m; ++k) {
+            float gk;
+            std::memcpy(&gk, g + 4 * k, 4);
+            a.sum[k] += gk;
+          }
           ++a.count;
           ++accepted;
           a.cv.notify_all();
@@ -426,10 +474,10 @@ class Server {
         uint8_t finalize = b.get<uint8_t>();
         uint32_t tokens = b.get<uint32_t>();
         uint32_t n = b.get<uint32_t>();
-        std::vector<Var*> vs;
+        std::vector<VarPtr> vs;
         for (uint32_t i = 0; i < n && b.ok; ++i) {
           std::string name = b.str();
-          Var* v = find(name);
+          VarPtr v = find(name);
           if (!v) {
             out->assign(name);
             return kNotFound;
@@ -437,16 +485,13 @@ class Server {
           vs.push_back(v);
         }
         if (!b.ok) return kErr;
-        for (Var* v : vs) {
+        for (VarPtr& v : vs) {
           Accumulator& a = v->acc;
           std::unique_lock<std::mutex> lk(a.mu);
           a.cv.wait(lk, [&] { return stopping_.load() || a.count >= static_cast<int64_t>(num_required); });
           if (stopping_) return kShuttingDown;
           const float inv = 1.0f / static_cast<float>(a.count);
-          float* w = v->f();
-          const size_t m = v->numel();
-          if (a.sum.size() == m)
-            for (size_t k = 0; k < m; ++k) w[k] -= lr * (a.sum[k] * inv);
+          if (a.sum.size() == v->numel()) v->axpy(-lr * inv, a.sum.data());
           std::fill(a.sum.begin(), a.sum.end(), 0.f);
           a.count = 0;
           ++a.step;
@@ -510,11 +555,14 @@ class Server {
           out->assign(ttd_last_error_str());
           return kErr;
         }
+        std::vector<char> snap;
         std::lock_guard<std::mutex> lk(vars_mu_);
         for (auto& kv : vars_) {
           Var* v = kv.second.get();
+          snap.resize(v->nbytes());
+          v->load(snap.data());
           if (ttd_bundle_writer_add(w, kv.first.c_str(), v->dtype, static_cast<int>(v->shape.size()),
-                                    v->shape.data(), v->data.data(), v->data.size()) != 0) {
+                                    v->shape.data(), snap.data(), snap.size()) != 0) {
             out->assign(ttd_last_error_str());
             ttd_bundle_writer_finish(w);
             return kErr;
@@ -562,8 +610,12 @@ class Server {
           auto it = vars_.find(key);
           if (it == vars_.end()) continue;  // owned by another PS task
           Var* v = it->second.get();
-          if (v->data.size() != nb) continue;
-          if (ttd_bundle_reader_read(r, key.c_str(), v->data.data(), nb) == 0) ++restored;
+          if (v->nbytes() != nb) continue;
+          std::vector<char> buf(nb);
+          if (ttd_bundle_reader_read(r, key.c_str(), buf.data(), nb) == 0) {
+            v->store(buf.data());
+            ++restored;
+          }
         }
         ttd_bundle_reader_close(r);
         put<uint32_t>(out, restored);
@@ -628,9 +680,10 @@ class Server {
   std::condition_variable stop_cv_;
   std::atomic<bool> stopping_{false};
   bool stopped_ = false;
+  std::thread shutdown_thread_;
 
   std::mutex vars_mu_;
-  std::map<std::string, std::unique_ptr<Var>> vars_;
+  std::map<std::string, VarPtr> vars_;
   std::atomic<bool> ready_{false};
   std::atomic<int64_t> generation_{0};
   std::atomic<int64_t> global_step_{0};
