@@ -18,6 +18,7 @@ namespace ttdk {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kUnroll = 4;  // independent 16 B loads per lane per trip in the streaming passes
 
 // Sums over rows of x[M][C] (and of x^2), 8 channels per thread-column. Writes
 // partial[blockIdx.x][2][C]. Requires C % 8 == 0.
@@ -34,13 +35,23 @@ __global__ __launch_bounds__(kThreads) void stats_partial_kernel(const bf16_t* _
     const int c8 = cbase + col;
     float s[8] = {0}, q[8] = {0};
     if (rl < rlanes && c8 < cg) {
-      for (long long r = r0 + rl; r < r1; r += rlanes) {
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(x + r * C + c8 * 8), f);
+      for (long long rb = r0 + rl; rb < r1; rb += static_cast<long long>(rlanes) * kUnroll) {
+        uint4 xv[kUnroll];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          s[j] += f[j];
-          q[j] += f[j] * f[j];
+        for (int u = 0; u < kUnroll; ++u) {
+          const long long r = rb + static_cast<long long>(u) * rlanes;
+          if (r < r1) xv[u] = *reinterpret_cast<const uint4*>(x + r * C + c8 * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          if (rb + static_cast<long long>(u) * rlanes >= r1) break;
+          float f[8];
+          unpack8(xv[u], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            s[j] += f[j];
+            q[j] += f[j] * f[j];
+          }
         }
       }
     }
@@ -86,28 +97,45 @@ __global__ __launch_bounds__(kThreads) void bwd_partial_kernel(const bf16_t* __r
     const int c8 = cbase + col;
     float s[8] = {0}, q[8] = {0};
     if (rl < rlanes && c8 < cg) {
-      for (long long r = r0 + rl; r < r1; r += rlanes) {
-        const long long off = r * C + c8 * 8;
-        float g[8], yv[8];
-        uint4 graw = *reinterpret_cast<const uint4*>(dy + off);
-        unpack8(graw, g);
-        if (mask) {
-          const uint32_t mb = mask[off >> 3];
+      // kUnroll rows per trip, all loads issued before the math (several 16 B reads in flight)
+      for (long long rb = r0 + rl; rb < r1; rb += static_cast<long long>(rlanes) * kUnroll) {
+        uint4 gv[kUnroll], yr[kUnroll], ov[kUnroll];
+        uint32_t mb[kUnroll];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
-          if (g_out) *reinterpret_cast<uint4*>(g_out + off) = pack8(g);
-        } else if (out) {
-          float o[8];
-          unpack8(*reinterpret_cast<const uint4*>(out + off), o);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
-          if (g_out) *reinterpret_cast<uint4*>(g_out + off) = pack8(g);
+        for (int u = 0; u < kUnroll; ++u) {
+          const long long r = rb + static_cast<long long>(u) * rlanes;
+          if (r < r1) {
+            const long long off = r * C + c8 * 8;
+            gv[u] = *reinterpret_cast<const uint4*>(dy + off);
+            yr[u] = *reinterpret_cast<const uint4*>(y + off);
+            if (mask) mb[u] = mask[off >> 3];
+            else if (out) ov[u] = *reinterpret_cast<const uint4*>(out + off);
+          }
         }
-        unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          s[j] += g[j];
-          q[j] += g[j] * yv[j];
+        for (int u = 0; u < kUnroll; ++u) {
+          const long long r = rb + static_cast<long long>(u) * rlanes;
+          if (r >= r1) break;
+          const long long off = r * C + c8 * 8;
+          float g[8], yv[8];
+          unpack8(gv[u], g);
+          if (mask) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] = (mb[u] >> j) & 1u ? g[j] : 0.f;
+            if (g_out) *reinterpret_cast<uint4*>(g_out + off) = pack8(g);
+          } else if (out) {
+            float o[8];
+            unpack8(ov[u], o);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+            if (g_out) *reinterpret_cast<uint4*>(g_out + off) = pack8(g);
+          }
+          unpack8(yr[u], yv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            s[j] += g[j];
+            q[j] += g[j] * yv[j];
+          }
         }
       }
     }
@@ -191,7 +219,114 @@ __global__ void bwd_finalize_kernel(const float* __restrict__ sums, float count,
   coef[2 * C + c] = cc;
 }
 
-// out = act(y*scale[c] + shift[c] (+ residual)); 8 channels per thread.
+// Cross-tile reduction + finalize in two fence-free launches (replacing memset + atomic
+// reduce + finalize): reduce_slices folds partial[T][2][C] into slab[S][2][C] (grid =
+// ceil(C/32) x S, block = 8 row-groups x 32 channels, <= 32 rows per block), finalize folds
+// the S slab rows in a fixed order (deterministic, no float atomics) and writes the per-channel
+// coefficients. A single-launch "last block finalizes" variant (arrival counter + device-scope
+// fence per block; on gfx950 the release fence writes back the XCD's L2) measured ~3x slower
+// than the three launches it was meant to replace, so this keeps two.
+struct FinalizeArgs {
+  float count;
+  const float* gamma;
+  const float* beta;  // fwd
+  float eps, momentum;
+  float* running_mean;
+  float* running_var;
+  float* mean;  // fwd: out; bwd: in
+  float* rstd;  // fwd: out; bwd: in
+  float* scale;  // fwd: out
+  float* shift;  // fwd: out
+  float* dgamma;  // bwd
+  float* dbeta;   // bwd
+  float* coef;    // bwd: [3][C]
+  int accumulate;
+};
+
+__global__ __launch_bounds__(kThreads) void reduce_slices_kernel(const float* __restrict__ partial, int T, int C,
+                                                                 int t_per_slice, float* __restrict__ slab) {
+  __shared__ float red[2][8][33];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  const int t0 = blockIdx.y * t_per_slice, t1 = min(T, t0 + t_per_slice);
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int t = t0 + rg; t < t1; t += 8) {
+      const float* p = partial + static_cast<long long>(t) * 2 * C + c;
+      s += p[0];
+      q += p[C];
+    }
+  }
+  red[0][rg][cl] = s;
+  red[1][rg][cl] = q;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int k = 1; k < 8; ++k) {
+      s += red[0][k][cl];
+      q += red[1][k][cl];
+    }
+    slab[(2LL * blockIdx.y) * C + c] = s;
+    slab[(2LL * blockIdx.y + 1) * C + c] = q;
+  }
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(kThreads) void finalize_kernel(const float* __restrict__ slab, int S, int C, FinalizeArgs a) {
+  __shared__ float red[2][8][33];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int y = rg; y < S; y += 8) {
+      s += slab[(2LL * y) * C + c];
+      q += slab[(2LL * y + 1) * C + c];
+    }
+  }
+  red[0][rg][cl] = s;
+  red[1][rg][cl] = q;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  for (int k = 1; k < 8; ++k) {
+    s += red[0][k][cl];
+    q += red[1][k][cl];
+  }
+  const float gam = a.gamma ? a.gamma[c] : 1.f;
+  if (!BWD) {
+    const float mean = s / a.count;
+    const float var = fmaxf(q / a.count - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + a.eps);
+    a.mean[c] = mean;
+    a.rstd[c] = rstd;
+    const float sc = gam * rstd;
+    a.scale[c] = sc;
+    a.shift[c] = (a.beta ? a.beta[c] : 0.f) - mean * sc;
+    if (a.running_mean) {
+      const float unbiased = a.count > 1.f ? var * a.count / (a.count - 1.f) : var;
+      a.running_mean[c] = a.running_mean[c] * a.momentum + mean * (1.f - a.momentum);
+      a.running_var[c] = a.running_var[c] * a.momentum + unbiased * (1.f - a.momentum);
+    }
+  } else {
+    const float m = a.mean[c], r = a.rstd[c];
+    const float dgam = r * (q - m * s);
+    if (a.dgamma) a.dgamma[c] = dgam + (a.accumulate ? a.dgamma[c] : 0.f);
+    if (a.dbeta) a.dbeta[c] = s + (a.accumulate ? a.dbeta[c] : 0.f);
+    const float ca = gam * r;
+    const float cb = -gam * r * r * dgam / a.count;
+    a.coef[c] = ca;
+    a.coef[C + c] = cb;
+    a.coef[2 * C + c] = -ca * s / a.count - cb * m;
+  }
+}
+
+// Streaming passes. A block covers kUnroll*256 consecutive 8-channel vectors; when the
+// number of 8-channel groups per row divides 256 (every ResNet width) a thread always sees
+// the same channel group, so its per-channel coefficients live in registers (FIXED), and all
+// kUnroll loads are issued before any math so each lane keeps several 16 B reads in flight.
+
+// out = act(y*scale[c] + shift[c] (+ residual)); 8 channels per vector.
+template <bool FIXED>
 __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
                                                          const bf16_t* __restrict__ residual, bf16_t* __restrict__ out,
@@ -201,53 +336,75 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
   // fp8 e4m3 copy with the slot's delayed scale; this step's amax goes to q8_slot[1]
   const float qs = q8 ? q8_slot[2] : 1.f;
   float qmax = 0.f;
-  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n8;
-       i += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int c0 = static_cast<int>(i % cg) * 8;
-    float f[8];
-    unpack8(reinterpret_cast<const uint4*>(y)[i], f);
+  float sc[8], sh[8];
+  auto load_coef = [&](int c0) {
     const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(scale + c0), s1 = *reinterpret_cast<const f32x4_t*>(scale + c0 + 4);
     const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(shift + c0), h1 = *reinterpret_cast<const f32x4_t*>(shift + c0 + 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      f[j] = f[j] * s0[j] + h0[j];
-      f[4 + j] = f[4 + j] * s1[j] + h1[j];
+      sc[j] = s0[j];
+      sc[4 + j] = s1[j];
+      sh[j] = h0[j];
+      sh[4 + j] = h1[j];
     }
-    if (residual) {
-      float r[8];
-      unpack8(reinterpret_cast<const uint4*>(residual)[i], r);
+  };
+  if (FIXED) load_coef((threadIdx.x % cg) * 8);
+  const long long span = static_cast<long long>(kThreads) * kUnroll;
+  for (long long base = blockIdx.x * span; base < n8; base += static_cast<long long>(gridDim.x) * span) {
+    uint4 yv[kUnroll], rv[kUnroll];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += r[j];
-    }
-    if (relu) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-    }
-    const uint4 packed = pack8(f);
-    reinterpret_cast<uint4*>(out)[i] = packed;
-    if (mask) {  // 1 bit per element of [stored bf16 > 0]: the ReLU mask backward reads instead of `out`
-      const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
-      uint32_t mb = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-        mb |= ((h & 0x7fffu) != 0 && !(h & 0x8000u) ? 1u : 0u) << j;
+    for (int u = 0; u < kUnroll; ++u) {
+      const long long i = base + u * kThreads + threadIdx.x;
+      if (i < n8) {
+        yv[u] = reinterpret_cast<const uint4*>(y)[i];
+        if (residual) rv[u] = reinterpret_cast<const uint4*>(residual)[i];
       }
-      mask[i] = static_cast<uint8_t>(mb);
     }
-    if (q8) {
-      float fq[8];
-      unpack8(packed, fq);
-      uint32_t lo = 0, hi = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        qmax = fmaxf(qmax, fabsf(fq[j]));
-        const float v = fminf(fmaxf(fq[j] * qs, -448.f), 448.f);
-        const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false) & 0xff);
-        if (j < 4) lo |= b << (8 * j);
-        else hi |= b << (8 * (j - 4));
+    for (int u = 0; u < kUnroll; ++u) {
+      const long long i = base + u * kThreads + threadIdx.x;
+      if (i >= n8) break;
+      if (!FIXED) load_coef(static_cast<int>(i % cg) * 8);
+      float f[8];
+      unpack8(yv[u], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+      if (residual) {
+        float r[8];
+        unpack8(rv[u], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += r[j];
       }
-      reinterpret_cast<uint2*>(q8)[i] = make_uint2(lo, hi);
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      }
+      const uint4 packed = pack8(f);
+      reinterpret_cast<uint4*>(out)[i] = packed;
+      if (mask) {  // 1 bit per element of [stored bf16 > 0]: the ReLU mask backward reads instead of `out`
+        const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
+        uint32_t mb = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+          mb |= ((h & 0x7fffu) != 0 && !(h & 0x8000u) ? 1u : 0u) << j;
+        }
+        mask[i] = static_cast<uint8_t>(mb);
+      }
+      if (q8) {
+        float fq[8];
+        unpack8(packed, fq);
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          qmax = fmaxf(qmax, fabsf(fq[j]));
+          const float v = fminf(fmaxf(fq[j] * qs, -448.f), 448.f);
+          const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false) & 0xff);
+          if (j < 4) lo |= b << (8 * j);
+          else hi |= b << (8 * (j - 4));
+        }
+        reinterpret_cast<uint2*>(q8)[i] = make_uint2(lo, hi);
+      }
     }
   }
   if (q8) {  // block max, then one atomic per block spread over the slot's 64 amax lanes
@@ -263,7 +420,8 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
   }
 }
 
-// dz = a*g + b*y + c, g = dy * [out > 0] if out given.
+// dz = a*g + b*y + c, g = dy * [out > 0] (ReLU mask bit, or `out` > 0, or no mask).
+template <bool FIXED>
 __global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ out,
                                                              const uint8_t* __restrict__ mask,
@@ -271,28 +429,57 @@ __global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __res
                                                              const float* __restrict__ coef, bf16_t* __restrict__ dz,
                                                              long long n8, int C) {
   const int cg = C >> 3;
-  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n8;
-       i += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int c0 = static_cast<int>(i % cg) * 8;
-    float g[8], yv[8];
-    unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
-    if (mask) {
-      const uint32_t mb = mask[i];
+  float ca[8], cb[8], cc[8];
+  auto load_coef = [&](int c0) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
-    } else if (out) {
-      float o[8];
-      unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+    for (int k = 0; k < 2; ++k) {
+      const f32x4_t a = *reinterpret_cast<const f32x4_t*>(coef + c0 + 4 * k);
+      const f32x4_t b = *reinterpret_cast<const f32x4_t*>(coef + C + c0 + 4 * k);
+      const f32x4_t c = *reinterpret_cast<const f32x4_t*>(coef + 2 * C + c0 + 4 * k);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        ca[4 * k + j] = a[j];
+        cb[4 * k + j] = b[j];
+        cc[4 * k + j] = c[j];
+      }
     }
-    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+  };
+  if (FIXED) load_coef((threadIdx.x % cg) * 8);
+  const long long span = static_cast<long long>(kThreads) * kUnroll;
+  for (long long base = blockIdx.x * span; base < n8; base += static_cast<long long>(gridDim.x) * span) {
+    uint4 gv[kUnroll], yv[kUnroll], ov[kUnroll];
+    uint32_t mb[kUnroll];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      g[j] = coef[c] * g[j] + coef[C + c] * yv[j] + coef[2 * C + c];
+    for (int u = 0; u < kUnroll; ++u) {
+      const long long i = base + u * kThreads + threadIdx.x;
+      if (i < n8) {
+        gv[u] = reinterpret_cast<const uint4*>(dy)[i];
+        yv[u] = reinterpret_cast<const uint4*>(y)[i];
+        if (mask) mb[u] = mask[i];
+        else if (out) ov[u] = reinterpret_cast<const uint4*>(out)[i];
+      }
     }
-    reinterpret_cast<uint4*>(dz)[i] = pack8(g);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const long long i = base + u * kThreads + threadIdx.x;
+      if (i >= n8) break;
+      if (!FIXED) load_coef(static_cast<int>(i % cg) * 8);
+      float g[8], yf[8];
+      unpack8(gv[u], g);
+      if (mask) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = (mb[u] >> j) & 1u ? g[j] : 0.f;
+      } else if (out) {
+        float o[8];
+        unpack8(ov[u], o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+      }
+      unpack8(yv[u], yf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = ca[j] * g[j] + cb[j] * yf[j] + cc[j];
+      reinterpret_cast<uint4*>(dz)[i] = pack8(g);
+    }
   }
 }
 
@@ -312,7 +499,7 @@ TTDK_EXPORT int ttdk_bn_num_partials(long long M, int C) {
   const int cols = cg < kThreads ? cg : kThreads;
   const int rlanes = kThreads / cols;
   long long want = (M + 16LL * rlanes - 1) / (16LL * rlanes);  // >= 16 rows per row-lane
-  if (want > 1024) want = 1024;
+  if (want > 2048) want = 2048;
   if (want < 1) want = 1;
   return static_cast<int>(want);
 }
@@ -369,8 +556,13 @@ TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* 
                               hipStream_t st) {
   if (C % 8 || n % 8 || (q8 && !q8_slot)) return hipErrorInvalidValue;
   const long long n8 = n / 8;
-  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, q8,
-                     q8_slot, n8, C, relu);
+  const int grid = grid_for(n8, kThreads * kUnroll);
+  if (kThreads % (C >> 3) == 0)
+    hipLaunchKernelGGL(apply_kernel<true>, dim3(grid), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, q8,
+                       q8_slot, n8, C, relu);
+  else
+    hipLaunchKernelGGL(apply_kernel<false>, dim3(grid), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, q8,
+                       q8_slot, n8, C, relu);
   return hipGetLastError();
 }
 
@@ -378,6 +570,37 @@ TTDK_EXPORT int ttdk_bn_bwd_apply(const bf16_t* dy, const bf16_t* out, const uin
                                   const float* coef, bf16_t* dz, long long n, int C, hipStream_t st) {
   if (C % 8 || n % 8) return hipErrorInvalidValue;
   const long long n8 = n / 8;
-  hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_for(n8)), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, n8, C);
+  const int grid = grid_for(n8, kThreads * kUnroll);
+  if (kThreads % (C >> 3) == 0)
+    hipLaunchKernelGGL(bwd_apply_kernel<true>, dim3(grid), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, n8, C);
+  else
+    hipLaunchKernelGGL(bwd_apply_kernel<false>, dim3(grid), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, n8, C);
+  return hipGetLastError();
+}
+
+// Slab rows (slices) ttdk_bn_reduce_finalize uses for T partial rows: the caller provides a
+// slab of slices*2*C floats.
+TTDK_EXPORT int ttdk_bn_finalize_slices(int T) {
+  int s = (T + 31) / 32;
+  return s < 1 ? 1 : (s > 256 ? 256 : s);
+}
+
+// bwd == 0: mean/rstd/scale/shift (+ running stats) from the fwd partials;
+// bwd == 1: dgamma/dbeta/coef from the bwd partials (mean/rstd inputs).
+TTDK_EXPORT int ttdk_bn_reduce_finalize(const float* partial, int T, int C, float* slab, int bwd, float count,
+                                        const float* gamma, const float* beta, float eps, float momentum,
+                                        float* running_mean, float* running_var, float* mean, float* rstd,
+                                        float* scale, float* shift, float* dgamma, float* dbeta, float* coef,
+                                        int accumulate, hipStream_t st) {
+  const int S = ttdk_bn_finalize_slices(T);
+  const int per = (T + S - 1) / S;
+  FinalizeArgs a{count, gamma, beta, eps, momentum, running_mean, running_var, mean, rstd, scale, shift,
+                 dgamma, dbeta, coef, accumulate};
+  const int cgr = (C + 31) / 32;
+  hipLaunchKernelGGL(reduce_slices_kernel, dim3(cgr, S), dim3(kThreads), 0, st, partial, T, C, per, slab);
+  if (bwd)
+    hipLaunchKernelGGL(finalize_kernel<true>, dim3(cgr), dim3(kThreads), 0, st, slab, S, C, a);
+  else
+    hipLaunchKernelGGL(finalize_kernel<false>, dim3(cgr), dim3(kThreads), 0, st, slab, S, C, a);
   return hipGetLastError();
 }

@@ -218,11 +218,10 @@ class ResNet:
         else:
             y = G.conv_fwd(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
                            tile=(bm, bn))
-        sums = K.bn_reduce_partials(partial, T, c.cout)
         st = K.BNState(c.cout, x.device)
         pre = c.name + "_bn/"
-        K.bn_fwd_finalize(sums, M, P.var[pre + "gamma"], P.var[pre + "beta"], self.bn_eps, self.bn_momentum,
-                          P.var[pre + "moving_mean"], P.var[pre + "moving_variance"], st)
+        K.bn_fwd_stats(partial, T, M, P.var[pre + "gamma"], P.var[pre + "beta"], self.bn_eps, self.bn_momentum,
+                       P.var[pre + "moving_mean"], P.var[pre + "moving_variance"], st)
         y2 = y.view(M, c.cout)
         mask = torch.empty(M * c.cout // 8, dtype=torch.uint8, device=x.device) if relu else None
         q8 = slot = None

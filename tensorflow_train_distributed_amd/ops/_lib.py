@@ -51,6 +51,7 @@ _SIGS = {
     "ttdk_gemm_bf16": [P, L, I, P, L, I, I, I, I, I, I, I, E, P],
     "ttdk_conv_fwd": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
+    "ttdk_conv_dgrad_subpixel": [P, P, G, P, E, P],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
     # batchnorm.hip
@@ -59,6 +60,8 @@ _SIGS = {
     "ttdk_bn_bwd_partial": [P, P, P, P, L, I, P, I, P, P],
     "ttdk_bn_reduce_partials": [P, I, I, P, P],
     "ttdk_bn_fwd_finalize": [P, F, I, P, P, F, F, P, P, P, P, P, P, P],
+    "ttdk_bn_finalize_slices": [I],
+    "ttdk_bn_reduce_finalize": [P, I, I, P, I, F, P, P, F, F, P, P, P, P, P, P, P, P, P, I, P],
     "ttdk_bn_bwd_finalize": [P, F, I, P, P, P, P, P, P, I, P],
     "ttdk_bn_apply": [P, P, P, P, P, P, P, P, L, I, I, P],
     "ttdk_bn_bwd_apply": [P, P, P, P, P, P, L, I, P],

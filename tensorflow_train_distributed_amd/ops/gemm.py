@@ -185,6 +185,11 @@ def conv_fwd(x, w, stride=(1, 1), padding=(0, 0), *, out=None, residual=None, ac
     return out
 
 
+# strided (non-pointwise) dgrad via sub-pixel phase decomposition; TTD_SUBPIXEL_DGRAD=0 keeps
+# the direct strided gather (A/B comparisons)
+_SUBPIXEL = _os.environ.get("TTD_SUBPIXEL_DGRAD", "1") != "0"
+
+
 def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
                tile=(0, 0)):
     """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
@@ -200,8 +205,17 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     if out is None:
         alloc = torch.zeros if (strided_pw and not beta) else torch.empty
         out = alloc(tuple(x_shape), dtype=torch.bfloat16, device=dy.device)
-    _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * (g.P * g.Q if strided_pw else g.H * g.W), C, R * S * K)
     e = _epi(out, ldo=C, beta=beta, residual=residual)
+    if (_SUBPIXEL and not strided_pw and g.sh == g.sw and g.sh > 1 and R >= g.sh and S >= g.sw and residual is None
+            and tile == (0, 0)):
+        # strided dgrad as s*s unit-stride phase GEMMs (skips the zero taps of the direct gather)
+        _log("dgrad_%dx%d_s%d_subpixel" % (R, S, stride[0]), g.N * g.H * g.W // (g.sh * g.sw), C,
+             R * S * K // (g.sh * g.sw))
+        ws = torch.empty_like(wt)
+        _lib.call("ttdk_conv_dgrad_subpixel", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), ws.data_ptr(),
+                  ctypes.byref(e), _lib.stream())
+        return out
+    _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * (g.P * g.Q if strided_pw else g.H * g.W), C, R * S * K)
     _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), tile[0], tile[1], ctypes.byref(e),
               _lib.stream())
     return out

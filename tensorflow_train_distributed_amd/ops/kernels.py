@@ -52,6 +52,24 @@ class BNState:
         self.mean, self.rstd, self.scale, self.shift = buf[0], buf[1], buf[2], buf[3]
 
 
+def _bn_reduce_finalize(partial, T, C, bwd, count, gamma=None, beta=None, eps=0.0, momentum=0.0,
+                        running_mean=None, running_var=None, state=None, dgamma=None, dbeta=None, coef=None,
+                        accumulate=False):
+    S = _lib.query("ttdk_bn_finalize_slices", T)
+    slab = torch.empty((S, 2, C), dtype=torch.float32, device=partial.device)
+    _lib.call("ttdk_bn_reduce_finalize", partial.data_ptr(), T, C, slab.data_ptr(), int(bwd), float(count), _p(gamma), _p(beta), float(eps),
+              float(momentum), _p(running_mean), _p(running_var), state.mean.data_ptr(), state.rstd.data_ptr(),
+              state.scale.data_ptr(), state.shift.data_ptr(), _p(dgamma), _p(dbeta), _p(coef), int(accumulate),
+              _s())
+
+
+def bn_fwd_stats(partial, T, count, gamma, beta, eps, momentum, running_mean, running_var, state):
+    """Fold the per-tile partial sums [T, 2, C] (conv epilogue or bn_stats_partial) and
+    finalize the forward statistics into `state` in one launch."""
+    _bn_reduce_finalize(partial, T, partial.shape[-1], False, count, gamma, beta, eps, momentum, running_mean,
+                        running_var, state)
+
+
 def bn_fwd_finalize(sums, count, gamma, beta, eps, momentum, running_mean, running_var, state):
     C = sums.shape[-1]
     _lib.call("ttdk_bn_fwd_finalize", sums.data_ptr(), float(count), C, _p(gamma), _p(beta), float(eps),
@@ -94,10 +112,9 @@ def bn_backward(dout, out_for_relu, y, gamma, state, dgamma, dbeta, *, g_out=Non
     partial = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
     _lib.call("ttdk_bn_bwd_partial", dout.data_ptr(), _p(out_for_relu), _p(mask), y.data_ptr(), M, C,
               partial.data_ptr(), T, _p(g_out), _s())
-    sums = bn_reduce_partials(partial, T, C)
     coef = torch.empty((3, C), dtype=torch.float32, device=y.device)
-    _lib.call("ttdk_bn_bwd_finalize", sums.data_ptr(), float(M), C, _p(gamma), state.mean.data_ptr(),
-              state.rstd.data_ptr(), _p(dgamma), _p(dbeta), coef.data_ptr(), int(accumulate), _s())
+    _bn_reduce_finalize(partial, T, C, True, M, gamma, state=state, dgamma=dgamma, dbeta=dbeta, coef=coef,
+                        accumulate=accumulate)
     if dz is None:
         dz = torch.empty_like(y)
     _lib.call("ttdk_bn_bwd_apply", dout.data_ptr(), _p(out_for_relu), _p(mask), y.data_ptr(), coef.data_ptr(),

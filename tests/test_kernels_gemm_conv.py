@@ -93,6 +93,42 @@ def test_conv_fwd_dgrad_wgrad(cfg):
     assert _rel(dw1, wr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", [
+    # N, H, W, C, K, R, stride, pad — odd extents (unequal phases), stride 3, 5x5, big-tile phases
+    (2, 15, 13, 32, 64, 3, 2, 1),
+    (2, 12, 12, 16, 64, 3, 3, 1),
+    (2, 9, 9, 16, 64, 5, 2, 2),
+    (8, 56, 56, 128, 128, 3, 2, 1),
+])
+def test_conv_dgrad_subpixel_phases(cfg):
+    """Strided dgrad as s*s unit-stride phase GEMMs vs the fp32 reference, vs the direct
+    strided gather, and with beta accumulation into an existing gradient."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    N, H, W, C, K, R, s, p = cfg
+    torch.manual_seed(7)
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    w = (torch.randn(K, R, R, C, device="cuda") / (R * R * C) ** 0.5).bfloat16()
+    xr = _nchw(x.float()).requires_grad_(True)
+    yr = F.conv2d(xr, w.float().permute(0, 3, 1, 2), stride=s, padding=p)
+    dy = torch.randn(N, yr.shape[2], yr.shape[3], K, device="cuda").bfloat16()
+    yr.backward(_nchw(dy.float()))
+    ref = _nhwc(xr.grad)
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    assert G._SUBPIXEL
+    dx = G.conv_dgrad(dy, wt, x.shape, (s, s), (p, p))
+    assert _rel(dx, ref) < 1e-2
+    G._SUBPIXEL = False
+    try:
+        dx_direct = G.conv_dgrad(dy, wt, x.shape, (s, s), (p, p))
+    finally:
+        G._SUBPIXEL = True
+    assert _rel(dx, dx_direct.float()) < 1e-2
+    prev = torch.randn_like(dx)
+    acc = prev.clone()
+    G.conv_dgrad(dy, wt, x.shape, (s, s), (p, p), out=acc, beta=1)
+    assert _rel(acc, ref + prev.float()) < 1e-2
+
+
 def test_conv_bn_stat_epilogue_big_tile():
     from tensorflow_train_distributed_amd.ops import gemm as G
     torch.manual_seed(4)

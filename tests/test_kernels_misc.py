@@ -55,6 +55,36 @@ def test_batchnorm_fwd_bwd_relu_residual():
     torch.testing.assert_close(dg2, dg) and torch.testing.assert_close(db2, db)
 
 
+@pytest.mark.parametrize("M,C", [(3000, 96), (200000, 40), (50000, 2048)])
+def test_bn_fused_reduce_finalize_matches_unfused(M, C):
+    """Slice reduction + finalize (two launches, no atomics) == the memset/atomic-reduce/finalize
+    sequence, for fwd and bwd, called repeatedly."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(M + C)
+    y = (torch.randn(M, C, device="cuda") * 2 + 1).bfloat16()
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda")
+    partial, T = K.bn_stats_partial(y)
+    ref = K.BNState(C, "cuda")
+    rm0, rv0 = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    K.bn_fwd_finalize(K.bn_reduce_partials(partial, T, C), M, gamma, beta, 1e-5, 0.9, rm0, rv0, ref)
+    for _ in range(3):
+        st = K.BNState(C, "cuda")
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        K.bn_fwd_stats(partial, T, M, gamma, beta, 1e-5, 0.9, rm, rv, st)
+        for a, b in ((st.mean, ref.mean), (st.rstd, ref.rstd), (st.scale, ref.scale), (st.shift, ref.shift),
+                     (rm, rm0), (rv, rv0)):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    dout = torch.randn(M, C, device="cuda").bfloat16()
+    yr = y.float().requires_grad_(True)
+    g_r = gamma.clone().requires_grad_(True)
+    F.batch_norm(yr, None, None, g_r, None, training=True, eps=1e-5).backward(dout.float())
+    dg, db = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    dz = K.bn_backward(dout, None, y, gamma, st, dg, db)
+    assert _rel(dz, yr.grad) < 2e-2 and _rel(dg, g_r.grad) < 1e-2
+    torch.testing.assert_close(db, dout.float().sum(0), rtol=1e-3, atol=1e-2)
+
+
 def test_maxpool_avgpool():
     from tensorflow_train_distributed_amd.ops import kernels as K
     torch.manual_seed(1)
