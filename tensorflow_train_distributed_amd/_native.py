@@ -172,8 +172,12 @@ def hip() -> ctypes.CDLL:
     if _hip is None:
         with _lock:
             if _hip is None:
-                _ensure("hip", HIP_LIB, build_hip)
-                _hip = ctypes.CDLL(HIP_LIB)
+                alt = os.environ.get("TTD_HIP_LIB_OVERRIDE")  # A/B runs against another build
+                if alt:
+                    _hip = ctypes.CDLL(alt)
+                else:
+                    _ensure("hip", HIP_LIB, build_hip)
+                    _hip = ctypes.CDLL(HIP_LIB)
     return _hip
 
 

@@ -376,6 +376,111 @@ __device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
   return (static_cast<long long>(n) * E.rOH + p * E.rs) * E.rOW + q * E.rs;
 }
 
+// Row loop of the bf16 epilogues (both kernels): one thread owns 16-B column chunk `c` of
+// rows r0, r0+RPP, ... of the LDS-staged tile. Rows go in batches of EB with every
+// residual / accumulate (beta) load of the batch issued before any of them is used: with one
+// workgroup per CU (LDS-bound tiles) a load-use per row left the epilogue latency-bound,
+// which is what capped the K <= 128 ResNet 1x1 GEMMs at ~50% of HBM bandwidth.
+template <int BM, int RPP, int PITCH, bool PF>
+__device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, int c, int r0, int n, int m0, int M,
+                                         int N, bool vst, bool vres, const float (&bias8)[8], float (&s8)[8],
+                                         float (&q8)[8]) {
+  constexpr int NR = (BM + RPP - 1) / RPP;
+  constexpr int EB = !PF ? 1 : (NR < 8 ? NR : 8);
+  bf16_t* out = static_cast<bf16_t*>(E.out);
+  if (n >= N) return;
+#pragma unroll 1
+  for (int rb = r0; rb < BM; rb += RPP * EB) {
+    uint4 pres[EB], pold[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int r = rb + u * RPP, m = m0 + r;
+      if (r < BM && m < M) {
+        if (E.residual && vres) pres[u] = *reinterpret_cast<const uint4*>(E.residual + static_cast<long long>(m) * E.ldr + n);
+        if (E.beta && vst) pold[u] = *reinterpret_cast<const uint4*>(out + out_row(E, m) * E.ldo + n);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int r = rb + u * RPP, m = m0 + r;
+      if (r >= BM || m >= M) break;
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += bias8[j];
+      if (E.residual) {
+        const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
+        float rv[8];
+        if (vres) {
+          unpack8(pres[u], rv);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rv[j] = n + j < N ? bf2f(rp[j]) : 0.f;
+        }
+        if (E.act == kActDGelu) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] *= gelu_tanh_grad(rv[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] += rv[j];
+        }
+      }
+      bf16_t* op = out + out_row(E, m) * E.ldo + n;
+      if (E.beta) {
+        float ov[8];
+        if (vst) {
+          unpack8(pold[u], ov);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ov[j] = n + j < N ? bf2f(op[j]) : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += ov[j];
+      }
+      if (E.aux) {
+        bf16_t* ap = E.aux + out_row(E, m) * E.ldo + n;
+        const uint4 pa = pack8(f);
+        if (vst) {
+          *reinterpret_cast<uint4*>(ap) = pa;
+        } else {
+          const uint32_t w[4] = {pa.x, pa.y, pa.z, pa.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (n + j < N) ap[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+        }
+      }
+      if (E.act == kActRelu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      } else if (E.act == kActGelu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
+      } else if (E.act == kActTanh) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = tanhf(f[j]);
+      }
+      const uint4 packed = pack8(f);
+      if (vst) {
+        *reinterpret_cast<uint4*>(op) = packed;
+      } else {
+        const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n + j < N) op[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+      }
+      if (E.stat) {
+        float sv[8];
+        unpack8(packed, sv);  // statistics of the values actually stored
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s8[j] += sv[j];
+          q8[j] += sv[j] * sv[j];
+        }
+      }
+    }
+  }
+}
+
 template <int BM, int BN>
 __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM / 32][BN / 32], int m0, int n0,
                                          int mwave, int nwave, int lane, int M, int N, int split, int tile_m,
@@ -431,90 +536,16 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
   const bool nfull = n + 8 <= N;
   const bool vst = nfull && (E.ldo & 7) == 0;
   const bool vres = nfull && (E.ldr & 7) == 0;
-  bf16_t* out = static_cast<bf16_t*>(E.out);
   float bias8[8], s8[8], q8[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
     s8[j] = q8[j] = 0.f;
   }
-  for (int r = r0; r < BM; r += RPP) {
-    const int m = m0 + r;
-    if (m >= M || n >= N) break;
-    float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16), f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] += bias8[j];
-    if (E.residual) {
-      const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
-      float rv[8];
-      if (vres) {
-        unpack8(*reinterpret_cast<const uint4*>(rp), rv);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) rv[j] = n + j < N ? bf2f(rp[j]) : 0.f;
-      }
-      if (E.act == kActDGelu) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= gelu_tanh_grad(rv[j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += rv[j];
-      }
-    }
-    bf16_t* op = out + out_row(E, m) * E.ldo + n;
-    if (E.beta) {
-      float ov[8];
-      if (vst) {
-        unpack8(*reinterpret_cast<const uint4*>(op), ov);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ov[j] = n + j < N ? bf2f(op[j]) : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += ov[j];
-    }
-    if (E.aux) {
-      bf16_t* ap = E.aux + out_row(E, m) * E.ldo + n;
-      const uint4 pa = pack8(f);
-      if (vst) {
-        *reinterpret_cast<uint4*>(ap) = pa;
-      } else {
-        const uint32_t w[4] = {pa.x, pa.y, pa.z, pa.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (n + j < N) ap[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
-      }
-    }
-    if (E.act == kActRelu) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-    } else if (E.act == kActGelu) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
-    } else if (E.act == kActTanh) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = tanhf(f[j]);
-    }
-    const uint4 packed = pack8(f);
-    if (vst) {
-      *reinterpret_cast<uint4*>(op) = packed;
-    } else {
-      const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (n + j < N) op[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
-    }
-    if (E.stat) {
-      float sv[8];
-      unpack8(packed, sv);  // statistics of the values actually stored
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s8[j] += sv[j];
-        q8[j] += sv[j] * sv[j];
-      }
-    }
-  }
+  if (E.beta || E.residual)  // batched loads only where there are loads (no cost to plain stores)
+    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+  else
+    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
   if (E.stat) {
     // lanes sharing a chunk column: lane % CPR equal -> reduce over the wave, then over 4 waves.
 #pragma unroll
@@ -1133,90 +1164,16 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
   const bool nfull = n + 8 <= N;
   const bool vst = nfull && (E.ldo & 7) == 0;
   const bool vres = nfull && (E.ldr & 7) == 0;
-  bf16_t* out = static_cast<bf16_t*>(E.out);
   float bias8[8], s8[8], q8[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
     s8[j] = q8[j] = 0.f;
   }
-  for (int r = r0; r < BM; r += RPP) {
-    const int m = m0 + r;
-    if (m >= M || n >= N) break;
-    float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16), f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] += bias8[j];
-    if (E.residual) {
-      const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
-      float rv[8];
-      if (vres) {
-        unpack8(*reinterpret_cast<const uint4*>(rp), rv);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) rv[j] = n + j < N ? bf2f(rp[j]) : 0.f;
-      }
-      if (E.act == kActDGelu) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= gelu_tanh_grad(rv[j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += rv[j];
-      }
-    }
-    bf16_t* op = out + out_row(E, m) * E.ldo + n;
-    if (E.beta) {
-      float ov[8];
-      if (vst) {
-        unpack8(*reinterpret_cast<const uint4*>(op), ov);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ov[j] = n + j < N ? bf2f(op[j]) : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += ov[j];
-    }
-    if (E.aux) {
-      bf16_t* ap = E.aux + out_row(E, m) * E.ldo + n;
-      const uint4 pa8 = pack8(f);
-      if (vst) {
-        *reinterpret_cast<uint4*>(ap) = pa8;
-      } else {
-        const uint32_t w[4] = {pa8.x, pa8.y, pa8.z, pa8.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (n + j < N) ap[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
-      }
-    }
-    if (E.act == kActRelu) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-    } else if (E.act == kActGelu) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
-    } else if (E.act == kActTanh) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = tanhf(f[j]);
-    }
-    const uint4 packed = pack8(f);
-    if (vst) {
-      *reinterpret_cast<uint4*>(op) = packed;
-    } else {
-      const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (n + j < N) op[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
-    }
-    if (E.stat) {
-      float sv[8];
-      unpack8(packed, sv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s8[j] += sv[j];
-        q8[j] += sv[j] * sv[j];
-      }
-    }
-  }
+  if (E.beta || E.residual)  // batched loads only where there are loads (no cost to plain stores)
+    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+  else
+    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
   if (E.stat) {
     // threads sharing a chunk column c: tid % CPR equal -> within a wave lanes c, c+CPR, ...
 #pragma unroll

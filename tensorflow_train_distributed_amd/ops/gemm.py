@@ -190,6 +190,18 @@ def conv_fwd(x, w, stride=(1, 1), padding=(0, 0), *, out=None, residual=None, ac
 _SUBPIXEL = _os.environ.get("TTD_SUBPIXEL_DGRAD", "1") != "0"
 
 
+def _phases(s, pad, R, H):
+    """(taps, extent) of each sub-pixel phase along one axis (mirror of gemm_conv.hip phase_of)."""
+    out = []
+    for a in range(s):
+        r0 = (a + pad) % s
+        T = (R - r0 + s - 1) // s if r0 < R else 0
+        n = (H - a + s - 1) // s if a < H else 0
+        if n:
+            out.append((T, n))
+    return out
+
+
 def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
                tile=(0, 0)):
     """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
@@ -209,8 +221,11 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     if (_SUBPIXEL and not strided_pw and g.sh == g.sw and g.sh > 1 and R >= g.sh and S >= g.sw and residual is None
             and tile == (0, 0)):
         # strided dgrad as s*s unit-stride phase GEMMs (skips the zero taps of the direct gather)
-        _log("dgrad_%dx%d_s%d_subpixel" % (R, S, stride[0]), g.N * g.H * g.W // (g.sh * g.sw), C,
-             R * S * K // (g.sh * g.sw))
+        if _LOG is not None:  # one GEMM per phase, in ttdk_conv_dgrad_subpixel's launch order
+            for pa in _phases(g.sh, g.ph, R, g.H):
+                for pb in _phases(g.sw, g.pw, S, g.W):
+                    _log("dgrad_%dx%d_s%d_phase%dx%d" % (R, S, g.sh, pa[0], pb[0]), g.N * pa[1] * pb[1], C,
+                         pa[0] * pb[0] * K)
         ws = torch.empty_like(wt)
         _lib.call("ttdk_conv_dgrad_subpixel", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), ws.data_ptr(),
                   ctypes.byref(e), _lib.stream())
