@@ -8,3 +8,4 @@ from .strategy import (CommunicationImplementation, CommunicationOptions, CrossD
                        InputContext, MirroredStrategy, MultiWorkerMirroredStrategy, NcclAllReduce, OneDeviceStrategy,
                        ParameterServerStrategy, RcclAllReduce, ReduceOp, ReductionToOneDevice, Strategy,
                        get_strategy, has_strategy, in_cross_replica_context)
+from .fault import FaultInjectionHook, FaultInjector, Heartbeat, HeartbeatHook, as_preemption_error

@@ -90,11 +90,15 @@ class BucketedAllReducer:
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
-        for w, c, t in self._works:
-            w.wait()
+        works, self._works = self._works, []
+        for w, c, t in works:
+            try:
+                w.wait()
+            except Exception as e:  # noqa: BLE001 - an aborted/failed communicator is a preemption
+                from .fault import as_preemption_error
+                raise as_preemption_error(e) from e
             if c is not None:
                 t.copy_(c)
-        self._works = []
 
 
 def allreduce_mean_(tensor: torch.Tensor, group=None):

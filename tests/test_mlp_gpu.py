@@ -1,0 +1,127 @@
+"""The reference workload itself on the MI355X (SURVEY.md §7.3 "minimum slice B"): the
+784-200-100-50-25-10 ELU/dropout MLP of /root/reference/distribute_training.py:39-110 run by
+the HIP kernels (MFMA GEMMs, fused bias+ELU+dropout, fused xent+in_top_k, flat SGD):
+
+* GPU step == fp32 CPU reference step (dropout off so both see the same function);
+* the reference training loop (global step, staircase exponential decay, GradientDescent,
+  MonitoredTrainingSession with StopAtStepHook + checkpoints) trains on the GPU engine;
+* the whole step (forward, backward, optimizer) replays from one hipGraph bit-identically;
+* the bucketed gradient all-reduce runs through RCCL (single-rank communicator).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import tensorflow_train_distributed_amd as ttd
+from tensorflow_train_distributed_amd.data import mnist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mnist_dir(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("mnist_gpu"))
+    mnist.write_synthetic(d, n_train=4000, n_test=200)
+    return d
+
+
+def _batch(seed, B=128):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand((B, 784), generator=g)
+    y = torch.randint(0, 10, (B,), generator=g)
+    return x, y
+
+
+def test_reference_mlp_gpu_step_matches_cpu():
+    cpu = ttd.models.mnist_mlp(device="cpu", seed=5, dropout_rate=0.0)
+    gpu = ttd.models.mnist_mlp(device="cuda", seed=5, dropout_rate=0.0)
+    torch.testing.assert_close(gpu.params.master.cpu(), cpu.params.master)
+    x, y = _batch(0)
+    rc = cpu.forward_backward({"x-input": x, "y-input": y})
+    rg = gpu.forward_backward({"x-input": x, "y-input": y})
+    torch.cuda.synchronize()
+    assert abs(float(rg["loss"]) - float(rc["loss"])) < 2e-2 * max(1.0, float(rc["loss"]))
+    assert abs(float(rg["accuracy"]) - float(rc["accuracy"])) <= 2.0 / 128
+    for n in cpu.params.names():
+        a, b = gpu.params.g[n].float().cpu(), cpu.params.g[n]
+        rel = float((a - b).norm() / (b.norm() + 1e-12))
+        assert rel < 3e-2, (n, rel)
+
+
+def test_reference_training_loop_on_gpu(tmp_path, mnist_dir):
+    data = mnist.read_data_sets(mnist_dir, seed=0)
+    ttd.train.reset_default_graph()
+    gs = ttd.train.get_or_create_global_step()
+    model = ttd.models.mnist_mlp(device="cuda", seed=0)
+    lr = ttd.train.exponential_decay(0.05, gs, 468, 0.96, staircase=True)
+    op = ttd.train.GradientDescentOptimizer(lr).minimize(model, global_step=gs)
+    x = ttd.placeholder(torch.float32, [None, 784], "x-input")
+    y = ttd.placeholder(torch.int64, [None], "y-input")
+    losses = []
+    ck = str(tmp_path / "ck")
+    with ttd.train.MonitoredTrainingSession(checkpoint_dir=ck, hooks=[ttd.train.StopAtStepHook(last_step=150)],
+                                            save_checkpoint_steps=100, save_summaries_steps=50) as sess:
+        while not sess.should_stop():
+            bx, by = data.train.next_batch(128)
+            _, l, g = sess.run([op, op.loss, gs], feed_dict={x: bx, y: by})
+            losses.append(l)
+    assert g == 150 and len(losses) == 150
+    assert np.mean(losses[-20:]) < np.mean(losses[:20]) - 0.3, (losses[:5], losses[-5:])
+    keys = dict(ttd.train.list_variables(ttd.train.latest_checkpoint(ck)))
+    assert keys["hidden1/kernel"] == (784, 200) and keys["output/bias"] == (10,)
+    ttd.train.reset_default_graph()
+
+
+def test_reference_mlp_step_hipgraph_replay_is_bit_identical():
+    from tensorflow_train_distributed_amd.train.flat import FlatSGD, Schedule
+    from tensorflow_train_distributed_amd.utils.graphs import capture
+
+    def make():
+        m = ttd.models.mnist_mlp(device="cuda", seed=9, dropout_rate=0.0)
+        return m, FlatSGD(m.params, Schedule(kind=0, base_lr=0.05))
+
+    x, y = _batch(1)
+    xd, yd = x.cuda(), y.cuda()
+    eager, opt_e = make()
+    for _ in range(4):
+        eager.forward_backward({"x-input": xd, "y-input": yd})
+        opt_e.step()
+    graphed, opt_g = make()
+
+    def step():
+        out = graphed.forward_backward({"x-input": xd, "y-input": yd})
+        opt_g.step()
+        return out
+
+    cs, _ = capture(step, warmup=1)  # warmup = eager step 1, capture records (does not run) one step
+    for _ in range(3):
+        cs.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(graphed.params.master, eager.params.master)
+
+
+def test_bucketed_allreduce_through_rccl_single_rank(tmp_path):
+    import torch.distributed as dist
+    from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        m = ttd.models.mnist_mlp(device="cuda", seed=4, dropout_rate=0.0)
+        red = BucketedAllReducer(m.params, bucket_mb=0.25, first_bucket_mb=0.05)
+        red.world = 2  # force the collective path on a single-rank communicator (SUM over 1 rank == identity)
+        assert len(red.buckets) >= 3
+        x, y = _batch(2)
+        red.begin()
+        m.forward_backward({"x-input": x.cuda(), "y-input": y.cuda()}, grad_hook=red.mark_ready)
+        early = list(red.launch_log)
+        red.finish()
+        ref = m.params.grad.clone()
+        torch.cuda.synchronize()
+        assert early and early == list(range(len(early)))  # buckets launched during backward, in order
+        assert red.launch_log == list(range(len(red.buckets)))
+        assert torch.equal(m.params.grad, ref)
+        assert float(ref.abs().sum()) > 0
+    finally:
+        dist.destroy_process_group()
