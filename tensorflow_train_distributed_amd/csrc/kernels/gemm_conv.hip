@@ -359,6 +359,12 @@ struct EpiParams {
   bf16_t* aux;  // optional: pre-activation copy (GELU backward input), row stride ldo
   const float* ascale0;  // optional device scalars multiplied into alpha (fp8 dequant scales)
   const float* ascale1;
+  // BN-backward statistics of the produced gradient (dgrad feeding a conv+BN(+ReLU) unit):
+  // with `by` set the stored value is g = v * mask (ReLU bit per element, `bmask`, optional)
+  // and `stat` receives per-tile (sum g, sum g*y) with y = by (the unit's pre-BN conv output,
+  // same layout as out) — the separate bwd-partial pass over dy and y disappears.
+  const bf16_t* by;
+  const uint8_t* bmask;
 };
 
 __device__ __forceinline__ float epi_alpha(const EpiParams& E) {
@@ -391,13 +397,19 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
   if (n >= N) return;
 #pragma unroll 1
   for (int rb = r0; rb < BM; rb += RPP * EB) {
-    uint4 pres[EB], pold[EB];
+    uint4 pres[EB], pold[EB], pby[EB];
+    uint32_t pmb[EB];
 #pragma unroll
     for (int u = 0; u < EB; ++u) {
       const int r = rb + u * RPP, m = m0 + r;
       if (r < BM && m < M) {
         if (E.residual && vres) pres[u] = *reinterpret_cast<const uint4*>(E.residual + static_cast<long long>(m) * E.ldr + n);
         if (E.beta && vst) pold[u] = *reinterpret_cast<const uint4*>(out + out_row(E, m) * E.ldo + n);
+        if (E.by) {  // vst is guaranteed by the host (N % 8 == 0, ldo % 8 == 0)
+          const long long o = out_row(E, m) * E.ldo + n;
+          pby[u] = *reinterpret_cast<const uint4*>(E.by + o);
+          pmb[u] = E.bmask ? E.bmask[o >> 3] : 0xffu;
+        }
       }
     }
 #pragma unroll
@@ -459,6 +471,10 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = tanhf(f[j]);
       }
+      if (E.by) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (pmb[u] >> j) & 1u ? f[j] : 0.f;
+      }
       const uint4 packed = pack8(f);
       if (vst) {
         *reinterpret_cast<uint4*>(op) = packed;
@@ -468,7 +484,16 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
         for (int j = 0; j < 8; ++j)
           if (n + j < N) op[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
       }
-      if (E.stat) {
+      if (E.by) {
+        float sv[8], yv[8];
+        unpack8(packed, sv);  // statistics of the gradient actually stored
+        unpack8(pby[u], yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s8[j] += sv[j];
+          q8[j] += sv[j] * yv[j];
+        }
+      } else if (E.stat) {
         float sv[8];
         unpack8(packed, sv);  // statistics of the values actually stored
 #pragma unroll
@@ -542,7 +567,7 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
     bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
     s8[j] = q8[j] = 0.f;
   }
-  if (E.beta || E.residual)  // batched loads only where there are loads (no cost to plain stores)
+  if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
     epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
   else
     epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
@@ -1170,7 +1195,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
     bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
     s8[j] = q8[j] = 0.f;
   }
-  if (E.beta || E.residual)  // batched loads only where there are loads (no cost to plain stores)
+  if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
     epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
   else
     epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
@@ -1319,6 +1344,8 @@ struct TtdkEpilogue {
   bf16_t* aux;  // optional second bf16 output: the pre-activation value (same layout as out)
   const float* ascale0;  // optional device scalars multiplied into alpha (fp8 dequant scales)
   const float* ascale1;
+  const bf16_t* by;      // optional BN-backward statistics source (see EpiParams::by)
+  const uint8_t* bmask;
 };
 
 static EpiParams to_epi(const TtdkEpilogue* e) {
@@ -1343,6 +1370,8 @@ static EpiParams to_epi(const TtdkEpilogue* e) {
   p.aux = e->aux;
   p.ascale0 = e->ascale0;
   p.ascale1 = e->ascale1;
+  p.by = e->by;
+  p.bmask = e->bmask;
   return p;
 }
 
@@ -1470,6 +1499,8 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
                                 const TtdkEpilogue* epi, hipStream_t st) {
   if (g->K % 8) return hipErrorInvalidValue;
   EpiParams pe = to_epi(epi);
+  if (pe.by && (pe.stat == nullptr || pe.mode != 0 || g->C % 8 || pe.ldo % 8 || pe.residual || pe.act))
+    return hipErrorInvalidValue;
   const int N = g->C, K = g->R * g->S * g->K;
   DenseParams pb{wt, K, N, K};
   if (g->R == 1 && g->S == 1 && g->ph == 0 && g->pw == 0) {
@@ -1485,9 +1516,12 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
       pe.rs = g->sh;
     }
     const int bbn = big_bn(M, N, K);
-    if ((bm == 0 || bm == 256) && bbn && pe.stat == nullptr)  // the big epilogue honours the row remap
+    // per-tile statistics need the caller to know the tile height: with `stat` the 256-row
+    // kernel runs only on an explicit bm == 256 request (and must then be eligible)
+    if (((bm == 0 && pe.stat == nullptr) || bm == 256) && bbn && (bm != 256 || bn == bbn))
       return bbn == 256 ? big::dense<256>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st)
                         : big::dense<128>(dy, g->K, true, wt, K, true, pe, M, N, K, 1, st);
+    if (bm == 256 && pe.stat) return hipErrorInvalidValue;
     if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
     return dispatch<KDense, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
   }
@@ -1500,7 +1534,8 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
     return e != nullptr && e[0] == '1';
   }();
   const bool unit = g->sh == 1 && g->sw == 1;
-  if ((bm == 0 || bm == 256) && bbn && g->K % 64 == 0 && pe.stat == nullptr && !pe.remap && (unit || strided_big)) {
+  if (((bm == 0 && pe.stat == nullptr) || bm == 256) && bbn && (bm != 256 || bn == bbn) && g->K % 64 == 0 &&
+      !pe.remap && (unit || strided_big)) {
     const big::ConvP pa = conv_params(dy, g->P, g->Q, g->K, g->H, g->W, g, M);
     const big::DenseP pb2{wt, K, N};
     if (unit) {
@@ -1512,6 +1547,7 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
       return big::launch<256, big::OpConvK<128, 2, true>, big::OpDenseK<128, 2>>(pa, pb2, pe, M, N, K, 1, st);
     return big::launch<128, big::OpConvK<128, 2, true>, big::OpDenseK<64, 2>>(pa, pb2, pe, M, N, K, 1, st);
   }
+  if (bm == 256 && pe.stat) return hipErrorInvalidValue;
   if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
   GatherParams pa{dy, g->P, g->Q, g->K, g->H, g->W, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, M, K};
   return dispatch<KConvDgrad, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);

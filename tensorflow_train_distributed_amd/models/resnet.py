@@ -21,6 +21,7 @@ conversion to TF's [R,S,C,K] kernel layout happens in the checkpoint layer.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -79,6 +80,9 @@ class ResNet:
         if precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
         self.precision = precision
+        # dgrad epilogues emit the next BN-backward's masked gradient + partial sums
+        # (TTD_FUSE_BN_BWD=0 restores the separate statistics pass, for A/B runs)
+        self.fuse_bn_bwd = os.environ.get("TTD_FUSE_BN_BWD", "1") != "0"
         self.device = torch.device(device)
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -234,7 +238,13 @@ class ResNet:
             return out, (x, y, mask, st), (q8, slot)
         return out, (x, y, mask, st)
 
-    def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0):
+    def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0, dstat=None,
+                    feeds=None):
+        """Backward of one conv+BN(+ReLU) unit. dout: gradient of the unit's output; with
+        dstat = (partial, T) it is already ReLU-masked and its BN-backward sums came from the
+        producing dgrad's epilogue. feeds: ctx of the conv+BN unit whose output is this conv's
+        input — the dgrad epilogue then emits that unit's masked gradient + sums.
+        Returns (dx, dstat_of_dx)."""
         from ..ops import gemm as G
         from ..ops import kernels as K
         P = self.params
@@ -242,16 +252,26 @@ class ResNet:
         N, Pp, Q, Kc = y.shape
         M = N * Pp * Q
         pre = c.name + "_bn/"
-        dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
-                           P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
-                           mask=mask).view(N, Pp, Q, Kc)
+        if dstat is not None:
+            dz = K.bn_backward_from_partial(dout.view(M, Kc), y.view(M, Kc), P.var[pre + "gamma"], st,
+                                            P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1]).view(N, Pp, Q, Kc)
+        else:
+            dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
+                               P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
+                               mask=mask).view(N, Pp, Q, Kc)
         wname = c.name + "_conv/kernel"
         G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
         self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
         if not need_dx:
-            return None
+            return None, None
         wt = K.krsc_to_crsk(P.c[wname])
-        return G.conv_dgrad(dz, wt, x.shape, (c.stride, c.stride), (c.pad, c.pad), out=dx, beta=dx_beta)
+        stride, pad = (c.stride, c.stride), (c.pad, c.pad)
+        if (feeds is not None and self.fuse_bn_bwd
+                and G.dgrad_stat_tile(tuple(x.shape), tuple(wt.shape), stride, pad) is not None):
+            _, fy, fmask, _ = feeds
+            out, partial, T = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, bn_stat=(fy, fmask))
+            return out, (partial, T)
+        return G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta), None
 
     def _ready(self, name):
         if self._grad_hook is not None:
@@ -308,15 +328,23 @@ class ResNet:
         self._ready("predictions/bias")
         dpooled = G.gemm(dlogits, P.c["predictions/kernel"], trans_b=True)
         dh = K.avgpool_bwd(dpooled, feat_shape)
-        for blk, (c1, c2, c3, cd) in zip(reversed(self.blocks), reversed(ctxs)):
-            g_sc = torch.empty_like(dh)
-            d2 = self._convbn_bwd(blk["c3"], dh, c3, g_out=g_sc)
-            d1 = self._convbn_bwd(blk["c2"], d2, c2)
+        dh_stat = None  # (partial, T) when dh is already the masked gradient of the block's c3 unit
+        for i in reversed(range(len(self.blocks))):
+            blk = self.blocks[i]
+            c1, c2, c3, cd = ctxs[i]
+            prev_c3 = ctxs[i - 1][2] if i > 0 else None  # the unit that produced this block's input
+            if dh_stat is not None:
+                g_sc = dh  # already ReLU-masked by the producing dgrad epilogue
+                d2, st2 = self._convbn_bwd(blk["c3"], dh, c3, dstat=dh_stat, feeds=c2)
+            else:
+                g_sc = torch.empty_like(dh)
+                d2, st2 = self._convbn_bwd(blk["c3"], dh, c3, g_out=g_sc, feeds=c2)
+            d1, st1 = self._convbn_bwd(blk["c2"], d2, c2, dstat=st2, feeds=c1)
             if blk["cd"] is not None:
-                dx = self._convbn_bwd(blk["cd"], g_sc, cd)
+                dx, _ = self._convbn_bwd(blk["cd"], g_sc, cd)
             else:
                 dx = g_sc
-            dh = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1)
+            dh, dh_stat = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1, dstat=st1, feeds=prev_c3)
         dstem = K.maxpool_bwd(dh, arg, s_out.shape, 3, 2, 1)
         self._convbn_bwd(self.stem, dstem, s_ctx, need_dx=False)
         self._grad_hook = None

@@ -32,7 +32,7 @@ class Epilogue(ctypes.Structure):
         ("bias", c_void_p), ("residual", c_void_p), ("ldr", c_longlong), ("act", c_int),
         ("beta", c_int), ("remap", c_int), ("rP", c_int), ("rQ", c_int), ("rOH", c_int),
         ("rOW", c_int), ("rs", c_int), ("stat", c_void_p), ("alpha", c_float), ("aux", c_void_p),
-        ("ascale0", c_void_p), ("ascale1", c_void_p),
+        ("ascale0", c_void_p), ("ascale1", c_void_p), ("by", c_void_p), ("bmask", c_void_p),
     ]
 
 

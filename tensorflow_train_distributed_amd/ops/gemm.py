@@ -33,7 +33,7 @@ def _log(kind, M, N, K, splits=1):
 
 
 def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,
-         slab_stride=0, aux=None, ascale=(None, None)):
+         slab_stride=0, aux=None, ascale=(None, None), by=None, bmask=None):
     e = _lib.Epilogue()
     e.mode = mode
     e.out = out.data_ptr()
@@ -49,6 +49,8 @@ def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat
     e.aux = aux.data_ptr() if aux is not None else None
     e.ascale0 = ascale[0].data_ptr() if ascale[0] is not None else None
     e.ascale1 = ascale[1].data_ptr() if ascale[1] is not None else None
+    e.by = by.data_ptr() if by is not None else None
+    e.bmask = bmask.data_ptr() if bmask is not None else None
     return e
 
 
@@ -202,12 +204,42 @@ def _phases(s, pad, R, H):
     return out
 
 
+def _pick_tile(M, N):
+    """Mirror of the C++ pick_tile() (4-wave kernel tile)."""
+    return (64 if M <= 64 else 128), (64 if N <= 64 else 128)
+
+
+def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
+    """(bm, bn, rows) the data-gradient launcher uses when the epilogue also emits BN-backward
+    statistics (conv_dgrad(bn_stat=...)), or None when that fusion is not available (strided
+    convs: their GEMMs write dx in parts — sub-pixel phases, or only the sampled pixels)."""
+    C, R, S, K = wt_shape
+    N, H, W, _ = x_shape
+    pointwise = R == 1 and S == 1 and tuple(padding) == (0, 0)
+    if tuple(stride) != (1, 1):  # strided: sub-pixel phases / sampled-row remap cover dx only in parts
+        return None
+    if C % 8:
+        return None
+    M = N * H * W
+    Kg = R * S * K
+    bbn = big_bn(M, C, Kg)
+    if bbn and (pointwise or K % 64 == 0):
+        return 256, bbn, -(-M // 256)
+    bm, bn = _pick_tile(M, C)
+    return bm, bn, -(-M // bm)
+
+
 def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
-               tile=(0, 0)):
+               tile=(0, 0), bn_stat=None):
     """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
 
     For strided 1x1 convs only the sampled pixels are written: pass a zero-initialised `out`
     or beta=1 with `out` already holding another gradient contribution.
+
+    bn_stat=(y, mask): dx is the output gradient of a conv+BN(+ReLU) unit whose pre-BN conv
+    output is y (same shape as dx) and ReLU bit mask is `mask` (or None). The epilogue then
+    stores g = dx * mask and per-tile BN-backward partial sums (sum g, sum g*y); returns
+    (out, partial [T, 2, C], T). Requires dgrad_stat_tile(...) to be not None.
     """
     _check(dy, torch.bfloat16, "dy")
     _check(wt, torch.bfloat16, "wt")
@@ -217,6 +249,19 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     if out is None:
         alloc = torch.zeros if (strided_pw and not beta) else torch.empty
         out = alloc(tuple(x_shape), dtype=torch.bfloat16, device=dy.device)
+    if bn_stat is not None:
+        y, mask = bn_stat
+        t = dgrad_stat_tile(tuple(x_shape), tuple(wt.shape), stride, padding)
+        if t is None or residual is not None or tuple(y.shape) != tuple(x_shape):
+            raise ValueError("conv_dgrad: BN-statistics epilogue not available for this conv")
+        _check(y, torch.bfloat16, "bn_stat y")
+        bm, bn, T = t
+        partial = torch.empty((T, 2, C), dtype=torch.float32, device=dy.device)
+        e = _epi(out, ldo=C, beta=beta, stat=partial, by=y, bmask=mask)
+        _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * (g.P * g.Q if strided_pw else g.H * g.W), C, R * S * K)
+        _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), bm, bn, ctypes.byref(e),
+                  _lib.stream())
+        return out, partial, T
     e = _epi(out, ldo=C, beta=beta, residual=residual)
     if (_SUBPIXEL and not strided_pw and g.sh == g.sw and g.sh > 1 and R >= g.sh and S >= g.sw and residual is None
             and tile == (0, 0)):

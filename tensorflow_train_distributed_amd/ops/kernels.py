@@ -122,6 +122,21 @@ def bn_backward(dout, out_for_relu, y, gamma, state, dgamma, dbeta, *, g_out=Non
     return dz
 
 
+def bn_backward_from_partial(g, y, gamma, state, dgamma, dbeta, partial, T, *, dz=None, accumulate=False):
+    """BN backward when the producer of the (already ReLU-masked) gradient g also emitted the
+    per-tile sums (sum g, sum g*y) — ops.gemm.conv_dgrad(bn_stat=...): finalize + one apply
+    pass, no separate statistics pass over g and y."""
+    M, C = y.shape
+    coef = torch.empty((3, C), dtype=torch.float32, device=y.device)
+    _bn_reduce_finalize(partial, T, C, True, M, gamma, state=state, dgamma=dgamma, dbeta=dbeta, coef=coef,
+                        accumulate=accumulate)
+    if dz is None:
+        dz = torch.empty_like(y)
+    _lib.call("ttdk_bn_bwd_apply", g.data_ptr(), None, None, y.data_ptr(), coef.data_ptr(), dz.data_ptr(), M * C, C,
+              _s())
+    return dz
+
+
 # ------------------------------------------------------------------ pooling
 def pool_out(H, k, s, p):
     return (H + 2 * p - k) // s + 1

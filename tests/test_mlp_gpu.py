@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def mnist_dir(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("mnist_gpu"))
-    mnist.write_synthetic(d, n_train=4000, n_test=200)
+    mnist.write_synthetic(d, n_train=8000, n_test=200)
     return d
 
 

@@ -82,7 +82,7 @@ def test_convbn_unit_backward_oracle(which):
     out, ctx = m._convbn_fwd(c, x, relu)
     dout = torch.randn_like(out)
     m._grad_hook = None
-    dx = m._convbn_bwd(c, dout, ctx, need_dx=which != "stem")
+    dx, _ = m._convbn_bwd(c, dout, ctx, need_dx=which != "stem")
     _, y, mask, st = ctx
     g = dout.float() * (out.float() > 0) if relu else dout.float()
     if relu:  # the saved bit mask is exactly [out > 0]

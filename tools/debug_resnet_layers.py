@@ -63,10 +63,10 @@ for i, blk in enumerate(m.blocks[:5] + [None] + m.blocks[13:15]):
     dout = torch.randn_like(o3)
     m._grad_hook = None
     g_sc = torch.empty_like(dout)
-    d2 = m._convbn_bwd(blk["c3"], dout, c3, g_out=g_sc)
-    d1 = m._convbn_bwd(blk["c2"], d2, c2)
-    dx = m._convbn_bwd(blk["cd"], g_sc, cd) if blk["cd"] is not None else g_sc
-    dh = m._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1)
+    d2, _ = m._convbn_bwd(blk["c3"], dout, c3, g_out=g_sc)
+    d1, _ = m._convbn_bwd(blk["c2"], d2, c2)
+    dx = m._convbn_bwd(blk["cd"], g_sc, cd)[0] if blk["cd"] is not None else g_sc
+    dh, _ = m._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1)
     # reference
     names = [blk[k].name for k in ("c1", "c2", "c3", "cd") if blk[k] is not None]
     leaves = {}
