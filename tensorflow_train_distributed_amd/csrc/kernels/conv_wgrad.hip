@@ -1,0 +1,49 @@
+// Convolution weight gradient (split-K); kernels in gemm_conv.h.
+#include "gemm_conv.h"
+
+// dw[K,R,S,C] (fp32) = sum over pixels of dy ⊗ im2col(x). `ws` is a split-K workspace of
+// splits*K*R*S*C floats (may be null when splits == 1, then dw is written directly).
+TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkConv* g, float* dw, float* ws,
+                                int splits, int beta, int bm, int bn, hipStream_t st) {
+  const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
+  if (g->C % 8 || g->K % 8) return hipErrorInvalidValue;
+  const int bbn = (bm == 0 || bm == 256) ? big_bn_wgrad(M, N, K) : 0;
+  if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
+  const int ktiles = ceil_div(K, BK);
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  if (splits > 1 && !ws) return hipErrorInvalidValue;
+  EpiParams pe{};
+  pe.alpha = 1.f;
+  pe.ldo = N;
+  if (splits > 1) {
+    pe.mode = 1;
+    pe.out = ws;
+    pe.slab_stride = static_cast<long long>(M) * N;
+  } else {
+    pe.mode = 2;
+    pe.out = dw;
+    pe.beta = beta;
+  }
+  DenseParams pa{dy, g->K, M, K};
+  hipError_t e;
+  if (bbn && is_pointwise(g)) {
+    e = bbn == 256 ? big::dense<256>(dy, g->K, false, x, g->C, false, pe, M, N, K, splits, st)
+                   : big::dense<128>(dy, g->K, false, x, g->C, false, pe, M, N, K, splits, st);
+  } else if (bbn) {
+    const big::DenseP pa2{dy, g->K, M};
+    const big::ConvP pb2 = conv_params(x, g->H, g->W, g->C, g->P, g->Q, g, N);
+    e = bbn == 256 ? big::launch<256, big::OpDenseMN<128>, big::OpWgradMN<128>>(pa2, pb2, pe, M, N, K, splits, st)
+                   : big::launch<128, big::OpDenseMN<128>, big::OpWgradMN<64>>(pa2, pb2, pe, M, N, K, splits, st);
+  } else if (is_pointwise(g)) {
+    DenseParams pb{x, g->C, N, K};
+    e = dispatch<MNDense, MNDense>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  } else {
+    GatherParams pb{x, g->H, g->W, g->C, g->P, g->Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, N, K};
+    e = dispatch<MNDense, MNConvGather>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  }
+  if (e != hipSuccess || splits == 1) return e;
+  return splitk_reduce(ws, splits, static_cast<long long>(M) * N, dw, beta, st);
+}

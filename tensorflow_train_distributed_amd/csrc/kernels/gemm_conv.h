@@ -1,0 +1,1397 @@
+#pragma once
+// MFMA (bf16, gfx950) GEMM engine + implicit-GEMM convolution (fwd / dgrad / wgrad): the
+// kernel templates and host-side dispatch helpers shared by gemm_conv.hip (dense GEMM),
+// conv_fwd.hip (forward conv, fp8), conv_dgrad.hip and conv_wgrad.hip — one translation
+// unit per entry group so hipcc builds them in parallel.
+//
+// This is the MatMul/Conv2D hot path of the framework: the dense layers of the reference's
+// MLP (tf.layers.dense, /root/reference/distribute_training.py:54,61 — fwd MatMul F1/F5 and
+// the backward MatMuls G3/G4 of SURVEY.md §2.6) and every conv / FC / projection of the
+// BASELINE.json north-star models (ResNet-50, BERT-Large).
+//
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §3, §5):
+//  * One templated kernel: BMxBN output tile (64/128 each), BK = 64, 256 threads = 4 waves in
+//    a 2x2 arrangement, each wave owning (BM/2)x(BN/2) as 16x16 tiles of
+//    v_mfma_f32_16x16x32_bf16 (fp32 accumulate).
+//  * Operands are staged global -> registers -> LDS (double buffered, one barrier per K-step,
+//    loads for step k+1 issued before the MFMAs of step k, LDS write after them: T14).
+//    Register staging lets the A loader be an implicit-GEMM *gather* with zero padding.
+//  * Each operand is either K-major (reduction dim contiguous: 16-B ds_read_b128 fragments,
+//    XOR-swizzled rows) or MN-major (rows contiguous: stored [k][rows] and read with the
+//    gfx950 transposing ds_read_b64_tr_b16, 32-B-slot XOR swizzle), so NN/NT/TN/TT GEMMs and
+//    the conv weight-gradient (both operands pixel-strided) share one engine, conflict-free.
+//  * The MFMA is issued with operands swapped (D = B·Aᵀ) so each lane ends up holding 4
+//    consecutive output columns of one row: 8-/16-byte vector stores in the epilogue.
+//  * XCD-aware bijective block remap (T1) so blocks sharing an A panel share an L2.
+//  * Split-K (grid.y) writes fp32 slabs that a reduce kernel sums (no float atomics).
+//  * Optional fused epilogue: bias, ReLU/GELU, residual add, accumulate-into-output,
+//    strided output-row remap (stride-2 1x1 dgrad), per-tile BatchNorm partial sums.
+#include "common.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+namespace ttdk {
+namespace {
+
+constexpr int BK = 64;
+constexpr int NTHR = 256;
+
+// ------------------------------------------------------------------ LDS layouts
+// K-major tile: ROWS x 64 bf16 (128 B per row, 8 chunks of 16 B), chunk ^= (row>>1)&7.
+__device__ __forceinline__ int kmaj_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// MN-major tile: 64 k-rows x ROWS bf16; 32-B slots XOR-swizzled so that the 8 k-rows a
+// half-wave touches in one ds_read_b64_tr_b16 land on distinct banks.
+template <int ROWS>
+__device__ __forceinline__ int mn_swz(int k) {
+  if constexpr (ROWS == 128)
+    return (k & 3) | ((k >> 1) & 4);
+  else
+    return ((k >> 1) & 1) | ((k >> 2) & 2);
+}
+template <int ROWS>
+__device__ __forceinline__ int mnmaj_off(int k, int col) {
+  return k * (ROWS * 2) + (((col >> 4) ^ mn_swz<ROWS>(k)) << 5) + ((col & 15) << 1);
+}
+
+__device__ __forceinline__ bf16x8_t lds_read_b128(const char* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+__device__ __forceinline__ s16x4_t lds_read_tr(const char* p) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p));
+}
+
+__device__ __forceinline__ uint4 ldg16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// ------------------------------------------------------------------ operand loaders
+// Every loader: Params; init(params, row0, tid); load(k0) -> regs; store(lds); frag(...).
+
+struct DenseParams {  // K-major: element (row, k) at p[row*ld + k]; MN-major: (k, row) at p[k*ld + row]
+  const bf16_t* p;
+  long long ld;
+  int rows;
+  int K;
+};
+
+struct GatherParams {  // conv operand geometry (see KConvGather / MNConvGather)
+  const bf16_t* x;
+  int Hs, Ws, Cs;
+  int P, Q;
+  int R, S;
+  int sh, sw, ph, pw, dh, dw;
+  int rows;
+  int K;
+};
+
+template <int ROWS, bool VEC = true>
+struct KDense {  // element (row, k) at p[row * ld + k]; VEC: K % 8 == 0, ld % 8 == 0, 16-B aligned base
+  using Params = DenseParams;
+  static constexpr int N = ROWS / 32;
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* ptr[N];
+  bool ok[N];
+  int c, K;
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    c = tid & 7;
+    K = P.K;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int row = row0 + (tid >> 3) + 32 * i;
+      ok[i] = row < P.rows;
+      ptr[i] = P.p + static_cast<long long>(ok[i] ? row : 0) * P.ld + c * 8;
+    }
+  }
+  __device__ __forceinline__ void load(int k0) {
+    if constexpr (VEC) {
+      const bool kin = k0 + c * 8 < K;
+#pragma unroll
+      for (int i = 0; i < N; ++i) r[i] = (ok[i] && kin) ? ldg16(ptr[i] + k0) : make_uint4(0, 0, 0, 0);
+    } else {
+      const int kb = k0 + c * 8;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t lo = (ok[i] && kb + 2 * e < K) ? ptr[i][k0 + 2 * e] : 0u;
+          const uint32_t hi = (ok[i] && kb + 2 * e + 1 < K) ? ptr[i][k0 + 2 * e + 1] : 0u;
+          w[e] = lo | (hi << 16);
+        }
+        r[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + kmaj_off((tid >> 3) + 32 * i, c)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int rowbase, int ks, int lane) {
+    return lds_read_b128(lds + kmaj_off(rowbase + (lane & 15), ks * 4 + (lane >> 4)));
+  }
+};
+
+// Implicit-GEMM gather of a conv input patch, K-major: row = output pixel (n, p, q),
+// k = (r, s, c). DGRAD=false: forward conv, source pixel = p*stride - pad + r*dil.
+// DGRAD=true: data gradient, source pixel of dY = (p + pad - r*dil) / stride when divisible.
+template <int ROWS, bool DGRAD>
+struct KConvGather {
+  // x: source activations NHWC [Nimg, Hs, Ws, Cs]; (P, Q): pixel grid of the GEMM rows;
+  // rows = Nimg*P*Q; K = R*S*Cs.
+  using Params = GatherParams;
+  static constexpr int N = ROWS / 32;
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* x;
+  int Hs, Ws, Cs, cch, S, sh, sw, dh, dw, K, c;
+  int img[N], hb[N], wb[N];
+  bool ok[N];
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    x = P.x;
+    Hs = P.Hs;
+    Ws = P.Ws;
+    Cs = P.Cs;
+    cch = P.Cs >> 3;
+    S = P.S;
+    sh = P.sh;
+    sw = P.sw;
+    dh = P.dh;
+    dw = P.dw;
+    K = P.K;
+    c = tid & 7;
+    const int pq = P.P * P.Q;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int m = row0 + (tid >> 3) + 32 * i;
+      ok[i] = m < P.rows;
+      const int mm = ok[i] ? m : 0;
+      const int n = mm / pq, rem = mm - n * pq;
+      const int p = rem / P.Q, q = rem - p * P.Q;
+      img[i] = n * P.Hs;
+      if (DGRAD) {
+        hb[i] = p + P.ph;
+        wb[i] = q + P.pw;
+      } else {
+        hb[i] = p * P.sh - P.ph;
+        wb[i] = q * P.sw - P.pw;
+      }
+    }
+  }
+  __device__ __forceinline__ void load(int k0) {
+    const int kc = (k0 >> 3) + c;
+    const bool kin = kc * 8 < K;
+    const int tap = kc / cch, c8 = kc - tap * cch;
+    const int rr = tap / S, ss = tap - rr * S;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      int h, w;
+      bool v = ok[i] && kin;
+      if (DGRAD) {
+        const int hn = hb[i] - rr * dh, wn = wb[i] - ss * dw;
+        h = hn / sh;
+        w = wn / sw;
+        v = v && hn >= 0 && wn >= 0 && h * sh == hn && w * sw == wn;
+      } else {
+        h = hb[i] + rr * dh;
+        w = wb[i] + ss * dw;
+        v = v && h >= 0 && w >= 0;
+      }
+      v = v && h < Hs && w < Ws;
+      r[i] = v ? ldg16(x + ((static_cast<long long>(img[i] + h) * Ws + w) * Cs + c8 * 8)) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + kmaj_off((tid >> 3) + 32 * i, c)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int rowbase, int ks, int lane) {
+    return KDense<ROWS>::frag(lds, rowbase, ks, lane);
+  }
+};
+
+template <int ROWS>
+__device__ __forceinline__ bf16x8_t mn_frag(const char* lds, int colbase, int ks, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int ka = ks * 32 + 8 * g + q;
+  const int col = colbase + 4 * p;
+  const s16x4_t lo = lds_read_tr(lds + mnmaj_off<ROWS>(ka, col));
+  const s16x4_t hi = lds_read_tr(lds + mnmaj_off<ROWS>(ka + 4, col));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int ROWS, bool VEC = true>
+struct MNDense {  // element (k, row) at p[k * ld + row]; VEC: rows % 8 == 0, ld % 8 == 0, aligned base
+  using Params = DenseParams;
+  static constexpr int CPR = ROWS / 8;           // 16-B chunks per k-row
+  static constexpr int KPP = NTHR / CPR;         // k-rows per pass
+  static constexpr int N = BK / KPP;             // passes
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* p;
+  long long ld;
+  int K, cc, kr, rows_left;
+  bool cok;
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    cc = tid % CPR;
+    kr = tid / CPR;
+    ld = P.ld;
+    K = P.K;
+    cok = row0 + cc * 8 < P.rows;
+    rows_left = P.rows - (row0 + cc * 8);
+    p = P.p + row0 + cc * 8;
+  }
+  __device__ __forceinline__ void load(int k0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int k = k0 + kr + KPP * i;
+      if constexpr (VEC) {
+        r[i] = (cok && k < K) ? ldg16(p + static_cast<long long>(k) * ld) : make_uint4(0, 0, 0, 0);
+      } else {
+        const bf16_t* q = p + static_cast<long long>(k) * ld;
+        const bool kok = cok && k < K;
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t lo = (kok && 2 * e < rows_left) ? q[2 * e] : 0u;
+          const uint32_t hi = (kok && 2 * e + 1 < rows_left) ? q[2 * e + 1] : 0u;
+          w[e] = lo | (hi << 16);
+        }
+        r[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + mnmaj_off<ROWS>(kr + KPP * i, cc * 8)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int colbase, int ks, int lane) {
+    return mn_frag<ROWS>(lds, colbase, ks, lane);
+  }
+};
+
+// Weight-gradient im2col operand, MN-major: k = output pixel (n, p, q), column = (r, s, c),
+// element = x[n, p*sh - ph + r*dh, q*sw - pw + s*dw, c].
+template <int ROWS>
+struct MNConvGather {
+  // x: conv input [Nimg, Hs, Ws, Cs]; (P, Q): output grid; rows = R*S*Cs; K = Nimg*P*Q.
+  using Params = GatherParams;
+  static constexpr int CPR = ROWS / 8;
+  static constexpr int KPP = NTHR / CPR;
+  static constexpr int N = BK / KPP;
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* x;
+  int H, W, C, P, Q, pq, sh, sw, K, kr, cc, roff, soff;
+  bool cok;
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& Pm, int row0, int tid) {
+    cc = tid % CPR;
+    kr = tid / CPR;
+    x = Pm.x;
+    H = Pm.Hs;
+    W = Pm.Ws;
+    C = Pm.Cs;
+    P = Pm.P;
+    Q = Pm.Q;
+    pq = Pm.P * Pm.Q;
+    sh = Pm.sh;
+    sw = Pm.sw;
+    K = Pm.K;
+    const int col = row0 + cc * 8;
+    cok = col < Pm.rows;
+    const int cl = cok ? col : 0;
+    const int tap = cl / C, c = cl - tap * C;
+    const int rr = tap / Pm.S, ss = tap - rr * Pm.S;
+    roff = rr * Pm.dh - Pm.ph;
+    soff = ss * Pm.dw - Pm.pw;
+    x += c;
+  }
+  __device__ __forceinline__ void load(int k0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int k = k0 + kr + KPP * i;
+      const int n = k / pq, rem = k - n * pq;
+      const int p = rem / Q, q = rem - p * Q;
+      const int h = p * sh + roff, w = q * sw + soff;
+      const bool v = cok && k < K && h >= 0 && w >= 0 && h < H && w < W;
+      r[i] = v ? ldg16(x + (static_cast<long long>(n * H + h) * W + w) * C) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + mnmaj_off<ROWS>(kr + KPP * i, cc * 8)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int colbase, int ks, int lane) {
+    return mn_frag<ROWS>(lds, colbase, ks, lane);
+  }
+};
+
+// ------------------------------------------------------------------ epilogues
+// kActDGelu: backward of the tanh-GELU: out = acc * gelu'(residual) (residual = the
+// pre-activation saved by the forward epilogue; not added).
+enum Act : int { kActNone = 0, kActRelu = 1, kActGelu = 2, kActTanh = 3, kActDGelu = 4 };
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float t = tanhf(k0 * (x + k1 * x * x * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+struct EpiParams {
+  int mode;  // 0 = bf16 store, 1 = fp32 slab store (split-K), 2 = fp32 store
+  void* out;
+  long long ldo;
+  long long slab_stride;  // elements between split-K slabs (mode 1)
+  const float* bias;      // [N] or null
+  const bf16_t* residual; // same layout as out, or null
+  long long ldr;
+  int act;
+  int beta;               // accumulate: out = acc + out
+  // strided output-row remap (dgrad of strided 1x1 convs): row m=(n,p,q) -> (n, p*rs, q*rs) of [OH,OW]
+  int remap;
+  int rP, rQ, rOH, rOW, rs;
+  float* stat;  // BN partial sums: [tiles_m][2][N] (sum, sumsq) or null
+  float alpha;  // scale applied to acc
+  bf16_t* aux;  // optional: pre-activation copy (GELU backward input), row stride ldo
+  const float* ascale0;  // optional device scalars multiplied into alpha (fp8 dequant scales)
+  const float* ascale1;
+  // BN-backward statistics of the produced gradient (dgrad feeding a conv+BN(+ReLU) unit):
+  // with `by` set the stored value is g = v * mask (ReLU bit per element, `bmask`, optional)
+  // and `stat` receives per-tile (sum g, sum g*y) with y = by (the unit's pre-BN conv output,
+  // same layout as out) — the separate bwd-partial pass over dy and y disappears.
+  const bf16_t* by;
+  const uint8_t* bmask;
+};
+
+__device__ __forceinline__ float epi_alpha(const EpiParams& E) {
+  float a = E.alpha;
+  if (E.ascale0) a *= *E.ascale0;
+  if (E.ascale1) a *= *E.ascale1;
+  return a;
+}
+
+__device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
+  if (!E.remap) return m;
+  const int pq = E.rP * E.rQ;
+  const int n = m / pq, rem = m - n * pq;
+  const int p = rem / E.rQ, q = rem - p * E.rQ;
+  return (static_cast<long long>(n) * E.rOH + p * E.rs) * E.rOW + q * E.rs;
+}
+
+// Row loop of the bf16 epilogues (both kernels): one thread owns 16-B column chunk `c` of
+// rows r0, r0+RPP, ... of the LDS-staged tile. Rows go in batches of EB with every
+// residual / accumulate (beta) load of the batch issued before any of them is used: with one
+// workgroup per CU (LDS-bound tiles) a load-use per row left the epilogue latency-bound,
+// which is what capped the K <= 128 ResNet 1x1 GEMMs at ~50% of HBM bandwidth.
+template <int BM, int RPP, int PITCH, bool PF>
+__device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, int c, int r0, int n, int m0, int M,
+                                         int N, bool vst, bool vres, const float (&bias8)[8], float (&s8)[8],
+                                         float (&q8)[8]) {
+  constexpr int NR = (BM + RPP - 1) / RPP;
+  constexpr int EB = !PF ? 1 : (NR < 8 ? NR : 8);
+  bf16_t* out = static_cast<bf16_t*>(E.out);
+  if (n >= N) return;
+#pragma unroll 1
+  for (int rb = r0; rb < BM; rb += RPP * EB) {
+    uint4 pres[EB], pold[EB], pby[EB];
+    uint32_t pmb[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int r = rb + u * RPP, m = m0 + r;
+      if (r < BM && m < M) {
+        if (E.residual && vres) pres[u] = *reinterpret_cast<const uint4*>(E.residual + static_cast<long long>(m) * E.ldr + n);
+        if (E.beta && vst) pold[u] = *reinterpret_cast<const uint4*>(out + out_row(E, m) * E.ldo + n);
+        if (E.by) {  // vst is guaranteed by the host (N % 8 == 0, ldo % 8 == 0)
+          const long long o = out_row(E, m) * E.ldo + n;
+          pby[u] = *reinterpret_cast<const uint4*>(E.by + o);
+          pmb[u] = E.bmask ? E.bmask[o >> 3] : 0xffu;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int r = rb + u * RPP, m = m0 + r;
+      if (r >= BM || m >= M) break;
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += bias8[j];
+      if (E.residual) {
+        const bf16_t* rp = E.residual + static_cast<long long>(m) * E.ldr + n;
+        float rv[8];
+        if (vres) {
+          unpack8(pres[u], rv);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rv[j] = n + j < N ? bf2f(rp[j]) : 0.f;
+        }
+        if (E.act == kActDGelu) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] *= gelu_tanh_grad(rv[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] += rv[j];
+        }
+      }
+      bf16_t* op = out + out_row(E, m) * E.ldo + n;
+      if (E.beta) {
+        float ov[8];
+        if (vst) {
+          unpack8(pold[u], ov);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ov[j] = n + j < N ? bf2f(op[j]) : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += ov[j];
+      }
+      if (E.aux) {
+        bf16_t* ap = E.aux + out_row(E, m) * E.ldo + n;
+        const uint4 pa = pack8(f);
+        if (vst) {
+          *reinterpret_cast<uint4*>(ap) = pa;
+        } else {
+          const uint32_t w[4] = {pa.x, pa.y, pa.z, pa.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (n + j < N) ap[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+        }
+      }
+      if (E.act == kActRelu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      } else if (E.act == kActGelu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
+      } else if (E.act == kActTanh) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = tanhf(f[j]);
+      }
+      if (E.by) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (pmb[u] >> j) & 1u ? f[j] : 0.f;
+      }
+      const uint4 packed = pack8(f);
+      if (vst) {
+        *reinterpret_cast<uint4*>(op) = packed;
+      } else {
+        const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n + j < N) op[j] = static_cast<bf16_t>((w[j >> 1] >> (16 * (j & 1))) & 0xffff);
+      }
+      if (E.by) {
+        float sv[8], yv[8];
+        unpack8(packed, sv);  // statistics of the gradient actually stored
+        unpack8(pby[u], yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s8[j] += sv[j];
+          q8[j] += sv[j] * yv[j];
+        }
+      } else if (E.stat) {
+        float sv[8];
+        unpack8(packed, sv);  // statistics of the values actually stored
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s8[j] += sv[j];
+          q8[j] += sv[j] * sv[j];
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM / 32][BN / 32], int m0, int n0,
+                                         int mwave, int nwave, int lane, int M, int N, int split, int tile_m,
+                                         char* smem) {
+  static_assert(BM * (BN * 2 + 16) + 4 * 2 * BN * 4 <= 2 * (BM + BN) * BK * 2, "staged epilogue must fit in LDS");
+  constexpr int TM = BM / 32, TN = BN / 32;
+  const int g = lane >> 4, i16 = lane & 15;
+  const float alpha_e = epi_alpha(E);
+  if (E.mode != 0) {
+    float* out = static_cast<float*>(E.out) + (E.mode == 1 ? split * E.slab_stride : 0);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int m = mwave + tm * 16 + i16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int n = nwave + tn * 16 + 4 * g;
+        f32x4_t v = acc[tm][tn] * alpha_e;
+        float* o = out + static_cast<long long>(m) * E.ldo + n;
+        if (n + 3 < N && (E.ldo & 3) == 0) {
+          if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
+          *reinterpret_cast<f32x4_t*>(o) = v;
+        } else {
+          #pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (n + j < N) o[j] = v[j] + (E.beta ? o[j] : 0.f);
+        }
+      }
+    }
+    return;
+  }
+  // ---- bf16 output: stage the tile through LDS (the K loop ended on a barrier, so the
+  // operand buffers are free), then every thread stores whole 16-B chunks of full rows:
+  // one wave-instruction writes 4 x 256 contiguous bytes instead of 16 x 32-B segments.
+  constexpr int PITCH = BN * 2 + 16;  // 16-B aligned rows; +16 B breaks the bank period
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int r = mwave - m0 + tm * 16 + i16, c = nwave - n0 + tn * 16 + 4 * g;
+      const f32x4_t v = acc[tm][tn] * alpha_e;
+      uint2 w;
+      w.x = pack_bf16x2(v[0], v[1]);
+      w.y = pack_bf16x2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) = w;
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;       // 16-B chunks per row
+  constexpr int RPP = NTHR / CPR;   // rows per pass
+  const int c = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + c * 8;
+  const bool nfull = n + 8 <= N;
+  const bool vst = nfull && (E.ldo & 7) == 0;
+  const bool vres = nfull && (E.ldr & 7) == 0;
+  float bias8[8], s8[8], q8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
+    s8[j] = q8[j] = 0.f;
+  }
+  if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
+    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+  else
+    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+  if (E.stat) {
+    // lanes sharing a chunk column: lane % CPR equal -> reduce over the wave, then over 4 waves.
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        s8[j] += __shfl_xor(s8[j], o, 64);
+        q8[j] += __shfl_xor(q8[j], o, 64);
+      }
+    }
+    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [4 waves][2][BN]
+    const int w = tid >> 6;
+    if ((tid & 63) < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(w * 2 + 0) * BN + c * 8 + j] = s8[j];
+        red[(w * 2 + 1) * BN + c * 8 + j] = q8[j];
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < BN; t += NTHR) {
+      if (n0 + t < N) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          ss += red[(k * 2 + 0) * BN + t];
+          qq += red[(k * 2 + 1) * BN + t];
+        }
+        E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t] = ss;
+        E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t] = qq;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int xcd = bid & 7, idx = bid >> 3;
+  const int q = nblocks >> 3, r = nblocks & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int BM, int BN, class LA, class LB>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, typename LB::Params pb, EpiParams pe,
+                                                      int M, int N, int K, int tiles_m, int tiles_n, int kt_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (LA::BYTES + LB::BYTES)];
+  const int nblk = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  const int tile_n = t % tiles_n, tile_m = t / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  constexpr int TM = BM / 32, TN = BN / 32;
+
+  char* const sA0 = smem;
+  char* const sB0 = smem + 2 * LA::BYTES;
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ktiles = (K + BK - 1) / BK;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt1 = min(kt0 + kt_per_split, ktiles);
+
+  LA la;
+  LB lb;
+  la.init(pa, m0, tid);
+  lb.init(pb, n0, tid);
+  if (kt0 < kt1) {
+    la.load(kt0 * BK);
+    lb.load(kt0 * BK);
+    la.store(sA0, tid);
+    lb.store(sB0, tid);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const bool nxt = kt + 1 < kt1;
+    if (nxt) {
+      la.load((kt + 1) * BK);
+      lb.load((kt + 1) * BK);
+    }
+    const char* sa = sA0 + cur * LA::BYTES;
+    const char* sb = sB0 + cur * LB::BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a] = LA::frag(sa, wm * (BM / 2) + a * 16, ks, lane);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bfr[b] = LB::frag(sb, wn * (BN / 2) + b * 16, ks, lane);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+    }
+    if (nxt) {
+      la.store(sA0 + (cur ^ 1) * LA::BYTES, tid);
+      lb.store(sB0 + (cur ^ 1) * LB::BYTES, tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  epilogue<BM, BN>(pe, acc, m0, n0, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane, M, N, blockIdx.y, tile_m, smem);
+}
+
+// Sums split-K fp32 slabs: out[i] (+)= sum_s ws[s*n + i]. grid.y groups slabs by 8 so even a
+// small output (a few K elements) gets enough threads in flight; with >1 group the partial
+// sums land with float atomics into a pre-zeroed (or beta-preloaded) output.
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long n, float* __restrict__ out,
+                                     int beta, int per_group, int atomic) {
+  const long long i4 = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
+  if (i4 + 3 < n) {
+    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = s0; k < s1; ++k) s += *reinterpret_cast<const f32x4_t*>(ws + k * n + i4);
+    if (atomic) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(out + i4 + j, s[j]);
+    } else {
+      if (beta) s += *reinterpret_cast<const f32x4_t*>(out + i4);
+      *reinterpret_cast<f32x4_t*>(out + i4) = s;
+    }
+  } else {
+    for (long long i = i4; i < n; ++i) {
+      float t = 0.f;
+      for (int k = s0; k < s1; ++k) t += ws[k * n + i];
+      if (atomic)
+        atomicAdd(out + i, t);
+      else
+        out[i] = t + (beta ? out[i] : 0.f);
+    }
+  }
+}
+
+hipError_t splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {
+  const int per_group = 8;
+  const int groups = (splits + per_group - 1) / per_group;
+  const int atomic = groups > 1;
+  if (atomic && !beta) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * n, st);
+    if (e != hipSuccess) return e;
+  }
+  dim3 grid(ceil_div((n + 3) / 4, 256), groups);
+  hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, ws, splits, n, out, beta, per_group, atomic);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ 256-row LDS-DMA GEMM
+// Large-GEMM / large-conv path: 256 x BN x (128 B of K) tile, BN in {256, 128}, 8 waves,
+// ~1 workgroup per CU. Operand tiles stream global -> LDS with global_load_lds_dwordx4 (no
+// VGPR staging, no ds_write pass); the XOR swizzle is applied on the per-lane SOURCE address
+// so the LDS image stays lane-linear. Operand policies (A: rows = M, B: rows = N):
+//   OpDenseK   element (row, k) at p[row*ld + k]        (bf16, or fp8 e4m3/e5m2)
+//   OpDenseMN  element (k, row) at p[k*ld + row]        (bf16)
+//   OpConvK    implicit-GEMM conv row gather (fwd: x patch, dgrad: dy patch; C % (64|128))
+//   OpWgradMN  implicit-GEMM im2col columns for the weight gradient (bf16)
+// Padding / out-of-range rows read a zero page (DMA cannot zero-fill), so convolutions need
+// no masking in the MFMA loop.
+//
+// Each operand tile is split in two halves (A0/A1: 128 rows each, B0/B1: BN/2 rows). Wave
+// (wm, wn) owns rows {h*128 + wm*64 + [0,64)} and cols {h'*BN/2 + wn*BN/8 + [0,BN/8)}:
+// four quadrants, one per phase, ordered (A0,B0) (A0,B1) (A1,B1) (A1,B0) so every fragment
+// is read from LDS once per K-tile (B1 behind q0's MFMAs, A1 behind q1's, the next tile's
+// A0/B0 behind q3's) and each phase reloads one half no wave reads any more:
+//   q0 -> (T+1).A1, q1 -> (T+1).B0, q2 -> (T+2).A0, q3 -> (T+2).B1.
+// Barriers only at q2 (WAR for A0) and q3 (after a counted s_waitcnt vmcnt that retires
+// tile T+1 but leaves (T+2).A0 in flight; publishes T+1's DMA to every wave). All LDS lives
+// in one __shared__ array; s_setprio(1) brackets each MFMA cluster.
+// fp8: K-tile = 128 elements, v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales
+// (2x the bf16 MFMA rate); A and B fragments take the same 32 contiguous k per lane group,
+// so the product is independent of the instruction's internal k order.
+namespace big {
+constexpr int BM = 256, THR = 512;
+
+// zero page for padded / out-of-range DMA sources (static device memory is zero-filled)
+__device__ __attribute__((aligned(16))) unsigned char g_zero[256];
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
+
+template <int HROWS>
+__device__ __forceinline__ int swz_mn(int k) {
+  if constexpr (HROWS == 128)
+    return (k & 3) | ((k >> 1) & 4);
+  else
+    return ((k >> 1) & 1) | ((k >> 2) & 2);
+}
+
+__device__ __forceinline__ void glds(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(lds), 16, 0, 0);
+}
+
+struct DenseP {
+  const void* p;
+  long long ld;   // elements
+  int rows;
+};
+
+struct ConvP {  // implicit-GEMM geometry: source tensor [Nimg, Hs, Ws, Cs]; GEMM rows on the (P, Q) grid
+  const void* x;
+  int Hs, Ws, Cs;
+  int P, Q;
+  int R, S;
+  int sh, sw, ph, pw, dh, dw;
+  int rows;
+};
+
+// ---- dense K-major: half = HROWS rows x 128 B
+template <int HROWS, int ESZ>
+struct OpDenseK {
+  using Params = DenseP;
+  static constexpr int G = HROWS / 64;  // glds per wave per half
+  const char* src[2][G];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int q = i * THR + tid;
+        const int row = q >> 3, slot = q & 7;
+        const int chunk = slot ^ ((row >> 1) & 7);
+        const int r = min(row0 + h * HROWS + row, P.rows - 1);
+        src[h][i] = static_cast<const char*>(P.p) + (static_cast<long long>(r) * P.ld) * ESZ + chunk * 16;
+      }
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < G; ++i) glds(src[H][i] + static_cast<long long>(kt) * 128, lds + (i * THR + wave * 64) * 16);
+  }
+};
+
+// ---- dense MN-major (bf16): half = HROWS cols x 64 k
+template <int HROWS>
+struct OpDenseMN {
+  using Params = DenseP;
+  static constexpr int G = HROWS / 64;
+  static constexpr int CPR = HROWS / 8;  // 16-B chunks per k-row
+  const char* src[2][G];
+  long long kstep;
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int q = i * THR + tid;
+        const int k = q / CPR, j = q % CPR;
+        const int col = ((((j >> 1) ^ swz_mn<HROWS>(k))) << 4) + (j & 1) * 8;
+        const int c = min(row0 + h * HROWS + col, P.rows - 8);
+        src[h][i] = static_cast<const char*>(P.p) + (static_cast<long long>(k) * P.ld + c) * 2;
+      }
+    kstep = 64 * P.ld * 2;
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < G; ++i) glds(src[H][i] + kt * kstep, lds + (i * THR + wave * 64) * 16);
+  }
+};
+
+// ---- implicit-GEMM conv rows (K-major): row = output pixel of the (P, Q) grid, k = (r, s, c);
+// one K-tile (128 B) lies inside one tap (requires Cs*ESZ % 128 == 0).
+template <int HROWS, int ESZ, bool DGRAD, bool UNIT_STRIDE = false>
+struct OpConvK {
+  using Params = ConvP;
+  static constexpr int G = HROWS / 64;
+  static constexpr int KT = 128 / ESZ;  // elements per K-tile
+  const char* x;
+  int Hs, Ws, Cs, S, sh, sw, dh, dw, tid;
+  int img[2][G], hb[2][G], wb[2][G];  // img < 0: row beyond M (reads the zero page)
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid_) {
+    x = static_cast<const char*>(P.x);
+    Hs = P.Hs; Ws = P.Ws; Cs = P.Cs; S = P.S; sh = P.sh; sw = P.sw; dh = P.dh; dw = P.dw;
+    tid = tid_;
+    const int pq = P.P * P.Q;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int row = (i * THR + tid) >> 3;
+        const int m = row0 + h * HROWS + row;
+        const bool ok = m < P.rows;
+        const int mm = ok ? m : 0;
+        const int n = mm / pq, rem = mm - n * pq;
+        const int p = rem / P.Q, qq = rem - p * P.Q;
+        img[h][i] = ok ? n * P.Hs : -1;
+        if (DGRAD) {
+          hb[h][i] = p + P.ph;
+          wb[h][i] = qq + P.pw;
+        } else {
+          hb[h][i] = p * P.sh - P.ph;
+          wb[h][i] = qq * P.sw - P.pw;
+        }
+      }
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+    const int k0 = kt * KT;
+    const int tap = k0 / Cs, c0 = k0 - tap * Cs;
+    const int rr = tap / S, ss = tap - rr * S;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int row = (i * THR + tid) >> 3;
+      const int coff = (((tid & 7) ^ ((row >> 1) & 7))) * 16;
+      int hh, ww;
+      bool v = img[H][i] >= 0;
+      if (DGRAD && UNIT_STRIDE) {
+        hh = hb[H][i] - rr * dh;
+        ww = wb[H][i] - ss * dw;
+        v = v && hh >= 0 && ww >= 0;
+      } else if (DGRAD) {
+        const int hn = hb[H][i] - rr * dh, wn = wb[H][i] - ss * dw;
+        hh = hn / sh;
+        ww = wn / sw;
+        v = v && hn >= 0 && wn >= 0 && hh * sh == hn && ww * sw == wn;
+      } else {
+        hh = hb[H][i] + rr * dh;
+        ww = wb[H][i] + ss * dw;
+        v = v && hh >= 0 && ww >= 0;
+      }
+      v = v && hh < Hs && ww < Ws;
+      const char* s = v ? x + ((static_cast<long long>(img[H][i] + hh) * Ws + ww) * Cs + c0) * ESZ + coff
+                        : reinterpret_cast<const char*>(g_zero) + coff;
+      glds(s, lds + (i * THR + wave * 64) * 16);
+    }
+  }
+};
+
+// ---- weight-gradient im2col columns (MN-major, bf16): k = output pixel, column = (r, s, c)
+template <int HROWS>
+struct OpWgradMN {
+  using Params = ConvP;
+  static constexpr int G = HROWS / 64;
+  static constexpr int CPR = HROWS / 8;
+  const char* x;
+  int H, W, C, pq, Q, sh, sw;
+  int krow[2][G], roff[2][G], soff[2][G], cc[2][G];
+  bool cok[2][G];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    x = static_cast<const char*>(P.x);
+    H = P.Hs; W = P.Ws; C = P.Cs; pq = P.P * P.Q; Q = P.Q; sh = P.sh; sw = P.sw;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int q = i * THR + tid;
+        const int k = q / CPR, j = q % CPR;
+        const int col = row0 + h * HROWS + ((((j >> 1) ^ swz_mn<HROWS>(k))) << 4) + (j & 1) * 8;
+        krow[h][i] = k;
+        cok[h][i] = col < P.rows;
+        const int cl = cok[h][i] ? col : 0;
+        const int tap = cl / C, c = cl - tap * C;
+        const int rr = tap / P.S, ss = tap - rr * P.S;
+        roff[h][i] = rr * P.dh - P.ph;
+        soff[h][i] = ss * P.dw - P.pw;
+        cc[h][i] = c;
+      }
+  }
+  template <int HH>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int k = kt * 64 + krow[HH][i];
+      const int n = k / pq, rem = k - n * pq;
+      const int p = rem / Q, qq = rem - p * Q;
+      const int hh = p * sh + roff[HH][i], ww = qq * sw + soff[HH][i];
+      const bool v = cok[HH][i] && hh >= 0 && ww >= 0 && hh < H && ww < W;
+      const char* s = v ? x + ((static_cast<long long>(n * H + hh) * W + ww) * C + cc[HH][i]) * 2
+                        : reinterpret_cast<const char*>(g_zero);
+      glds(s, lds + (i * THR + wave * 64) * 16);
+    }
+  }
+};
+
+template <class OP>
+struct Traits {
+  static constexpr bool kmaj = true;
+};
+template <int HR>
+struct Traits<OpDenseMN<HR>> {
+  static constexpr bool kmaj = false;
+};
+template <int HR>
+struct Traits<OpWgradMN<HR>> {
+  static constexpr bool kmaj = false;
+};
+
+// fragment readers
+__device__ __forceinline__ bf16x8_t frag_k(const char* lds, int base, int ks, int lane) {
+  return lds_read_b128(lds + kmaj_off(base + (lane & 15), ks * 4 + (lane >> 4)));
+}
+__device__ __forceinline__ i32x8_t frag_k8(const char* lds, int base, int lane) {
+  const int row = base + (lane & 15), g = lane >> 4;
+  const uint4 lo = *reinterpret_cast<const uint4*>(lds + kmaj_off(row, 2 * g));
+  const uint4 hi = *reinterpret_cast<const uint4*>(lds + kmaj_off(row, 2 * g + 1));
+  i32x8_t v = {static_cast<int>(lo.x), static_cast<int>(lo.y), static_cast<int>(lo.z), static_cast<int>(lo.w),
+               static_cast<int>(hi.x), static_cast<int>(hi.y), static_cast<int>(hi.z), static_cast<int>(hi.w)};
+  return v;
+}
+template <int HROWS>
+__device__ __forceinline__ bf16x8_t frag_mn(const char* lds, int colbase, int ks, int lane) {
+  return mn_frag<HROWS>(lds, colbase, ks, lane);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BN>
+struct Geo {
+  static constexpr int BNH = BN / 2;          // B half rows
+  static constexpr int AH = 128 * 128;        // A half bytes
+  static constexpr int BH = BNH * 128;        // B half bytes
+  static constexpr int STAGE = 2 * AH + 2 * BH;
+  static constexpr int NB = BNH / 64;         // 16-col blocks per wave per B half
+  static constexpr int PITCH = BN * 2 + 16;
+  static constexpr int EPI = BM * PITCH + 8 * 2 * BN * 4;
+  static constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+};
+
+// F8: 0 = bf16, 1 = fp8 e4m3 x e4m3, 2 = e5m2 (A) x e4m3 (B)  (dgrad: gradients in e5m2)
+template <int BN, class OA, class OB, int F8>
+__global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa, typename OB::Params pb, EpiParams E,
+                                                         int M, int N, int K, int tiles_m, int tiles_n,
+                                                         int kt_per_split) {
+  using Gm = Geo<BN>;
+  constexpr int BNH = Gm::BNH, NB = Gm::NB, GA = 2, GB = BNH / 64;
+  constexpr bool AK = Traits<OA>::kmaj, BKM = Traits<OB>::kmaj;
+  static_assert(F8 == 0 || (AK && BKM), "fp8 operands must be K-major");
+  __shared__ __attribute__((aligned(16))) char smem[Gm::SMEM];
+  const int nblk = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  const int tile_n = t % tiles_n, tile_m = t / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  OA la;
+  OB lb;
+  la.init(pa, m0, tid);
+  lb.init(pb, n0, tid);
+
+  // acc[ha][hb][a][b]: rows ha*128 + wm*64 + a*16, cols hb*BNH + wn*(BNH/4) + b*16
+  f32x4_t acc[2][2][4][NB];
+#pragma unroll
+  for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[ha][hb][a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int ktiles = K / (F8 ? 128 : 64);
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt1 = min(kt0 + kt_per_split, ktiles);
+  auto buf = [&](int kt) { return smem + ((kt - kt0) & 1) * Gm::STAGE; };
+  constexpr int A0 = 0, A1 = Gm::AH, B0 = 2 * Gm::AH, B1 = 2 * Gm::AH + Gm::BH;
+
+  // fragments: [slot][ks][block]; fp8 uses one "ks" of K = 128
+  constexpr int KS = F8 ? 1 : 2;
+  typedef typename std::conditional<F8 != 0, i32x8_t, bf16x8_t>::type frag_t;
+  frag_t fa[2][KS][4], fb[2][KS][NB];
+  auto read_a = [&](const char* sA, frag_t (&f)[KS][4]) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        if constexpr (F8 != 0) f[ks][a] = frag_k8(sA, wm * 64 + a * 16, lane);
+        else if constexpr (AK) f[ks][a] = frag_k(sA, wm * 64 + a * 16, ks, lane);
+        else f[ks][a] = frag_mn<128>(sA, wm * 64 + a * 16, ks, lane);
+      }
+  };
+  auto read_b = [&](const char* sB, frag_t (&f)[KS][NB]) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        if constexpr (F8 != 0) f[ks][b] = frag_k8(sB, wn * (BNH / 4) + b * 16, lane);
+        else if constexpr (BKM) f[ks][b] = frag_k(sB, wn * (BNH / 4) + b * 16, ks, lane);
+        else f[ks][b] = frag_mn<BNH>(sB, wn * (BNH / 4) + b * 16, ks, lane);
+      }
+  };
+  auto mma = [&](const frag_t (&x)[KS][4], const frag_t (&y)[KS][NB], f32x4_t (&c)[4][NB]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          if constexpr (F8 == 1)
+            c[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(y[ks][b], x[ks][a], c[a][b], 0, 0, 0, 127, 0, 127);
+          else if constexpr (F8 == 2)  // A (x operand, second arg) in e5m2: blgp = 1
+            c[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(y[ks][b], x[ks][a], c[a][b], 0, 1, 0, 127, 0, 127);
+          else
+            c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y[ks][b], x[ks][a], c[a][b], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // issue order per tile: A0, B1, A1, B0 (B0 last) => one counted wait retires a whole tile
+  if (kt0 < kt1) {
+    char* b0 = buf(kt0);
+    la.template issue<0>(b0 + A0, kt0, wave);
+    lb.template issue<1>(b0 + B1, kt0, wave);
+    la.template issue<1>(b0 + A1, kt0, wave);
+    lb.template issue<0>(b0 + B0, kt0, wave);
+    if (kt0 + 1 < kt1) {
+      char* b1 = buf(kt0 + 1);
+      la.template issue<0>(b1 + A0, kt0 + 1, wave);
+      lb.template issue<1>(b1 + B1, kt0 + 1, wave);
+      wait_vm<GA + GB>();
+    } else {
+      wait_vm<0>();
+    }
+    barrier();
+    read_a(b0 + A0, fa[0]);
+    read_b(b0 + B0, fb[0]);
+  }
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const bool has1 = kt + 1 < kt1, has2 = kt + 2 < kt1;
+    char* cb = buf(kt);
+    // q0: (A0, B0)
+    if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
+    mma(fa[0], fb[0], acc[0][0]);
+    read_b(cb + B1, fb[1]);
+    // q1: (A0, B1)
+    if (has1) lb.template issue<0>(buf(kt + 1) + B0, kt + 1, wave);
+    mma(fa[0], fb[1], acc[0][1]);
+    read_a(cb + A1, fa[1]);
+    // q2: (A1, B1)
+    barrier();
+    if (has2) la.template issue<0>(cb + A0, kt + 2, wave);
+    mma(fa[1], fb[1], acc[1][1]);
+    // q3: (A1, B0); retire tile kt+1 ((kt+2).A0 may stay in flight), prefetch its A0/B0
+    if (has1) {
+      if (has2) wait_vm<GA>(); else wait_vm<0>();
+    }
+    barrier();
+    if (has2) lb.template issue<1>(cb + B1, kt + 2, wave);
+    mma(fa[1], fb[0], acc[1][0]);
+    if (has1) {
+      char* nb = buf(kt + 1);
+      read_a(nb + A0, fa[0]);
+      read_b(nb + B0, fb[0]);
+    }
+  }
+  wait_vm<0>();
+  __syncthreads();
+
+  // ---------------------------------------------------------------- epilogue
+  const int g = lane >> 4, i16 = lane & 15;
+  const float alpha_e = epi_alpha(E);
+  if (E.mode != 0) {
+    float* out = static_cast<float*>(E.out) + (E.mode == 1 ? blockIdx.y * E.slab_stride : 0);
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int m = m0 + ha * 128 + wm * 64 + a * 16 + i16;
+        if (m >= M) continue;
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const int n = n0 + hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
+            f32x4_t v = acc[ha][hb][a][b] * alpha_e;
+            float* o = out + out_row(E, m) * E.ldo + n;
+            if (n + 3 < N && (E.ldo & 3) == 0) {
+              if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
+              *reinterpret_cast<f32x4_t*>(o) = v;
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (n + j < N) o[j] = v[j] + (E.beta ? o[j] : 0.f);
+            }
+          }
+      }
+    return;
+  }
+  constexpr int PITCH = Gm::PITCH;
+#pragma unroll
+  for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
+          const f32x4_t v = acc[ha][hb][a][b] * alpha_e;
+          *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+  __syncthreads();
+  constexpr int CPR = BN / 8;     // 16-B chunks per row
+  constexpr int RPP = THR / CPR;  // rows per pass
+  const int c = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + c * 8;
+  const bool nfull = n + 8 <= N;
+  const bool vst = nfull && (E.ldo & 7) == 0;
+  const bool vres = nfull && (E.ldr & 7) == 0;
+  float bias8[8], s8[8], q8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
+    s8[j] = q8[j] = 0.f;
+  }
+  if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
+    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+  else
+    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+  if (E.stat) {
+    // threads sharing a chunk column c: tid % CPR equal -> within a wave lanes c, c+CPR, ...
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        s8[j] += __shfl_xor(s8[j], o, 64);
+        q8[j] += __shfl_xor(q8[j], o, 64);
+      }
+    }
+    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [8 waves][2][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wave * 2 + 0) * BN + c * 8 + j] = s8[j];
+        red[(wave * 2 + 1) * BN + c * 8 + j] = q8[j];
+      }
+    }
+    __syncthreads();
+    for (int t2 = tid; t2 < BN; t2 += THR) {
+      if (n0 + t2 < N) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ss += red[(k * 2 + 0) * BN + t2];
+          qq += red[(k * 2 + 1) * BN + t2];
+        }
+        E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t2] = ss;
+        E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t2] = qq;
+      }
+    }
+  }
+}
+
+template <int BN, class OA, class OB, int F8 = 0>
+hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, const EpiParams& pe, int M, int N,
+                  int K, int splits, hipStream_t st) {
+  const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+  const int ktiles = K / (F8 ? 128 : 64);
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  hipLaunchKernelGGL((gemm256_kernel<BN, OA, OB, F8>), dim3(tm * tn, splits), dim3(THR), 0, st, pa, pb, pe, M, N, K,
+                     tm, tn, per);
+  return hipGetLastError();
+}
+
+// dense GEMM entry: A (M rows) and B (N rows), each K-major or MN-major, bf16
+template <int BN>
+hipError_t dense(const bf16_t* A, long long lda, bool ak, const bf16_t* B, long long ldb, bool bk,
+                 const EpiParams& pe, int M, int N, int K, int splits, hipStream_t st) {
+  DenseP pa{A, lda, M}, pb{B, ldb, N};
+  constexpr int BH = BN / 2;
+  if (ak && bk) return launch<BN, OpDenseK<128, 2>, OpDenseK<BH, 2>>(pa, pb, pe, M, N, K, splits, st);
+  if (ak) return launch<BN, OpDenseK<128, 2>, OpDenseMN<BH>>(pa, pb, pe, M, N, K, splits, st);
+  if (bk) return launch<BN, OpDenseMN<128>, OpDenseK<BH, 2>>(pa, pb, pe, M, N, K, splits, st);
+  return launch<BN, OpDenseMN<128>, OpDenseMN<BH>>(pa, pb, pe, M, N, K, splits, st);
+}
+
+}  // namespace big
+
+// ------------------------------------------------------------------ host-side dispatch
+template <int BM, int BN, class LA, class LB>
+hipError_t launch(const typename LA::Params& pa, const typename LB::Params& pb, const EpiParams& pe, int M, int N,
+                  int K, int splits, hipStream_t st) {
+  const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+  const int ktiles = ceil_div(K, BK);
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  dim3 grid(tm * tn, splits);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB>), grid, dim3(NTHR), 0, st, pa, pb, pe, M, N, K, tm, tn, per);
+  return hipGetLastError();
+}
+
+// Tile choice: prefer 128x128; shrink a dimension when it is small.
+// Tile width of the 256-row LDS-DMA kernel for an M x N x K GEMM, or 0 when the 4-wave
+// kernel is the better fit (small tiles / small GEMMs). Mirrored by ops/gemm.py big_bn().
+inline int big_bn(int M, int N, int K) {
+  if (M < 256 || N < 128 || K % 64 || N % 8 || static_cast<long long>(M) * N < (1LL << 20)) return 0;
+  return N >= 256 ? 256 : 128;
+}
+inline bool big_fits(int M, int N, int K) { return big_bn(M, N, K) != 0; }
+// Weight gradients have a long K (pixels) and split-K fills the machine, so only the tile
+// shape (not M*N) decides.
+inline int big_bn_wgrad(int M, int N, int K) {
+  if (M < 256 || N < 128 || K % 64 || N % 8) return 0;
+  return N >= 256 ? 256 : 128;
+}
+
+inline void pick_tile(int M, int N, int* bm, int* bn) {
+  *bm = (M <= 64) ? 64 : 128;
+  *bn = (N <= 64) ? 64 : 128;
+}
+
+template <template <int> class LA_T, template <int> class LB_T>
+hipError_t dispatch(const void* pa_raw, const void* pb_raw, const EpiParams& pe, int M, int N, int K, int splits,
+                    int bm, int bn, hipStream_t st) {
+#define TTDK_CASE(BM_, BN_)                                                                                        \
+  if (bm == BM_ && bn == BN_)                                                                                      \
+    return launch<BM_, BN_, LA_T<BM_>, LB_T<BN_>>(*static_cast<const typename LA_T<BM_>::Params*>(pa_raw),         \
+                                                  *static_cast<const typename LB_T<BN_>::Params*>(pb_raw), pe, M, N, \
+                                                  K, splits, st);
+  TTDK_CASE(128, 128)
+  TTDK_CASE(128, 64)
+  TTDK_CASE(64, 128)
+  TTDK_CASE(64, 64)
+#undef TTDK_CASE
+  return hipErrorInvalidValue;
+}
+
+template <int R>
+using KDenseS = KDense<R, false>;
+template <int R>
+using MNDenseS = MNDense<R, false>;
+template <int R>
+using KConvFwd = KConvGather<R, false>;
+template <int R>
+using KConvDgrad = KConvGather<R, true>;
+
+}  // namespace
+}  // namespace ttdk
+
+using namespace ttdk;
+
+// Epilogue descriptor passed from Python (ctypes Structure with identical layout).
+struct TtdkEpilogue {
+  int mode;
+  void* out;
+  long long ldo;
+  long long slab_stride;
+  const float* bias;
+  const bf16_t* residual;
+  long long ldr;
+  int act;
+  int beta;
+  int remap;
+  int rP, rQ, rOH, rOW, rs;
+  float* stat;
+  float alpha;
+  bf16_t* aux;  // optional second bf16 output: the pre-activation value (same layout as out)
+  const float* ascale0;  // optional device scalars multiplied into alpha (fp8 dequant scales)
+  const float* ascale1;
+  const bf16_t* by;      // optional BN-backward statistics source (see EpiParams::by)
+  const uint8_t* bmask;
+};
+
+inline EpiParams to_epi(const TtdkEpilogue* e) {
+  EpiParams p;
+  p.mode = e->mode;
+  p.out = e->out;
+  p.ldo = e->ldo;
+  p.slab_stride = e->slab_stride;
+  p.bias = e->bias;
+  p.residual = e->residual;
+  p.ldr = e->ldr;
+  p.act = e->act;
+  p.beta = e->beta;
+  p.remap = e->remap;
+  p.rP = e->rP;
+  p.rQ = e->rQ;
+  p.rOH = e->rOH;
+  p.rOW = e->rOW;
+  p.rs = e->rs;
+  p.stat = e->stat;
+  p.alpha = e->alpha == 0.f ? 1.f : e->alpha;
+  p.aux = e->aux;
+  p.ascale0 = e->ascale0;
+  p.ascale1 = e->ascale1;
+  p.by = e->by;
+  p.bmask = e->bmask;
+  return p;
+}
+
+struct TtdkConv {
+  int N, H, W, C;   // input NHWC
+  int K, R, S;      // filters [K][R][S][C]
+  int P, Q;         // output spatial
+  int sh, sw, ph, pw, dh, dw;
+};
+
+inline bool is_pointwise(const TtdkConv* g) {
+  return g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0;
+}
+
+// y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]).
+inline big::ConvP conv_params(const void* src, int Hs, int Ws, int Cs, int P, int Q, const TtdkConv* g, int rows) {
+  return big::ConvP{src, Hs, Ws, Cs, P, Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, rows};
+}
+
