@@ -50,6 +50,27 @@ __global__ void pad_channels_kernel(const bf16_t* __restrict__ x, bf16_t* __rest
   }
 }
 
+// 3 -> 8 channels (RGB image -> the stem's 16-B pixel vectors): 8 pixels per thread, three
+// aligned 16-B loads (8 x 3 bf16 = 48 B) and eight 16-B stores.
+__global__ void pad3to8_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long groups) {
+  GRID_STRIDE(i, groups) {
+    const uint4* src = reinterpret_cast<const uint4*>(x) + i * 3;
+    const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
+    const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+    uint4* dst = reinterpret_cast<uint4*>(y) + i * 8;
+#pragma unroll
+    for (int px = 0; px < 8; ++px) {
+      uint32_t e[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int k = px * 3 + c;  // bf16 index within the 24-element group
+        e[c] = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+      }
+      dst[px] = make_uint4(e[0] | (e[1] << 16), e[2], 0u, 0u);
+    }
+  }
+}
+
 __global__ void unpad_channels_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long rows, int Cp,
                                       int C) {
   GRID_STRIDE(i, rows * C) {
@@ -282,6 +303,11 @@ TTDK_EXPORT int ttdk_bf16_to_f32(const bf16_t* x, float* y, long long n, hipStre
 }
 
 TTDK_EXPORT int ttdk_pad_channels(const bf16_t* x, bf16_t* y, long long rows, int C, int Cp, hipStream_t st) {
+  if (C == 3 && Cp == 8 && rows % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+    hipLaunchKernelGGL(pad3to8_kernel, dim3(grid_for(rows / 8)), dim3(256), 0, st, x, y, rows / 8);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(pad_channels_kernel, dim3(grid_for(rows * Cp)), dim3(256), 0, st, x, y, rows, C, Cp);
   return hipGetLastError();
 }

@@ -193,9 +193,11 @@ class ResNet:
         return out
 
     # ----------------------------------------------------------------- GPU engine
-    def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False):
+    def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False, pool=False):
         """conv + BN (+residual) (+ReLU). x8 = (fp8 copy of x, its scale slot) selects the fp8
         forward GEMM; want8 makes the BN-apply pass also emit an fp8 copy of the output.
+        pool=True (stem): BN + ReLU + 3x3/s2 max pooling in one pass that never stores the
+        BN+ReLU output; returns (pooled, ctx, argmax).
         Returns (out, ctx) or (out, ctx, out8) when want8."""
         from ..ops import gemm as G
         from ..ops import kernels as K
@@ -226,6 +228,9 @@ class ResNet:
         pre = c.name + "_bn/"
         K.bn_fwd_stats(partial, T, M, P.var[pre + "gamma"], P.var[pre + "beta"], self.bn_eps, self.bn_momentum,
                        P.var[pre + "moving_mean"], P.var[pre + "moving_variance"], st)
+        if pool:
+            pooled, arg, mask = K.bn_relu_maxpool(y, st.scale, st.shift)
+            return pooled, (x, y, mask, st), arg
         y2 = y.view(M, c.cout)
         mask = torch.empty(M * c.cout // 8, dtype=torch.uint8, device=x.device) if relu else None
         q8 = slot = None
@@ -302,8 +307,14 @@ class ResNet:
             return r if want8 else (r[0], r[1], None)
 
         # ---- forward
-        s_out, s_ctx = self._convbn_fwd(self.stem, x, relu=True)
-        h, arg = K.maxpool_fwd(s_out, 3, 2, 1)
+        stem_shape = (N, (x.shape[1] + 2 * self.stem.pad - self.stem.k) // self.stem.stride + 1,
+                      (x.shape[2] + 2 * self.stem.pad - self.stem.k) // self.stem.stride + 1, self.stem.cout)
+        pool_fused = self.fuse_bn_bwd and K.stem_pool_fusable(stem_shape)
+        if pool_fused:
+            h, s_ctx, arg = self._convbn_fwd(self.stem, x, relu=True, pool=True)
+        else:
+            s_out, s_ctx = self._convbn_fwd(self.stem, x, relu=True)
+            h, arg = K.maxpool_fwd(s_out, 3, 2, 1)
         h8 = None
         ctxs = []
         for i, blk in enumerate(self.blocks):
@@ -345,8 +356,12 @@ class ResNet:
             else:
                 dx = g_sc
             dh, dh_stat = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1, dstat=st1, feeds=prev_c3)
-        dstem = K.maxpool_bwd(dh, arg, s_out.shape, 3, 2, 1)
-        self._convbn_bwd(self.stem, dstem, s_ctx, need_dx=False)
+        if pool_fused:
+            g, partial, T = K.maxpool_bwd_bnstat(dh, arg, s_ctx[2], s_ctx[1])
+            self._convbn_bwd(self.stem, g, s_ctx, need_dx=False, dstat=(partial, T))
+        else:
+            dstem = K.maxpool_bwd(dh, arg, s_out.shape, 3, 2, 1)
+            self._convbn_bwd(self.stem, dstem, s_ctx, need_dx=False)
         self._grad_hook = None
         return sums
 

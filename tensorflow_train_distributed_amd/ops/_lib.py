@@ -69,6 +69,9 @@ _SIGS = {
     "ttdk_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "ttdk_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
     "ttdk_avgpool_fwd": [P, P, P, I, I, I, P],
+    "ttdk_bn_relu_maxpool": [P, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ttdk_maxpool_bwd_bnstat_blocks": [I, I, I, I],
+    "ttdk_maxpool_bwd_bnstat": [P, P, P, P, P, P, I, I, I, I, I, I, P],
     "ttdk_avgpool_bwd": [P, P, I, I, I, P],
     # xent.hip
     "ttdk_sparse_xent": [P, I, P, I, I, I, F, P, P, P, P, P],

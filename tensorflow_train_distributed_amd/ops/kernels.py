@@ -160,6 +160,37 @@ def maxpool_bwd(dy, arg, x_shape, k=3, s=2, p=1):
     return dx
 
 
+def stem_pool_fusable(y_shape, k=3, s=2, p=1):
+    N, H, W, C = y_shape
+    return (k, s, p) == (3, 2, 1) and H % 2 == 0 and W % 2 == 0 and C % 8 == 0 and 256 % (C // 8) == 0
+
+
+def bn_relu_maxpool(y, scale, shift):
+    """pooled = maxpool3x3/s2/p1(relu(y*scale + shift)) without storing the BN+ReLU output;
+    returns (pooled, argmax bytes, ReLU bit mask of the activation) — see pool.hip."""
+    N, H, W, C = y.shape
+    P, Q = H // 2, W // 2
+    out = torch.empty((N, P, Q, C), dtype=y.dtype, device=y.device)
+    arg = torch.empty((N, P, Q, C), dtype=torch.uint8, device=y.device)
+    mask = torch.empty(N * H * W * C // 8, dtype=torch.uint8, device=y.device)
+    _lib.call("ttdk_bn_relu_maxpool", y.data_ptr(), scale.data_ptr(), shift.data_ptr(), out.data_ptr(), arg.data_ptr(),
+              mask.data_ptr(), N, H, W, C, P, Q, _s())
+    return out, arg, mask
+
+
+def maxpool_bwd_bnstat(dy, arg, mask, y):
+    """g = relu_mask * maxpool_bwd(dy) plus the BN-backward partial sums (sum g, sum g*y) of the
+    stem BN; returns (g, partial [T, 2, C], T) for bn_backward_from_partial."""
+    N, H, W, C = y.shape
+    P, Q = dy.shape[1], dy.shape[2]
+    T = _lib.query("ttdk_maxpool_bwd_bnstat_blocks", N, P, Q, C)
+    g = torch.empty_like(y)
+    partial = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
+    _lib.call("ttdk_maxpool_bwd_bnstat", dy.data_ptr(), arg.data_ptr(), mask.data_ptr(), y.data_ptr(), g.data_ptr(),
+              partial.data_ptr(), N, H, W, C, P, Q, _s())
+    return g, partial, T
+
+
 def avgpool_fwd(x):
     N, H, W, C = x.shape
     y = torch.empty((N, C), dtype=x.dtype, device=x.device)

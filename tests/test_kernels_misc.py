@@ -204,3 +204,44 @@ def test_colsum_and_dgrad_accumulate():
     out = base.clone()
     G.conv_dgrad(dy, w.permute(3, 1, 2, 0).contiguous(), (2, 8, 8, 32), (1, 1), (1, 1), out=out, beta=1)
     assert _rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 16, 64), (2, 12, 10, 32), (3, 8, 8, 256)])
+def test_stem_fused_bn_relu_maxpool_and_backward_stats(shape):
+    """Fused BN+ReLU+maxpool (stem) equals bn_apply followed by maxpool_fwd bit for bit; the
+    fused pooling backward equals maxpool_bwd * relu mask with exact BN partial sums."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(5)
+    N, H, W, C = shape
+    y = torch.randn(shape, device="cuda").bfloat16()
+    scale = torch.rand(C, device="cuda") + 0.5
+    shift = torch.randn(C, device="cuda") * 0.3
+    mask_ref = torch.empty(N * H * W * C // 8, dtype=torch.uint8, device="cuda")
+    act = K.bn_apply(y.view(-1, C), scale, shift, relu=True, mask=mask_ref).view(shape)
+    pooled_ref, arg_ref = K.maxpool_fwd(act, 3, 2, 1)
+    assert K.stem_pool_fusable(shape)
+    pooled, arg, mask = K.bn_relu_maxpool(y, scale, shift)
+    assert torch.equal(pooled, pooled_ref)
+    assert torch.equal(arg, arg_ref)
+    assert torch.equal(mask, mask_ref)
+    dy = torch.randn_like(pooled)
+    dx_ref = K.maxpool_bwd(dy, arg_ref, shape, 3, 2, 1).float()
+    bits = ((mask_ref[:, None] >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1).view(shape).float()
+    g_ref = dx_ref * bits
+    g, partial, T = K.maxpool_bwd_bnstat(dy, arg, mask, y)
+    assert partial.shape[0] == T
+    torch.testing.assert_close(g.float(), g_ref, rtol=1e-2, atol=1e-2)
+    sums = partial.sum(0)
+    gf = g.float().view(-1, C)
+    torch.testing.assert_close(sums[0], gf.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(sums[1], (gf * y.float().view(-1, C)).sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_pad_channels_rgb_fast_path():
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    x = torch.randn(3, 17, 16, 3, device="cuda").bfloat16()  # rows % 8 == 0 -> vector path
+    y = K.pad_channels(x, 8)
+    assert torch.equal(y[..., :3], x) and bool((y[..., 3:] == 0).all())
+    x2 = torch.randn(3, 5, 3, 3, device="cuda").bfloat16()  # 45 rows -> generic path
+    y2 = K.pad_channels(x2, 8)
+    assert torch.equal(y2[..., :3], x2) and bool((y2[..., 3:] == 0).all())
