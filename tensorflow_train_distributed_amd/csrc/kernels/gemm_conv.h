@@ -683,46 +683,90 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, t
   epilogue<BM, BN>(pe, acc, m0, n0, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane, M, N, blockIdx.y, tile_m, smem);
 }
 
-// Sums split-K fp32 slabs: out[i] (+)= sum_s ws[s*n + i]. grid.y groups slabs by 8 so even a
-// small output (a few K elements) gets enough threads in flight; with >1 group the partial
-// sums land with float atomics into a pre-zeroed (or beta-preloaded) output.
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long n, float* __restrict__ out,
-                                     int beta, int per_group, int atomic) {
+// Split-K reduction of fp32 slabs ws[splits][n] into out (+= when beta), deterministic, no
+// atomics, no memset. One pass when the output alone gives enough threads; otherwise pass 1
+// folds each group of `per` slabs into the group's first slab IN PLACE (every thread reads
+// and writes only its own elements) with 4 independent loads in flight per thread, and
+// pass 2 sums the group heads. The group count is chosen so pass 1 runs ~2^19 threads (the
+// wgrad slabs are tens of MB; the old atomic reducer plus its memset ran at ~1.7 TB/s).
+__global__ __launch_bounds__(256) void splitk_fold_kernel(float* __restrict__ ws, int splits, long long n, int per,
+                                                          float* __restrict__ out, int beta) {
   const long long i4 = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
   if (i4 >= n) return;
-  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
+  const int s0 = blockIdx.y * per, s1 = min(splits, s0 + per);
+  // out == nullptr: write the group sum to slab s0 (pass 1); else out (+)= sum (single pass / pass 2,
+  // where the "slabs" are the group heads: stride per*n)
   if (i4 + 3 < n) {
-    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
-    for (int k = s0; k < s1; ++k) s += *reinterpret_cast<const f32x4_t*>(ws + k * n + i4);
-    if (atomic) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(out + i4 + j, s[j]);
+    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    int k = s0;
+    for (; k + 3 < s1; k += 4) {
+      a0 += *reinterpret_cast<const f32x4_t*>(ws + k * n + i4);
+      a1 += *reinterpret_cast<const f32x4_t*>(ws + (k + 1) * n + i4);
+      a2 += *reinterpret_cast<const f32x4_t*>(ws + (k + 2) * n + i4);
+      a3 += *reinterpret_cast<const f32x4_t*>(ws + (k + 3) * n + i4);
+    }
+    for (; k < s1; ++k) a0 += *reinterpret_cast<const f32x4_t*>(ws + k * n + i4);
+    f32x4_t sum = (a0 + a1) + (a2 + a3);
+    if (out) {
+      if (beta) sum += *reinterpret_cast<const f32x4_t*>(out + i4);
+      *reinterpret_cast<f32x4_t*>(out + i4) = sum;
     } else {
-      if (beta) s += *reinterpret_cast<const f32x4_t*>(out + i4);
-      *reinterpret_cast<f32x4_t*>(out + i4) = s;
+      *reinterpret_cast<f32x4_t*>(ws + s0 * n + i4) = sum;
     }
   } else {
     for (long long i = i4; i < n; ++i) {
       float t = 0.f;
       for (int k = s0; k < s1; ++k) t += ws[k * n + i];
-      if (atomic)
-        atomicAdd(out + i, t);
-      else
+      if (out)
         out[i] = t + (beta ? out[i] : 0.f);
+      else
+        ws[s0 * n + i] = t;
     }
   }
 }
 
-hipError_t splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {
-  const int per_group = 8;
-  const int groups = (splits + per_group - 1) / per_group;
-  const int atomic = groups > 1;
-  if (atomic && !beta) {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * n, st);
-    if (e != hipSuccess) return e;
+// pass 2: out[i] (+)= sum over g of ws[g*per*n + i]
+__global__ __launch_bounds__(256) void splitk_heads_kernel(const float* __restrict__ ws, int groups, int per,
+                                                           long long n, float* __restrict__ out, int beta) {
+  const long long i4 = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  const long long gs = static_cast<long long>(per) * n;
+  if (i4 + 3 < n) {
+    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    int g = 0;
+    for (; g + 1 < groups; g += 2) {
+      a0 += *reinterpret_cast<const f32x4_t*>(ws + g * gs + i4);
+      a1 += *reinterpret_cast<const f32x4_t*>(ws + (g + 1) * gs + i4);
+    }
+    if (g < groups) a0 += *reinterpret_cast<const f32x4_t*>(ws + g * gs + i4);
+    f32x4_t sum = a0 + a1;
+    if (beta) sum += *reinterpret_cast<const f32x4_t*>(out + i4);
+    *reinterpret_cast<f32x4_t*>(out + i4) = sum;
+  } else {
+    for (long long i = i4; i < n; ++i) {
+      float t = 0.f;
+      for (int g = 0; g < groups; ++g) t += ws[g * gs + i];
+      out[i] = t + (beta ? out[i] : 0.f);
+    }
   }
-  dim3 grid(ceil_div((n + 3) / 4, 256), groups);
-  hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, ws, splits, n, out, beta, per_group, atomic);
+}
+
+hipError_t splitk_reduce(const float* ws_c, int splits, long long n, float* out, int beta, hipStream_t st) {
+  float* ws = const_cast<float*>(ws_c);  // pass 1 folds in place (the slabs are the caller's scratch)
+  const long long vec = (n + 3) / 4;
+  const int bx = ceil_div(vec, 256);
+  long long want = ((1LL << 19) + vec - 1) / vec;  // groups for ~2^19 pass-1 threads
+  int groups = static_cast<int>(want < 1 ? 1 : (want > splits ? splits : want));
+  int per = ceil_div(splits, groups);
+  if (per < 4 && splits >= 4) per = 4;  // at least 4 slabs per group (independent loads)
+  groups = ceil_div(splits, per);
+  if (groups <= 1) {
+    hipLaunchKernelGGL(splitk_fold_kernel, dim3(bx, 1), dim3(256), 0, st, ws, splits, n, splits, out, beta);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(splitk_fold_kernel, dim3(bx, groups), dim3(256), 0, st, ws, splits, n, per,
+                     static_cast<float*>(nullptr), 0);
+  hipLaunchKernelGGL(splitk_heads_kernel, dim3(bx), dim3(256), 0, st, ws, groups, per, n, out, beta);
   return hipGetLastError();
 }
 

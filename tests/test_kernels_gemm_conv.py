@@ -262,3 +262,21 @@ def test_conv_dgrad_bn_backward_stat_epilogue(cfg, beta):
     assert T == G.dgrad_stat_tile((N, H, W, C), tuple(wt.shape), (s, s), (p, p))[2]
     # strided convs write dx in parts (phases / sampled pixels): no fused statistics
     assert G.dgrad_stat_tile((N, 2 * H, 2 * W, C), tuple(wt.shape), (2, 2), (p, p)) is None
+
+
+@pytest.mark.parametrize("splits", [2, 7, 64, 300])
+def test_splitk_reduce_many_slabs_with_accumulate(splits):
+    """Split-K fp32 output over many slabs (single-pass and two-pass fold) with beta
+    accumulation into an existing gradient, vs fp32 reference."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(3)
+    M, N, K = 130, 70, 64 * 320
+    a = torch.randn(K, M, device="cuda").bfloat16()
+    b = torch.randn(K, N, device="cuda").bfloat16()
+    ref = a.float().t() @ b.float()
+    base = torch.randn(M, N, device="cuda")
+    out = base.clone()
+    G.gemm(a, b, trans_a=True, out=out, splits=splits, beta=1)
+    assert _rel(out, ref + base) < 1e-4
+    out2 = G.gemm(a, b, trans_a=True, out_dtype=torch.float32, splits=splits)
+    assert _rel(out2, ref) < 1e-4
