@@ -11,6 +11,7 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
   EpiParams pe = to_epi(epi);
   if (pe.by && (pe.stat == nullptr || pe.mode != 0 || g->C % 8 || pe.ldo % 8 || pe.residual || pe.act))
     return hipErrorInvalidValue;
+  if ((pe.by2 || pe.stat2) && !(pe.by && pe.by2 && pe.stat2)) return hipErrorInvalidValue;
   const int N = g->C, K = g->R * g->S * g->K;
   DenseParams pb{wt, K, N, K};
   if (g->R == 1 && g->S == 1 && g->ph == 0 && g->pw == 0) {
@@ -111,10 +112,13 @@ TTDK_EXPORT int ttdk_conv_dgrad_subpixel(const bf16_t* dy, const bf16_t* wt, con
   if (g->sw != s || s < 2 || g->dh != 1 || g->dw != 1 || g->R < s || g->S < s || g->K % 8 || g->C % 8)
     return hipErrorInvalidValue;
   EpiParams pe = to_epi(epi);
-  if (pe.remap || pe.stat || pe.residual || pe.aux || pe.mode == 1) return hipErrorInvalidValue;
+  if (pe.remap || pe.residual || pe.aux || pe.mode == 1 || pe.by2 || pe.stat2) return hipErrorInvalidValue;
+  if ((pe.stat != nullptr) != (pe.by != nullptr) || (pe.by && (pe.mode != 0 || g->C % 8 || pe.ldo % 8)))
+    return hipErrorInvalidValue;
   const int N = g->C, Kc = g->K;
   const size_t esz = pe.mode == 0 ? sizeof(bf16_t) : sizeof(float);
   bf16_t* wsp = ws;
+  long long stat_row = 0;  // BN-backward statistics: each phase GEMM owns its own block of tile rows
   for (int a = 0; a < s; ++a) {
     const Phase pr = phase_of(a, s, g->ph, g->R, g->H);
     for (int b = 0; b < s; ++b) {
@@ -132,9 +136,18 @@ TTDK_EXPORT int ttdk_conv_dgrad_subpixel(const bf16_t* dy, const bf16_t* wt, con
       e.rOH = g->H;
       e.rOW = g->W;
       e.rs = s;
-      e.out = static_cast<char*>(pe.out) + (static_cast<long long>(a) * g->W + b) * pe.ldo * esz;
+      const long long base = (static_cast<long long>(a) * g->W + b) * pe.ldo;  // phase origin (elements)
+      e.out = static_cast<char*>(pe.out) + base * esz;
       hipError_t err;
       const int bbn = big_bn(M, N, K);
+      if (pe.by) {
+        e.by = pe.by + base;
+        e.bmask = pe.bmask ? pe.bmask + base / 8 : nullptr;
+        e.stat = pe.stat + stat_row * 2 * N;
+        int pbm = 0, pbn = 0;
+        pick_tile(M, N, &pbm, &pbn);
+        stat_row += ceil_div(M, (bbn && Kc % 64 == 0) ? 256 : pbm);
+      }
       if (bbn && Kc % 64 == 0) {
         const big::ConvP pa{dy, g->P, g->Q, Kc, pr.n, pc.n, pr.T, pc.T, 1, 1, pr.off, pc.off, 1, 1, M};
         const big::DenseP pb{wsp, K, N};
@@ -153,4 +166,25 @@ TTDK_EXPORT int ttdk_conv_dgrad_subpixel(const bf16_t* dy, const bf16_t* wt, con
     }
   }
   return hipGetLastError();
+}
+
+// Tile rows of the BN-backward partial-sum buffer ttdk_conv_dgrad_subpixel fills when its
+// epilogue carries statistics (sum over phases of each phase GEMM's row tiles).
+TTDK_EXPORT long long ttdk_conv_dgrad_subpixel_stat_rows(const TtdkConv* g) {
+  const int s = g->sh;
+  if (g->sw != s || s < 2) return -1;
+  const int N = g->C;
+  long long rows = 0;
+  for (int a = 0; a < s; ++a) {
+    const Phase pr = phase_of(a, s, g->ph, g->R, g->H);
+    for (int b = 0; b < s; ++b) {
+      const Phase pc = phase_of(b, s, g->pw, g->S, g->W);
+      if (pr.n == 0 || pc.n == 0) continue;
+      const int M = g->N * pr.n * pc.n, K = pr.T * pc.T * g->K;
+      int pbm = 0, pbn = 0;
+      pick_tile(M, N, &pbm, &pbn);
+      rows += ceil_div(M, (big_bn(M, N, K) && g->K % 64 == 0) ? 256 : pbm);
+    }
+  }
+  return rows;
 }

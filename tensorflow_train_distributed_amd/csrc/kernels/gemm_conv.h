@@ -369,6 +369,10 @@ struct EpiParams {
   // same layout as out) — the separate bwd-partial pass over dy and y disappears.
   const bf16_t* by;
   const uint8_t* bmask;
+  // optional second BN fed by the same masked gradient (ResNet projection shortcut): stat2
+  // receives per-tile (sum g, sum g*by2)
+  const bf16_t* by2;
+  float* stat2;
 };
 
 __device__ __forceinline__ float epi_alpha(const EpiParams& E) {
@@ -394,14 +398,14 @@ __device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
 template <int BM, int RPP, int PITCH, bool PF>
 __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, int c, int r0, int n, int m0, int M,
                                          int N, bool vst, bool vres, const float (&bias8)[8], float (&s8)[8],
-                                         float (&q8)[8]) {
+                                         float (&q8)[8], float (&r8)[8]) {
   constexpr int NR = (BM + RPP - 1) / RPP;
   constexpr int EB = !PF ? 1 : (NR < 8 ? NR : 8);
   bf16_t* out = static_cast<bf16_t*>(E.out);
   if (n >= N) return;
 #pragma unroll 1
   for (int rb = r0; rb < BM; rb += RPP * EB) {
-    uint4 pres[EB], pold[EB], pby[EB];
+    uint4 pres[EB], pold[EB], pby[EB], pby2[EB];
     uint32_t pmb[EB];
 #pragma unroll
     for (int u = 0; u < EB; ++u) {
@@ -412,6 +416,7 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
         if (E.by) {  // vst is guaranteed by the host (N % 8 == 0, ldo % 8 == 0)
           const long long o = out_row(E, m) * E.ldo + n;
           pby[u] = *reinterpret_cast<const uint4*>(E.by + o);
+          if (E.by2) pby2[u] = *reinterpret_cast<const uint4*>(E.by2 + o);
           pmb[u] = E.bmask ? E.bmask[o >> 3] : 0xffu;
         }
       }
@@ -497,6 +502,11 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
           s8[j] += sv[j];
           q8[j] += sv[j] * yv[j];
         }
+        if (E.by2) {
+          unpack8(pby2[u], yv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r8[j] += sv[j] * yv[j];
+        }
       } else if (E.stat) {
         float sv[8];
         unpack8(packed, sv);  // statistics of the values actually stored
@@ -514,7 +524,7 @@ template <int BM, int BN>
 __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM / 32][BN / 32], int m0, int n0,
                                          int mwave, int nwave, int lane, int M, int N, int split, int tile_m,
                                          char* smem) {
-  static_assert(BM * (BN * 2 + 16) + 4 * 2 * BN * 4 <= 2 * (BM + BN) * BK * 2, "staged epilogue must fit in LDS");
+  static_assert(BM * (BN * 2 + 16) + 4 * 3 * BN * 4 <= 2 * (BM + BN) * BK * 2, "staged epilogue must fit in LDS");
   constexpr int TM = BM / 32, TN = BN / 32;
   const int g = lane >> 4, i16 = lane & 15;
   const float alpha_e = epi_alpha(E);
@@ -565,16 +575,16 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
   const bool nfull = n + 8 <= N;
   const bool vst = nfull && (E.ldo & 7) == 0;
   const bool vres = nfull && (E.ldr & 7) == 0;
-  float bias8[8], s8[8], q8[8];
+  float bias8[8], s8[8], q8[8], r8[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
-    s8[j] = q8[j] = 0.f;
+    s8[j] = q8[j] = r8[j] = 0.f;
   }
   if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
-    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
   else
-    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
   if (E.stat) {
     // lanes sharing a chunk column: lane % CPR equal -> reduce over the wave, then over 4 waves.
 #pragma unroll
@@ -583,28 +593,35 @@ __device__ __forceinline__ void epilogue(const EpiParams& E, f32x4_t (&acc)[BM /
       for (int o = CPR; o < 64; o <<= 1) {
         s8[j] += __shfl_xor(s8[j], o, 64);
         q8[j] += __shfl_xor(q8[j], o, 64);
+        if (E.stat2) r8[j] += __shfl_xor(r8[j], o, 64);
       }
     }
-    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [4 waves][2][BN]
+    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [4 waves][3][BN]
     const int w = tid >> 6;
     if ((tid & 63) < CPR) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        red[(w * 2 + 0) * BN + c * 8 + j] = s8[j];
-        red[(w * 2 + 1) * BN + c * 8 + j] = q8[j];
+        red[(w * 3 + 0) * BN + c * 8 + j] = s8[j];
+        red[(w * 3 + 1) * BN + c * 8 + j] = q8[j];
+        red[(w * 3 + 2) * BN + c * 8 + j] = r8[j];
       }
     }
     __syncthreads();
     for (int t = tid; t < BN; t += NTHR) {
       if (n0 + t < N) {
-        float ss = 0.f, qq = 0.f;
+        float ss = 0.f, qq = 0.f, rr = 0.f;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          ss += red[(k * 2 + 0) * BN + t];
-          qq += red[(k * 2 + 1) * BN + t];
+          ss += red[(k * 3 + 0) * BN + t];
+          qq += red[(k * 3 + 1) * BN + t];
+          rr += red[(k * 3 + 2) * BN + t];
         }
         E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t] = ss;
         E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t] = qq;
+        if (E.stat2) {
+          E.stat2[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t] = ss;
+          E.stat2[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t] = rr;
+        }
       }
     }
   }
@@ -1050,7 +1067,7 @@ struct Geo {
   static constexpr int STAGE = 2 * AH + 2 * BH;
   static constexpr int NB = BNH / 64;         // 16-col blocks per wave per B half
   static constexpr int PITCH = BN * 2 + 16;
-  static constexpr int EPI = BM * PITCH + 8 * 2 * BN * 4;
+  static constexpr int EPI = BM * PITCH + 8 * 3 * BN * 4;  // staged tile + [8 waves][3][BN] statistics
   static constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
 };
 
@@ -1237,16 +1254,16 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
   const bool nfull = n + 8 <= N;
   const bool vst = nfull && (E.ldo & 7) == 0;
   const bool vres = nfull && (E.ldr & 7) == 0;
-  float bias8[8], s8[8], q8[8];
+  float bias8[8], s8[8], q8[8], r8[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
-    s8[j] = q8[j] = 0.f;
+    s8[j] = q8[j] = r8[j] = 0.f;
   }
   if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
-    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
   else
-    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8);
+    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
   if (E.stat) {
     // threads sharing a chunk column c: tid % CPR equal -> within a wave lanes c, c+CPR, ...
 #pragma unroll
@@ -1255,27 +1272,34 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
       for (int o = CPR; o < 64; o <<= 1) {
         s8[j] += __shfl_xor(s8[j], o, 64);
         q8[j] += __shfl_xor(q8[j], o, 64);
+        if (E.stat2) r8[j] += __shfl_xor(r8[j], o, 64);
       }
     }
-    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [8 waves][2][BN]
+    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [8 waves][3][BN]
     if (lane < CPR) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        red[(wave * 2 + 0) * BN + c * 8 + j] = s8[j];
-        red[(wave * 2 + 1) * BN + c * 8 + j] = q8[j];
+        red[(wave * 3 + 0) * BN + c * 8 + j] = s8[j];
+        red[(wave * 3 + 1) * BN + c * 8 + j] = q8[j];
+        red[(wave * 3 + 2) * BN + c * 8 + j] = r8[j];
       }
     }
     __syncthreads();
     for (int t2 = tid; t2 < BN; t2 += THR) {
       if (n0 + t2 < N) {
-        float ss = 0.f, qq = 0.f;
+        float ss = 0.f, qq = 0.f, rr = 0.f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          ss += red[(k * 2 + 0) * BN + t2];
-          qq += red[(k * 2 + 1) * BN + t2];
+          ss += red[(k * 3 + 0) * BN + t2];
+          qq += red[(k * 3 + 1) * BN + t2];
+          rr += red[(k * 3 + 2) * BN + t2];
         }
         E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t2] = ss;
         E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t2] = qq;
+        if (E.stat2) {
+          E.stat2[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t2] = ss;
+          E.stat2[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t2] = rr;
+        }
       }
     }
   }
@@ -1394,6 +1418,8 @@ struct TtdkEpilogue {
   const float* ascale1;
   const bf16_t* by;      // optional BN-backward statistics source (see EpiParams::by)
   const uint8_t* bmask;
+  const bf16_t* by2;     // optional second statistics source (EpiParams::by2 / stat2)
+  float* stat2;
 };
 
 inline EpiParams to_epi(const TtdkEpilogue* e) {
@@ -1420,6 +1446,8 @@ inline EpiParams to_epi(const TtdkEpilogue* e) {
   p.ascale1 = e->ascale1;
   p.by = e->by;
   p.bmask = e->bmask;
+  p.by2 = e->by2;
+  p.stat2 = e->stat2;
   return p;
 }
 

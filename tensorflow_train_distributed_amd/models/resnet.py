@@ -244,11 +244,13 @@ class ResNet:
         return out, (x, y, mask, st)
 
     def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0, dstat=None,
-                    feeds=None):
+                    feeds=None, feeds2=None):
         """Backward of one conv+BN(+ReLU) unit. dout: gradient of the unit's output; with
         dstat = (partial, T) it is already ReLU-masked and its BN-backward sums came from the
         producing dgrad's epilogue. feeds: ctx of the conv+BN unit whose output is this conv's
-        input — the dgrad epilogue then emits that unit's masked gradient + sums.
+        input — the dgrad epilogue then emits that unit's masked gradient + sums; feeds2: a
+        second unit (projection shortcut BN) fed by the same gradient, whose sums come back as
+        the third element of dstat_of_dx.
         Returns (dx, dstat_of_dx)."""
         from ..ops import gemm as G
         from ..ops import kernels as K
@@ -272,8 +274,12 @@ class ResNet:
         wt = K.krsc_to_crsk(P.c[wname])
         stride, pad = (c.stride, c.stride), (c.pad, c.pad)
         if (feeds is not None and self.fuse_bn_bwd
-                and G.dgrad_stat_tile(tuple(x.shape), tuple(wt.shape), stride, pad) is not None):
+                and G.dgrad_stat_rows(tuple(x.shape), tuple(wt.shape), stride, pad) is not None):
             _, fy, fmask, _ = feeds
+            if feeds2 is not None and stride == (1, 1):
+                out, partial, T, partial2 = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta,
+                                                         bn_stat=(fy, fmask), bn_stat2=feeds2[1])
+                return out, (partial, T, partial2)
             out, partial, T = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, bn_stat=(fy, fmask))
             return out, (partial, T)
         return G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta), None
@@ -344,18 +350,21 @@ class ResNet:
             blk = self.blocks[i]
             c1, c2, c3, cd = ctxs[i]
             prev_c3 = ctxs[i - 1][2] if i > 0 else None  # the unit that produced this block's input
+            prev_cd = ctxs[i - 1][3] if i > 0 else None  # its projection shortcut (fed by the same gradient)
             if dh_stat is not None:
                 g_sc = dh  # already ReLU-masked by the producing dgrad epilogue
-                d2, st2 = self._convbn_bwd(blk["c3"], dh, c3, dstat=dh_stat, feeds=c2)
+                d2, st2 = self._convbn_bwd(blk["c3"], dh, c3, dstat=dh_stat[:2], feeds=c2)
             else:
                 g_sc = torch.empty_like(dh)
                 d2, st2 = self._convbn_bwd(blk["c3"], dh, c3, g_out=g_sc, feeds=c2)
             d1, st1 = self._convbn_bwd(blk["c2"], d2, c2, dstat=st2, feeds=c1)
             if blk["cd"] is not None:
-                dx, _ = self._convbn_bwd(blk["cd"], g_sc, cd)
+                cd_stat = (dh_stat[2], dh_stat[1]) if dh_stat is not None and len(dh_stat) == 3 else None
+                dx, _ = self._convbn_bwd(blk["cd"], g_sc, cd, dstat=cd_stat)
             else:
                 dx = g_sc
-            dh, dh_stat = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1, dstat=st1, feeds=prev_c3)
+            dh, dh_stat = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1, dstat=st1, feeds=prev_c3,
+                                           feeds2=prev_cd)
         if pool_fused:
             g, partial, T = K.maxpool_bwd_bnstat(dh, arg, s_ctx[2], s_ctx[1])
             self._convbn_bwd(self.stem, g, s_ctx, need_dx=False, dstat=(partial, T))

@@ -33,6 +33,7 @@ class Epilogue(ctypes.Structure):
         ("beta", c_int), ("remap", c_int), ("rP", c_int), ("rQ", c_int), ("rOH", c_int),
         ("rOW", c_int), ("rs", c_int), ("stat", c_void_p), ("alpha", c_float), ("aux", c_void_p),
         ("ascale0", c_void_p), ("ascale1", c_void_p), ("by", c_void_p), ("bmask", c_void_p),
+        ("by2", c_void_p), ("stat2", c_void_p),
     ]
 
 
@@ -52,6 +53,7 @@ _SIGS = {
     "ttdk_conv_fwd": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad_subpixel": [P, P, G, P, E, P],
+    "ttdk_conv_dgrad_subpixel_stat_rows": [G],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
     # batchnorm.hip
@@ -107,13 +109,16 @@ def register(sigs: dict):
     _SIGS.update(sigs)
 
 
+_RESTYPE = {"ttdk_conv_dgrad_subpixel_stat_rows": c_longlong}
+
+
 def fn(name):
     f = _fns.get(name)
     if f is None:
         lib = _native.hip()
         f = getattr(lib, name)
         f.argtypes = _SIGS[name]
-        f.restype = c_int
+        f.restype = _RESTYPE.get(name, c_int)
         _fns[name] = f
     return f
 

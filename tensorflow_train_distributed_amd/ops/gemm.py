@@ -33,7 +33,7 @@ def _log(kind, M, N, K, splits=1):
 
 
 def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,
-         slab_stride=0, aux=None, ascale=(None, None), by=None, bmask=None):
+         slab_stride=0, aux=None, ascale=(None, None), by=None, bmask=None, by2=None, stat2=None):
     e = _lib.Epilogue()
     e.mode = mode
     e.out = out.data_ptr()
@@ -51,6 +51,8 @@ def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat
     e.ascale1 = ascale[1].data_ptr() if ascale[1] is not None else None
     e.by = by.data_ptr() if by is not None else None
     e.bmask = bmask.data_ptr() if bmask is not None else None
+    e.by2 = by2.data_ptr() if by2 is not None else None
+    e.stat2 = stat2.data_ptr() if stat2 is not None else None
     return e
 
 
@@ -209,17 +211,35 @@ def _pick_tile(M, N):
     return (64 if M <= 64 else 128), (64 if N <= 64 else 128)
 
 
-def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
-    """(bm, bn, rows) the data-gradient launcher uses when the epilogue also emits BN-backward
-    statistics (conv_dgrad(bn_stat=...)), or None when that fusion is not available (strided
-    convs: their GEMMs write dx in parts — sub-pixel phases, or only the sampled pixels)."""
+def _subpixel_ok(g, R, S, stride, padding):
+    return (_SUBPIXEL and not (R == 1 and S == 1 and tuple(padding) == (0, 0)) and g.sh == g.sw and g.sh > 1
+            and R >= g.sh and S >= g.sw)
+
+
+def dgrad_stat_rows(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
+    """Partial-sum rows the data-gradient launcher writes when its epilogue also emits the
+    consuming BN's backward statistics (conv_dgrad(bn_stat=...)), or None when that fusion is
+    not available (strided 1x1: only the sampled pixels are computed)."""
     C, R, S, K = wt_shape
     N, H, W, _ = x_shape
-    pointwise = R == 1 and S == 1 and tuple(padding) == (0, 0)
-    if tuple(stride) != (1, 1):  # strided: sub-pixel phases / sampled-row remap cover dx only in parts
-        return None
     if C % 8:
         return None
+    if tuple(stride) != (1, 1):
+        g = conv_geom(tuple(x_shape), (K, R, S, C), stride, padding)
+        if not _subpixel_ok(g, R, S, stride, padding):
+            return None
+        return int(_lib.fn("ttdk_conv_dgrad_subpixel_stat_rows")(ctypes.byref(g)))
+    return dgrad_stat_tile(x_shape, wt_shape)[2]
+
+
+def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
+    """(bm, bn, rows) of a unit-stride data-gradient launch with the BN-statistics epilogue
+    (mirror of ttdk_conv_dgrad's tile choice when `stat` is set)."""
+    C, R, S, K = wt_shape
+    N, H, W, _ = x_shape
+    if tuple(stride) != (1, 1):
+        return None
+    pointwise = R == 1 and S == 1 and tuple(padding) == (0, 0)
     M = N * H * W
     Kg = R * S * K
     bbn = big_bn(M, C, Kg)
@@ -230,7 +250,7 @@ def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
 
 
 def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
-               tile=(0, 0), bn_stat=None):
+               tile=(0, 0), bn_stat=None, bn_stat2=None):
     """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
 
     For strided 1x1 convs only the sampled pixels are written: pass a zero-initialised `out`
@@ -239,7 +259,8 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     bn_stat=(y, mask): dx is the output gradient of a conv+BN(+ReLU) unit whose pre-BN conv
     output is y (same shape as dx) and ReLU bit mask is `mask` (or None). The epilogue then
     stores g = dx * mask and per-tile BN-backward partial sums (sum g, sum g*y); returns
-    (out, partial [T, 2, C], T). Requires dgrad_stat_tile(...) to be not None.
+    (out, partial [T, 2, C], T). bn_stat2=y2: a second BN fed by the same g (projection
+    shortcut); returns (out, partial, T, partial2). Requires dgrad_stat_rows(...) not None.
     """
     _check(dy, torch.bfloat16, "dy")
     _check(wt, torch.bfloat16, "wt")
@@ -251,20 +272,35 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
         out = alloc(tuple(x_shape), dtype=torch.bfloat16, device=dy.device)
     if bn_stat is not None:
         y, mask = bn_stat
-        t = dgrad_stat_tile(tuple(x_shape), tuple(wt.shape), stride, padding)
-        if t is None or residual is not None or tuple(y.shape) != tuple(x_shape):
+        T = dgrad_stat_rows(tuple(x_shape), tuple(wt.shape), stride, padding)
+        if T is None or residual is not None or tuple(y.shape) != tuple(x_shape):
             raise ValueError("conv_dgrad: BN-statistics epilogue not available for this conv")
         _check(y, torch.bfloat16, "bn_stat y")
-        bm, bn, T = t
         partial = torch.empty((T, 2, C), dtype=torch.float32, device=dy.device)
-        e = _epi(out, ldo=C, beta=beta, stat=partial, by=y, bmask=mask)
-        _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * (g.P * g.Q if strided_pw else g.H * g.W), C, R * S * K)
-        _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), bm, bn, ctypes.byref(e),
-                  _lib.stream())
-        return out, partial, T
+        partial2 = None
+        if bn_stat2 is not None:
+            _check(bn_stat2, torch.bfloat16, "bn_stat2")
+            if tuple(bn_stat2.shape) != tuple(x_shape) or tuple(stride) != (1, 1):
+                raise ValueError("conv_dgrad: second BN statistics need a unit-stride dgrad of the same shape")
+            partial2 = torch.empty((T, 2, C), dtype=torch.float32, device=dy.device)
+        e = _epi(out, ldo=C, beta=beta, stat=partial, by=y, bmask=mask, by2=bn_stat2, stat2=partial2)
+        if tuple(stride) != (1, 1):
+            if _LOG is not None:
+                for pa in _phases(g.sh, g.ph, R, g.H):
+                    for pb in _phases(g.sw, g.pw, S, g.W):
+                        _log("dgrad_%dx%d_s%d_phase%dx%d" % (R, S, g.sh, pa[0], pb[0]), g.N * pa[1] * pb[1], C,
+                             pa[0] * pb[0] * K)
+            ws = torch.empty_like(wt)
+            _lib.call("ttdk_conv_dgrad_subpixel", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), ws.data_ptr(),
+                      ctypes.byref(e), _lib.stream())
+        else:
+            bm, bn, _ = dgrad_stat_tile(tuple(x_shape), tuple(wt.shape))
+            _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * g.H * g.W, C, R * S * K)
+            _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), bm, bn, ctypes.byref(e),
+                      _lib.stream())
+        return (out, partial, T) if partial2 is None else (out, partial, T, partial2)
     e = _epi(out, ldo=C, beta=beta, residual=residual)
-    if (_SUBPIXEL and not strided_pw and g.sh == g.sw and g.sh > 1 and R >= g.sh and S >= g.sw and residual is None
-            and tile == (0, 0)):
+    if _subpixel_ok(g, R, S, stride, padding) and residual is None and tile == (0, 0):
         # strided dgrad as s*s unit-stride phase GEMMs (skips the zero taps of the direct gather)
         if _LOG is not None:  # one GEMM per phase, in ttdk_conv_dgrad_subpixel's launch order
             for pa in _phases(g.sh, g.ph, R, g.H):

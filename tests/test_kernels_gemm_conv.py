@@ -225,16 +225,20 @@ def test_gemm256_lds_dma_path_all_layouts(ta, tb, M, N, K):
 
 
 @pytest.mark.parametrize("cfg", [
-    # N, H, W, C, K, R, stride, pad — 4-wave tiles, 256-row tiles (1x1 dense + 3x3 gather)
+    # N, H, W, C, K, R, stride, pad — 4-wave tiles, 256-row tiles (1x1 dense + 3x3 gather),
+    # strided 3x3 as sub-pixel phases (4-wave and 256-row phase GEMMs); dx is [N, H, W, C]
     (2, 14, 14, 64, 64, 3, 1, 1),
     (16, 16, 16, 128, 256, 1, 1, 0),
     (8, 32, 32, 128, 128, 3, 1, 1),
     (16, 32, 32, 256, 64, 1, 1, 0),
+    (2, 16, 16, 64, 128, 3, 2, 1),
+    (8, 56, 56, 128, 128, 3, 2, 1),
 ])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_conv_dgrad_bn_backward_stat_epilogue(cfg, beta):
     """dgrad whose epilogue stores g = dx * relu_mask and per-tile (sum g, sum g*y) of the
-    consuming BN (the fused BN-backward statistics) vs an fp32 reference."""
+    consuming BN (the fused BN-backward statistics), plus (sum g, sum g*y2) of a second BN fed
+    by the same gradient (projection shortcut), vs an fp32 reference."""
     from tensorflow_train_distributed_amd.ops import gemm as G
     N, H, W, C, K, R, s, p = cfg
     torch.manual_seed(11)
@@ -243,6 +247,7 @@ def test_conv_dgrad_bn_backward_stat_epilogue(cfg, beta):
     w = (torch.randn(K, R, R, C, device="cuda") / (R * R * C) ** 0.5).bfloat16()
     wt = w.permute(3, 1, 2, 0).contiguous()
     y = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    y2 = torch.randn(N, H, W, C, device="cuda").bfloat16()
     keep = torch.rand(N * H * W * C, device="cuda") > 0.3
     bits = keep.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)
     mask = bits.sum(1).to(torch.uint8)
@@ -252,16 +257,23 @@ def test_conv_dgrad_bn_backward_stat_epilogue(cfg, beta):
         ref = ref + old.float()
     ref_g = ref * keep.view(N, H, W, C)
     out = old.clone() if beta else None
-    got, partial, T = G.conv_dgrad(dy, wt, (N, H, W, C), (s, s), (p, p), out=out, beta=beta, bn_stat=(y, mask))
+    second = s == 1
+    res = G.conv_dgrad(dy, wt, (N, H, W, C), (s, s), (p, p), out=out, beta=beta, bn_stat=(y, mask),
+                       bn_stat2=y2 if second else None)
+    got, partial, T = res[:3]
     assert _rel(got, ref_g) < 1e-2
     assert bool(((got.float() != 0) <= keep.view(N, H, W, C)).all())  # masked elements are exact zeros
-    sums = partial.sum(0)
     gs = got.float().view(-1, C)
+    sums = partial.sum(0)
     torch.testing.assert_close(sums[0], gs.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(sums[1], (gs * y.float().view(-1, C)).sum(0), rtol=1e-3, atol=1e-2)
-    assert T == G.dgrad_stat_tile((N, H, W, C), tuple(wt.shape), (s, s), (p, p))[2]
-    # strided convs write dx in parts (phases / sampled pixels): no fused statistics
-    assert G.dgrad_stat_tile((N, 2 * H, 2 * W, C), tuple(wt.shape), (2, 2), (p, p)) is None
+    if second:
+        sums2 = res[3].sum(0)
+        torch.testing.assert_close(sums2[0], gs.sum(0), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(sums2[1], (gs * y2.float().view(-1, C)).sum(0), rtol=1e-3, atol=1e-2)
+    assert T == G.dgrad_stat_rows((N, H, W, C), tuple(wt.shape), (s, s), (p, p))
+    # strided 1x1 convs compute only the sampled pixels: no fused statistics
+    assert G.dgrad_stat_rows((N, 2 * H, 2 * W, C), (C, 1, 1, K), (2, 2), (0, 0)) is None
 
 
 @pytest.mark.parametrize("splits", [2, 7, 64, 300])
