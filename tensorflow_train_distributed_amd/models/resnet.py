@@ -84,6 +84,9 @@ class ResNet:
         # (TTD_FUSE_BN_BWD=0 restores the separate statistics pass, for A/B runs)
         self.fuse_bn_bwd = os.environ.get("TTD_FUSE_BN_BWD", "1") != "0"
         self.device = torch.device(device)
+        # weight gradients on a second HIP stream (TTD_WGRAD_STREAM=0: single stream)
+        self.wgrad_stream = os.environ.get("TTD_WGRAD_STREAM", "1") != "0" and self.device.type == "cuda"
+        self._wgrad_stream = None
         self.num_classes = num_classes
         self.in_channels = in_channels
         self.in_store = 8 if in_channels <= 8 else (in_channels + 7) // 8 * 8
@@ -267,8 +270,21 @@ class ResNet:
                                P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
                                mask=mask).view(N, Pp, Q, Kc)
         wname = c.name + "_conv/kernel"
-        G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
-        self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
+        side = self._wgrad_stream
+        if side is not None:
+            # weight gradient on the side stream, concurrent with this unit's data gradient and
+            # the next units' BN passes (fills the tail waves of the 1-workgroup-per-CU GEMMs)
+            ev = torch.cuda.Event()
+            ev.record()
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+                self._ready(c.name + "_bn/moving_variance")  # collectives order after the side stream
+            x.record_stream(side)
+            dz.record_stream(side)
+        else:
+            G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+            self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
         if not need_dx:
             return None, None
         wt = K.krsc_to_crsk(P.c[wname])
@@ -301,6 +317,11 @@ class ResNet:
         self._grad_hook = grad_hook
         P = self.params
         N = images.shape[0]
+        self._wgrad_stream = None
+        if self.wgrad_stream:
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(device=self.device)
+            self._wgrad_stream = self._side
         if grad_scale is None:
             grad_scale = 1.0 / N
         x = images if images.shape[-1] == self.in_store else K.pad_channels(images.contiguous(), self.in_store)
@@ -371,6 +392,9 @@ class ResNet:
         else:
             dstem = K.maxpool_bwd(dh, arg, s_out.shape, 3, 2, 1)
             self._convbn_bwd(self.stem, dstem, s_ctx, need_dx=False)
+        if self._wgrad_stream is not None:
+            torch.cuda.current_stream().wait_stream(self._wgrad_stream)
+            self._wgrad_stream = None
         self._grad_hook = None
         return sums
 
