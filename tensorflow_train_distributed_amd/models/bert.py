@@ -27,6 +27,7 @@ query/kernel, cls/predictions/output_bias, ...).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -139,6 +140,8 @@ class BertPretraining:
                     if o2 != o + j * width:
                         raise AssertionError("q/k/v %s not contiguous" % name_a)
         self.rng = None
+        # encoder weight gradients on a second HIP stream (TTD_WGRAD_STREAM=0: single stream)
+        self.wgrad_stream = os.environ.get("TTD_WGRAD_STREAM", "1") != "0" and self.device.type == "cuda"
         if self.device.type == "cuda":
             from ..ops.transformer import RngState
             self.rng = RngState(seed * 7919 + 17, self.device)
@@ -250,6 +253,35 @@ class BertPretraining:
             M, N, Kd = dy.shape[1], x.shape[1], dy.shape[0]
             G.gemm(dy, x, trans_a=True, out=out, splits=G.gemm_wgrad_splits(M, N, Kd))
 
+        # encoder weight gradients (+ bias column sums) run on a second HIP stream, overlapping
+        # the data-gradient chain; the bucket hooks are issued from it so collectives order after
+        side = None
+        if self.wgrad_stream:
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(device=dev)
+            side = self._side
+
+        def wgrad_bias(dy, x, wout, bout):
+            if side is None:
+                wgrad(dy, x, wout)
+                K.colsum(dy, out=bout)
+                return
+            ev = torch.cuda.Event()
+            ev.record()
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                wgrad(dy, x, wout)
+                K.colsum(dy, out=bout)
+            dy.record_stream(side)
+            x.record_stream(side)
+
+        def layer_hook(name):
+            if side is None:
+                hook(name)
+            else:
+                with torch.cuda.stream(side):
+                    hook(name)
+
         ids = batch.input_ids.reshape(-1)
         tt = batch.token_type_ids.reshape(-1)
         seqlen = batch.seqlen
@@ -353,23 +385,22 @@ class BertPretraining:
                                        g[self._ln(l, "output/LayerNorm/beta")], ds_out=G1, want_dx=True, p_in=hd,
                                        site_in=site(l, 2), rng=rng, work=ln_work)
             del dy
-            wgrad(dout2, inter, g[self._ln(l, "output/dense/kernel")])
-            K.colsum(dout2, out=g[self._ln(l, "output/dense/bias")])
+            wgrad_bias(dout2, inter, g[self._ln(l, "output/dense/kernel")], g[self._ln(l, "output/dense/bias")])
             dpre = G.gemm(dout2, P.c[self._ln(l, "output/dense/kernel")], act=G.ACT_DGELU, residual=pre)
             del dout2, inter, pre
-            wgrad(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")])
-            K.colsum(dpre, out=g[self._ln(l, "intermediate/dense/bias")])
+            wgrad_bias(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")],
+                       g[self._ln(l, "intermediate/dense/bias")])
             G.gemm(dpre, P.c[self._ln(l, "intermediate/dense/kernel")], out=G1, beta=1)
             del dpre
-            hook(self._ln(l, "intermediate/dense/bias"))
+            layer_hook(self._ln(l, "intermediate/dense/bias"))
             G0 = torch.empty((Tk, H), dtype=bf, device=dev)
             _, dproj = T.layernorm_bwd(G1, s1, m1, r1, P.var[self._ln(l, "attention/output/LayerNorm/gamma")],
                                        g[self._ln(l, "attention/output/LayerNorm/gamma")],
                                        g[self._ln(l, "attention/output/LayerNorm/beta")], ds_out=G0, want_dx=True,
                                        p_in=hd, site_in=site(l, 1), rng=rng, work=ln_work)
             del G1
-            wgrad(dproj, ao, g[self._ln(l, "attention/output/dense/kernel")])
-            K.colsum(dproj, out=g[self._ln(l, "attention/output/dense/bias")])
+            wgrad_bias(dproj, ao, g[self._ln(l, "attention/output/dense/kernel")],
+                       g[self._ln(l, "attention/output/dense/bias")])
             dao = G.gemm(dproj, P.c[self._ln(l, "attention/output/dense/kernel")])
             del dproj
             dqkv = torch.empty((Tk, 3 * H), dtype=bf, device=dev)
@@ -377,12 +408,13 @@ class BertPretraining:
                             dqkv[:, H:2 * H], dqkv[:, 2 * H:], B, NH, S, delta=delta, seqlen=seqlen, p_drop=ad,
                             rng=rng, site=site(l, 0))
             del dao, ao, qkv
-            wgrad(dqkv, x, self._fused(l, "gw"))
-            K.colsum(dqkv, out=self._fused(l, "gb"))
+            wgrad_bias(dqkv, x, self._fused(l, "gw"), self._fused(l, "gb"))
             G.gemm(dqkv, self._fused(l, "w"), out=G0, beta=1)
             del dqkv
-            hook(self._ln(l, "attention/self/value/bias"))
+            layer_hook(self._ln(l, "attention/self/value/bias"))
             dy = G0
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
 
         # ---------------------------------------------------------------- backward: embeddings
         ds0, _ = T.layernorm_bwd(dy, s0, mean0, rstd0, P.var["bert/embeddings/LayerNorm/gamma"],
