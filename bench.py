@@ -171,6 +171,7 @@ def main():
     if rank == 0:
         cfg = dict(info["config"])
         cfg["hipgraph"] = bool(use_graph)
+        cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         cfg["final_loss"] = loss
         print(json.dumps({
             "metric": info["metric"],

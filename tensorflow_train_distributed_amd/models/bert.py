@@ -256,6 +256,7 @@ class BertPretraining:
         # encoder weight gradients (+ bias column sums) run on a second HIP stream, overlapping
         # the data-gradient chain; the bucket hooks are issued from it so collectives order after
         side = None
+        keep = []
         if self.wgrad_stream:
             if getattr(self, "_side", None) is None:
                 self._side = torch.cuda.Stream(device=dev)
@@ -272,8 +273,7 @@ class BertPretraining:
             with torch.cuda.stream(side):
                 wgrad(dy, x, wout)
                 K.colsum(dy, out=bout)
-            dy.record_stream(side)
-            x.record_stream(side)
+            keep.extend((dy, x))  # alive until the streams join (no deferred record_stream frees)
 
         def layer_hook(name):
             if side is None:
@@ -415,6 +415,7 @@ class BertPretraining:
             dy = G0
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
+        keep.clear()
 
         # ---------------------------------------------------------------- backward: embeddings
         ds0, _ = T.layernorm_bwd(dy, s0, mean0, rstd0, P.var["bert/embeddings/LayerNorm/gamma"],

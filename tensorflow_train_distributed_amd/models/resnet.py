@@ -280,8 +280,10 @@ class ResNet:
             with torch.cuda.stream(side):
                 G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
                 self._ready(c.name + "_bn/moving_variance")  # collectives order after the side stream
-            x.record_stream(side)
-            dz.record_stream(side)
+            # keep the operands alive until the streams join at the end of the backward (no
+            # record_stream: its deferred frees made the allocator re-malloc when the host ran
+            # several steps ahead)
+            self._side_keep += [x, dz]
         else:
             G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
             self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
@@ -318,6 +320,7 @@ class ResNet:
         P = self.params
         N = images.shape[0]
         self._wgrad_stream = None
+        self._side_keep = []
         if self.wgrad_stream:
             if getattr(self, "_side", None) is None:
                 self._side = torch.cuda.Stream(device=self.device)
@@ -346,9 +349,22 @@ class ResNet:
         ctxs = []
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            side = self._wgrad_stream
+            if blk["cd"] is not None and side is not None:
+                # projection shortcut on the side stream, concurrent with the c1 -> c2 chain
+                main = torch.cuda.current_stream()
+                ev = torch.cuda.Event()
+                ev.record()
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    sc, cd, _ = unit(blk["cd"], h, False, inp8=h8)
+                # h / h8 stay referenced (c1's ctx) past the join below; cd's outputs were made on
+                # the side stream, whose next work is always ordered after this step's main stream
             o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]))
             o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]))
-            if blk["cd"] is not None:
+            if blk["cd"] is not None and side is not None:
+                main.wait_stream(side)
+            elif blk["cd"] is not None:
                 sc, cd, _ = unit(blk["cd"], h, False, inp8=h8)
             else:
                 sc, cd = h, None
@@ -395,6 +411,7 @@ class ResNet:
         if self._wgrad_stream is not None:
             torch.cuda.current_stream().wait_stream(self._wgrad_stream)
             self._wgrad_stream = None
+        self._side_keep = []
         self._grad_hook = None
         return sums
 
