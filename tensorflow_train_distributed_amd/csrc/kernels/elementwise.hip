@@ -189,23 +189,37 @@ __global__ void bias_act_dropout_bwd_kernel(const T* __restrict__ dy, const T* _
   }
 }
 
-// out[c] (+)= sum_r x[r][c]; grid.x over column chunks of 256, grid.y row slices; atomics.
+// Column sums out[c] (+)= sum_r x[r][c] (bias gradients). grid.x over column chunks, grid.y row
+// slices; each slice writes its partial row ws[slice][C] and colsum_fold_kernel adds the
+// slices in a fixed order (no float atomics: bitwise reproducible). With one slice the
+// kernels write `out` directly (honouring beta).
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ x, long long rows, int C, float* __restrict__ out,
-                              long long rows_per_slice) {
+__global__ void colsum_kernel(const T* __restrict__ x, long long rows, int C, float* __restrict__ dst,
+                              long long rows_per_slice, int beta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const long long r0 = blockIdx.y * rows_per_slice, r1 = min(rows, r0 + rows_per_slice);
   float s = 0.f;
   for (long long r = r0; r < r1; ++r) s += ldv(x, r * C + c);
-  atomicAdd(&out[c], s);
+  float* d = dst + static_cast<long long>(blockIdx.y) * C + c;
+  *d = s + (beta ? *d : 0.f);
+}
+
+__global__ void colsum_fold_kernel(const float* __restrict__ ws, int slices, int C, float* __restrict__ out,
+                                   int beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < slices; ++k) s += ws[static_cast<long long>(k) * C + c];
+  out[c] = s + (beta ? out[c] : 0.f);
 }
 
 // Vectorised bf16 column sum (C % 8 == 0): a 256-thread block covers 256 columns (32 threads
 // x 8 columns, 16-B loads, 512 contiguous bytes per row) x 8 row lanes over its row slice;
-// the 8 row lanes reduce through LDS and each block adds its 256 sums with one atomic each.
+// the 8 row lanes reduce through LDS and each block writes its 256 sums to its slice row.
 __global__ __launch_bounds__(256) void colsum_bf16x8_kernel(const bf16_t* __restrict__ x, long long rows, int C,
-                                                            float* __restrict__ out, long long rows_per_slice) {
+                                                            float* __restrict__ dst, long long rows_per_slice,
+                                                            int beta) {
   __shared__ float red[8][257];
   const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int c = blockIdx.x * 256 + cl * 8;
@@ -240,7 +254,8 @@ __global__ __launch_bounds__(256) void colsum_bf16x8_kernel(const bf16_t* __rest
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += red[k][threadIdx.x];
-    atomicAdd(&out[col], t);
+    float* d = dst + static_cast<long long>(blockIdx.y) * C + col;
+    *d = t + (beta ? *d : 0.f);
   }
 }
 
@@ -358,31 +373,55 @@ TTDK_EXPORT int ttdk_bias_act_dropout_bwd(const void* dy, const void* x, const f
 }
 
 // out[C] = (beta ? out : 0) + column sums of x[rows][C]
-TTDK_EXPORT int ttdk_colsum(const void* x, long long rows, int C, float* out, int beta, int dtype, hipStream_t st) {
-  if (!beta) {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * C, st);
-    if (e != hipSuccess) return e;
-  }
-  if (dtype == 1 && C % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+static void colsum_plan(long long rows, int C, int dtype, bool vec, long long* slices, long long* per) {
+  long long sl;
+  if (vec) {
     const int cblocks = (C + 255) / 256;
-    long long slices = (1024 + cblocks - 1) / cblocks;  // ~1024 blocks
-    const long long max_slices = (rows + 63) / 64;       // >= 64 rows per slice
-    if (slices > max_slices) slices = max_slices;
-    if (slices < 1) slices = 1;
-    const long long per = (rows + slices - 1) / slices;
-    hipLaunchKernelGGL(colsum_bf16x8_kernel, dim3(cblocks, static_cast<int>(slices)), dim3(256), 0, st,
-                       static_cast<const bf16_t*>(x), rows, C, out, per);
-    return hipGetLastError();
+    sl = (1024 + cblocks - 1) / cblocks;            // ~1024 blocks
+    const long long max_slices = (rows + 63) / 64;  // >= 64 rows per slice
+    if (sl > max_slices) sl = max_slices;
+  } else {
+    sl = (rows + 127) / 128;
+    if (sl > 256) sl = 256;
   }
-  long long slices = (rows + 127) / 128;
-  if (slices > 256) slices = 256;
-  if (slices < 1) slices = 1;
-  const long long per = (rows + slices - 1) / slices;
-  dim3 grid((C + 255) / 256, static_cast<int>(slices));
-  if (dtype == 0)
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, static_cast<const float*>(x), rows, C, out, per);
-  else
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(x), rows, C, out, per);
+  if (sl < 1) sl = 1;
+  *per = (rows + sl - 1) / sl;
+  *slices = (rows + *per - 1) / *per;
+  if (*slices < 1) *slices = 1;
+}
+
+// Floats of workspace ttdk_colsum needs (covers both the vector and the scalar plan).
+TTDK_EXPORT long long ttdk_colsum_ws_floats(long long rows, int C, int dtype) {
+  long long s1, s2, per;
+  colsum_plan(rows, C, dtype, true, &s1, &per);
+  colsum_plan(rows, C, dtype, false, &s2, &per);
+  const long long sl = s1 > s2 ? s1 : s2;
+  return sl > 1 ? sl * C : 0;
+}
+
+TTDK_EXPORT int ttdk_colsum(const void* x, long long rows, int C, float* out, int beta, int dtype, float* ws,
+                            hipStream_t st) {
+  const bool vec = dtype == 1 && C % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  long long slices, per;
+  colsum_plan(rows, C, dtype, vec, &slices, &per);
+  if (slices > 1 && !ws) return hipErrorInvalidValue;
+  float* dst = slices > 1 ? ws : out;
+  const int bt = slices > 1 ? 0 : beta;
+  if (vec) {
+    hipLaunchKernelGGL(colsum_bf16x8_kernel, dim3((C + 255) / 256, static_cast<int>(slices)), dim3(256), 0, st,
+                       static_cast<const bf16_t*>(x), rows, C, dst, per, bt);
+  } else {
+    dim3 grid((C + 255) / 256, static_cast<int>(slices));
+    if (dtype == 0)
+      hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, static_cast<const float*>(x), rows, C, dst, per,
+                         bt);
+    else
+      hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(x), rows, C, dst,
+                         per, bt);
+  }
+  if (slices > 1)
+    hipLaunchKernelGGL(colsum_fold_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, static_cast<int>(slices), C,
+                       out, beta);
   return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ template <typename T, typename L>
 __global__ __launch_bounds__(256) void xent_kernel(const T* __restrict__ logits, const L* __restrict__ labels, int V,
                                                    float grad_scale, float* __restrict__ loss_rows,
                                                    T* __restrict__ dlogits, uint8_t* __restrict__ correct,
-                                                   float* __restrict__ sums, float inv_rows) {
+                                                   float* __restrict__ part, float inv_rows) {
   __shared__ float red[16];
   const long long row = blockIdx.x;
   const T* z = logits + row * V;
@@ -68,10 +68,27 @@ __global__ __launch_bounds__(256) void xent_kernel(const T* __restrict__ logits,
     const bool ok = lab_ok && isfinite(zt) && gsum < 1.f;
     if (loss_rows) loss_rows[row] = loss;
     if (correct) correct[row] = ok;
-    if (sums) {
-      atomicAdd(&sums[0], loss * inv_rows);
-      atomicAdd(&sums[1], (ok ? 1.f : 0.f) * inv_rows);
+    if (part) {  // per-row terms; xent_sums_kernel reduces them in a fixed order (deterministic)
+      part[2 * row] = loss * inv_rows;
+      part[2 * row + 1] = (ok ? 1.f : 0.f) * inv_rows;
     }
+  }
+}
+
+// sums[0..1] = sum over rows of part[row][0..1], one block, fixed order.
+__global__ __launch_bounds__(256) void xent_sums_kernel(const float* __restrict__ part, int rows,
+                                                        float* __restrict__ sums) {
+  __shared__ float red[16];
+  float a = 0.f, b = 0.f;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    a += part[2 * r];
+    b += part[2 * r + 1];
+  }
+  a = block_sum(a, red);
+  b = block_sum(b, red + 8);
+  if (threadIdx.x == 0) {
+    sums[0] = a;
+    sums[1] = b;
   }
 }
 
@@ -81,23 +98,22 @@ __global__ __launch_bounds__(256) void xent_kernel(const T* __restrict__ logits,
 using namespace ttdk;
 
 // logits_dtype: 0 = fp32, 1 = bf16. label_dtype: 0 = int32, 1 = int64.
-// sums (optional, fp32[2]) receives mean loss and mean accuracy (zeroed here).
+// sums (optional, fp32[2]) receives mean loss and mean accuracy; `part` (fp32[2*rows], needed
+// with sums) holds the per-row terms, reduced in a fixed order (bitwise reproducible).
 TTDK_EXPORT int ttdk_sparse_xent(const void* logits, int logits_dtype, const void* labels, int label_dtype, int rows,
                                  int V, float grad_scale, float* loss_rows, void* dlogits, uint8_t* correct,
-                                 float* sums, hipStream_t st) {
-  if (sums) {
-    hipError_t e = hipMemsetAsync(sums, 0, 2 * sizeof(float), st);
-    if (e != hipSuccess) return e;
-  }
+                                 float* sums, float* part, hipStream_t st) {
+  if (sums && !part) return hipErrorInvalidValue;
   const float inv = 1.f / rows;
   dim3 g(rows), b(256);
 #define TTDK_X(T, L)                                                                                              \
   hipLaunchKernelGGL((xent_kernel<T, L>), g, b, 0, st, static_cast<const T*>(logits), static_cast<const L*>(labels), \
-                     V, grad_scale, loss_rows, static_cast<T*>(dlogits), correct, sums, inv)
+                     V, grad_scale, loss_rows, static_cast<T*>(dlogits), correct, sums ? part : nullptr, inv)
   if (logits_dtype == 0 && label_dtype == 0) TTDK_X(float, int32_t);
   else if (logits_dtype == 0) TTDK_X(float, int64_t);
   else if (label_dtype == 0) TTDK_X(bf16_t, int32_t);
   else TTDK_X(bf16_t, int64_t);
 #undef TTDK_X
+  if (sums) hipLaunchKernelGGL(xent_sums_kernel, dim3(1), dim3(256), 0, st, part, rows, sums);
   return hipGetLastError();
 }

@@ -336,6 +336,9 @@ class ResNet:
             r = self._convbn_fwd(c, inp, relu, residual=residual, x8=inp8, want8=want8)
             return r if want8 else (r[0], r[1], None)
 
+        from ..utils import tracing
+        fwd_range = tracing.range("resnet/forward")
+        fwd_range.__enter__()
         # ---- forward
         stem_shape = (N, (x.shape[1] + 2 * self.stem.pad - self.stem.k) // self.stem.stride + 1,
                       (x.shape[2] + 2 * self.stem.pad - self.stem.k) // self.stem.stride + 1, self.stem.cout)
@@ -376,6 +379,9 @@ class ResNet:
         pooled = K.avgpool_fwd(h)
         logits = G.gemm(pooled, P.c["predictions/kernel"], bias=P.var["predictions/bias"])
         sums, dlogits, _, _ = K.sparse_xent(logits, labels, grad_scale)
+        fwd_range.__exit__(None, None, None)
+        bwd_range = tracing.range("resnet/backward")
+        bwd_range.__enter__()
         # ---- backward
         G.gemm(pooled, dlogits, trans_a=True, out=P.g["predictions/kernel"])
         K.colsum(dlogits, out=P.g["predictions/bias"])
@@ -412,6 +418,7 @@ class ResNet:
             torch.cuda.current_stream().wait_stream(self._wgrad_stream)
             self._wgrad_stream = None
         self._side_keep = []
+        bwd_range.__exit__(None, None, None)
         self._grad_hook = None
         return sums
 

@@ -76,7 +76,7 @@ _SIGS = {
     "ttdk_maxpool_bwd_bnstat": [P, P, P, P, P, P, I, I, I, I, I, I, P],
     "ttdk_avgpool_bwd": [P, P, I, I, I, P],
     # xent.hip
-    "ttdk_sparse_xent": [P, I, P, I, I, I, F, P, P, P, P, P],
+    "ttdk_sparse_xent": [P, I, P, I, I, I, F, P, P, P, P, P, P],
     # optim.hip
     "ttdk_opt_sgd": [P, P, P, P, P, I, P, P, P, I, P],
     "ttdk_opt_adam": [P, P, P, P, P, P, I, P, P, P, I, P],
@@ -92,7 +92,8 @@ _SIGS = {
     "ttdk_transpose2d_f32": [P, P, I, I, P],
     "ttdk_bias_act_dropout_fwd": [P, P, P, L, I, I, F, U64, U64, I, P],
     "ttdk_bias_act_dropout_bwd": [P, P, P, P, L, I, I, F, U64, U64, I, P],
-    "ttdk_colsum": [P, L, I, P, I, I, P],
+    "ttdk_colsum": [P, L, I, P, I, I, P, P],
+    "ttdk_colsum_ws_floats": [L, I, I],
     "ttdk_add_bf16": [P, P, P, L, F, F, P],
     "ttdk_amax_bf16": [P, L, P, I, P],
     "ttdk_quant_fp8": [P, P, L, P, I, P],
@@ -109,7 +110,7 @@ def register(sigs: dict):
     _SIGS.update(sigs)
 
 
-_RESTYPE = {"ttdk_conv_dgrad_subpixel_stat_rows": c_longlong}
+_RESTYPE = {"ttdk_conv_dgrad_subpixel_stat_rows": c_longlong, "ttdk_colsum_ws_floats": c_longlong}
 
 
 def fn(name):

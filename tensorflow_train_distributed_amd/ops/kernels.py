@@ -217,12 +217,13 @@ def sparse_xent(logits, labels, grad_scale=None, *, want_grad=True, want_rows=Fa
     lab = labels if labels.dtype in (torch.int32, torch.int64) else labels.long()
     if sums is None:
         sums = torch.empty(2, dtype=torch.float32, device=logits.device)
+    part = torch.empty(2 * rows, dtype=torch.float32, device=logits.device)  # per-row terms (fixed-order sum)
     dl = torch.empty_like(logits) if want_grad else None
     lr = torch.empty(rows, dtype=torch.float32, device=logits.device) if want_rows else None
     corr = torch.empty(rows, dtype=torch.uint8, device=logits.device) if want_rows else None
     _lib.call("ttdk_sparse_xent", logits.data_ptr(), _DT[logits.dtype], lab.data_ptr(),
               0 if lab.dtype == torch.int32 else 1, rows, V, float(grad_scale), _p(lr), _p(dl), _p(corr),
-              sums.data_ptr(), _s())
+              sums.data_ptr(), part.data_ptr(), _s())
     return sums, dl, lr, corr
 
 
@@ -280,7 +281,9 @@ def colsum(x2d, out=None, beta=0):
     rows, C = x2d.shape
     if out is None:
         out = torch.empty(C, dtype=torch.float32, device=x2d.device)
-    _lib.call("ttdk_colsum", x2d.data_ptr(), rows, C, out.data_ptr(), int(beta), _DT[x2d.dtype], _s())
+    nws = _lib.query("ttdk_colsum_ws_floats", rows, C, _DT[x2d.dtype])
+    ws = torch.empty(max(1, nws), dtype=torch.float32, device=x2d.device) if nws else None
+    _lib.call("ttdk_colsum", x2d.data_ptr(), rows, C, out.data_ptr(), int(beta), _DT[x2d.dtype], _p(ws), _s())
     return out
 
 
