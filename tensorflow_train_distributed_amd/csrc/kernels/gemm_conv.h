@@ -136,6 +136,11 @@ struct KDense {  // element (row, k) at p[row * ld + k]; VEC: K % 8 == 0, ld % 8
 // Implicit-GEMM gather of a conv input patch, K-major: row = output pixel (n, p, q),
 // k = (r, s, c). DGRAD=false: forward conv, source pixel = p*stride - pad + r*dil.
 // DGRAD=true: data gradient, source pixel of dY = (p + pad - r*dil) / stride when divisible.
+// The k-steps run in order, so the tap (r, s) and channel group of a thread's 16-B chunk are
+// tracked incrementally (no integer divisions per k-step) whenever C % 64 == 0 (the chunk's
+// channel group advances by 8 and wraps into the next tap) or C divides 64 (the tap advances by
+// 64/C); per-row work is then two adds, two unsigned range tests and one 64-bit add on a
+// per-row base pointer. Other shapes (and strided dgrad) recompute with divisions.
 template <int ROWS, bool DGRAD>
 struct KConvGather {
   // x: source activations NHWC [Nimg, Hs, Ws, Cs]; (P, Q): pixel grid of the GEMM rows;
@@ -146,8 +151,11 @@ struct KConvGather {
   const bf16_t* x;
   int Hs, Ws, Cs, cch, S, sh, sw, dh, dw, K, c;
   int img[N], hb[N], wb[N];
+  const bf16_t* base[N];  // tap-(0,0) source pixel of each row (may point outside x; only valid taps load)
   bool ok[N];
   uint4 r[N];
+  int knext, c8, rr, ss, mode, dss, drr;
+  bool unit;
   __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
     x = P.x;
     Hs = P.Hs;
@@ -161,6 +169,12 @@ struct KConvGather {
     dw = P.dw;
     K = P.K;
     c = tid & 7;
+    unit = !DGRAD || (P.sh == 1 && P.sw == 1);
+    mode = !unit ? 0 : (cch % 8 == 0 ? 1 : (8 % cch == 0 ? 2 : 0));
+    const int dt = mode == 2 ? 8 / cch : 0;
+    dss = mode == 2 ? dt % S : 0;
+    drr = mode == 2 ? dt / S : 0;
+    knext = -1;
     const int pq = P.P * P.Q;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -177,29 +191,55 @@ struct KConvGather {
         hb[i] = p * P.sh - P.ph;
         wb[i] = q * P.sw - P.pw;
       }
+      base[i] = x + (static_cast<long long>(img[i] + hb[i]) * Ws + wb[i]) * Cs;
     }
   }
   __device__ __forceinline__ void load(int k0) {
-    const int kc = (k0 >> 3) + c;
-    const bool kin = kc * 8 < K;
-    const int tap = kc / cch, c8 = kc - tap * cch;
-    const int rr = tap / S, ss = tap - rr * S;
+    if (k0 != knext) {  // (re)derive this thread's chunk position (first step / generic shapes)
+      const int kc = (k0 >> 3) + c;
+      const int tap = kc / cch;
+      c8 = kc - tap * cch;
+      rr = tap / S;
+      ss = tap - rr * S;
+    }
+    const bool kin = ((k0 >> 3) + c) * 8 < K;
+    if (unit) {
+      const int dhh = DGRAD ? -rr * dh : rr * dh, dww = DGRAD ? -ss * dw : ss * dw;
+      const long long off = (static_cast<long long>(dhh) * Ws + dww) * Cs + c8 * 8;
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      int h, w;
-      bool v = ok[i] && kin;
-      if (DGRAD) {
-        const int hn = hb[i] - rr * dh, wn = wb[i] - ss * dw;
-        h = hn / sh;
-        w = wn / sw;
-        v = v && hn >= 0 && wn >= 0 && h * sh == hn && w * sw == wn;
-      } else {
-        h = hb[i] + rr * dh;
-        w = wb[i] + ss * dw;
-        v = v && h >= 0 && w >= 0;
+      for (int i = 0; i < N; ++i) {
+        const bool v = ok[i] && kin && static_cast<unsigned>(hb[i] + dhh) < static_cast<unsigned>(Hs) &&
+                       static_cast<unsigned>(wb[i] + dww) < static_cast<unsigned>(Ws);
+        r[i] = v ? ldg16(base[i] + off) : make_uint4(0, 0, 0, 0);
       }
-      v = v && h < Hs && w < Ws;
-      r[i] = v ? ldg16(x + ((static_cast<long long>(img[i] + h) * Ws + w) * Cs + c8 * 8)) : make_uint4(0, 0, 0, 0);
+    } else {  // strided data gradient: source pixel only where the stride divides
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int hn = hb[i] - rr * dh, wn = wb[i] - ss * dw;
+        const int h = hn / sh, w = wn / sw;
+        const bool v = ok[i] && kin && hn >= 0 && wn >= 0 && h * sh == hn && w * sw == wn && h < Hs && w < Ws;
+        r[i] = v ? ldg16(x + ((static_cast<long long>(img[i] + h) * Ws + w) * Cs + c8 * 8)) : make_uint4(0, 0, 0, 0);
+      }
+    }
+    // advance to the next k-step (k0 + BK = 8 chunks further)
+    if (mode == 1) {
+      c8 += 8;
+      if (c8 >= cch) {
+        c8 -= cch;
+        if (++ss == S) {
+          ss = 0;
+          ++rr;
+        }
+      }
+      knext = k0 + BK;
+    } else if (mode == 2) {
+      ss += dss;
+      rr += drr;
+      if (ss >= S) {
+        ss -= S;
+        ++rr;
+      }
+      knext = k0 + BK;
     }
   }
   __device__ __forceinline__ void store(char* lds, int tid) const {
@@ -274,7 +314,9 @@ struct MNDense {  // element (k, row) at p[k * ld + row]; VEC: rows % 8 == 0, ld
 };
 
 // Weight-gradient im2col operand, MN-major: k = output pixel (n, p, q), column = (r, s, c),
-// element = x[n, p*sh - ph + r*dh, q*sw - pw + s*dw, c].
+// element = x[n, p*sh - ph + r*dh, q*sw - pw + s*dw, c]. Each thread's k-rows advance by BK
+// per step; their (n, p, q) are carried forward with adds and wraps instead of two integer
+// divisions per chunk per step.
 template <int ROWS>
 struct MNConvGather {
   // x: conv input [Nimg, Hs, Ws, Cs]; (P, Q): output grid; rows = R*S*Cs; K = Nimg*P*Q.
@@ -284,7 +326,8 @@ struct MNConvGather {
   static constexpr int N = BK / KPP;
   static constexpr int BYTES = ROWS * BK * 2;
   const bf16_t* x;
-  int H, W, C, P, Q, pq, sh, sw, K, kr, cc, roff, soff;
+  int H, W, C, P, Q, pq, sh, sw, K, kr, cc, roff, soff, dq, dp, knext;
+  int nn[N], pp[N], qq[N];
   bool cok;
   uint4 r[N];
   __device__ __forceinline__ void init(const Params& Pm, int row0, int tid) {
@@ -300,6 +343,9 @@ struct MNConvGather {
     sh = Pm.sh;
     sw = Pm.sw;
     K = Pm.K;
+    dq = BK % Q;
+    dp = BK / Q;
+    knext = -1;
     const int col = row0 + cc * 8;
     cok = col < Pm.rows;
     const int cl = cok ? col : 0;
@@ -310,15 +356,36 @@ struct MNConvGather {
     x += c;
   }
   __device__ __forceinline__ void load(int k0) {
+    if (k0 != knext) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int k = k0 + kr + KPP * i;
+        nn[i] = k / pq;
+        const int rem = k - nn[i] * pq;
+        pp[i] = rem / Q;
+        qq[i] = rem - pp[i] * Q;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int k = k0 + kr + KPP * i;
-      const int n = k / pq, rem = k - n * pq;
-      const int p = rem / Q, q = rem - p * Q;
-      const int h = p * sh + roff, w = q * sw + soff;
-      const bool v = cok && k < K && h >= 0 && w >= 0 && h < H && w < W;
-      r[i] = v ? ldg16(x + (static_cast<long long>(n * H + h) * W + w) * C) : make_uint4(0, 0, 0, 0);
+      const int h = pp[i] * sh + roff, w = qq[i] * sw + soff;
+      const bool v = cok && k < K && static_cast<unsigned>(h) < static_cast<unsigned>(H) &&
+                     static_cast<unsigned>(w) < static_cast<unsigned>(W);
+      r[i] = v ? ldg16(x + (static_cast<long long>(nn[i] * H + h) * W + w) * C) : make_uint4(0, 0, 0, 0);
+      // advance this k-row by BK pixels
+      qq[i] += dq;
+      pp[i] += dp;
+      if (qq[i] >= Q) {
+        qq[i] -= Q;
+        ++pp[i];
+      }
+      while (pp[i] >= P) {
+        pp[i] -= P;
+        ++nn[i];
+      }
     }
+    knext = k0 + BK;
   }
   __device__ __forceinline__ void store(char* lds, int tid) const {
 #pragma unroll
@@ -978,6 +1045,8 @@ struct OpWgradMN {
   int H, W, C, pq, Q, sh, sw;
   int krow[2][G], roff[2][G], soff[2][G], cc[2][G];
   bool cok[2][G];
+  // (incremental pixel tracking as in MNConvGather was tried here: the extra state spilled this
+  // register-bound 256-row kernel to scratch and doubled its time, so it keeps the divisions)
   __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
     x = static_cast<const char*>(P.x);
     H = P.Hs; W = P.Ws; C = P.Cs; pq = P.P * P.Q; Q = P.Q; sh = P.sh; sw = P.sw;
