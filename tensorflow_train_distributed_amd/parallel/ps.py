@@ -473,3 +473,50 @@ def current_device_setter() -> Optional[DeviceSetter]:
         if isinstance(s, DeviceSetter):
             return s
     return None
+
+
+# ------------------------------------------------------------------ tf-named views of the PS primitives
+class TokenQueue:
+    """The SyncReplicas token queue on parameter-server task 0 (tf.FIFOQueue of int64 tokens,
+    shared name `sync_token_q`, distribute_training.py:144-148 via SyncReplicasOptimizer):
+    enqueue_many(n, value) / dequeue() (blocks) / close() (wakes blocked dequeues with
+    OutOfRangeError) / size()."""
+
+    name = "sync_token_q"
+
+    def __init__(self, client: PSClient):
+        self.client = client
+
+    def enqueue_many(self, n: int, value: int):
+        self.client.enqueue_tokens(int(n), int(value))
+
+    def dequeue(self) -> int:
+        return self.client.dequeue_token()
+
+    def close(self, cancel_pending_enqueues: bool = False):
+        self.client.close_queue()
+
+    def size(self) -> int:
+        return self.client.stats(0)["queue"]
+
+
+class ConditionalAccumulatorSet:
+    """The per-variable ConditionalAccumulators of SyncReplicasOptimizer (one per trainable
+    variable, on the variable's PS task): apply_grad drops gradients whose local_step is older
+    than the accumulators' global step; take_apply waits for `num_required` fresh gradients,
+    applies their mean with GradientDescent, bumps the global step and enqueues tokens."""
+
+    def __init__(self, client: PSClient):
+        self.client = client
+
+    def apply_grad(self, local_step: int, grads: Dict[str, np.ndarray]) -> int:
+        return self.client.accum_apply(int(local_step), grads)
+
+    def set_global_step(self, step: int):
+        self.client.set_accum_step(int(step))
+
+    def take_apply(self, num_required: int, lr: float, tokens_per_step: int) -> int:
+        return self.client.take_apply(int(num_required), float(lr), int(tokens_per_step))
+
+    def num_dropped(self) -> int:
+        return self.client.stats(0)["dropped"]

@@ -16,5 +16,7 @@ from .optimizers import (AdamOptimizer, AdamWOptimizer, GradientDescentOptimizer
                          cosine_decay, exponential_decay, polynomial_decay)
 from .session import (ChiefSessionCreator, ConfigProto, Coordinator, MonitoredSession, MonitoredTrainingSession,
                       Scaffold, SessionConfig, SingularMonitoredSession, WorkerSessionCreator)
+from .queue_runner import QUEUE_RUNNERS, QueueRunner, SessionManager, add_queue_runner, start_queue_runners
+from ..summary import FileWriterCache as SummaryWriterCache
 from ..parallel.cluster import ClusterSpec
 from ..parallel.ps import Server, replica_device_setter
