@@ -54,6 +54,7 @@ def build_resnet(args, dev, rank, world):
         reducer.finish()
         opt.step()
         return sums
+    step.params = model.params
 
     info = {
         "metric": "images/sec (whole node) ResNet-50 %s MirroredStrategy" % args.precision,
@@ -91,6 +92,7 @@ def build_bert(args, dev, rank, world):
         reducer.finish()
         opt.step()
         return sums
+    step.params = model.params
 
     info = {
         "metric": "sequences/sec (whole node) BERT-Large seq%d bf16 MirroredStrategy" % S,
@@ -123,10 +125,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; TTD_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs
+    # (ranks share devices round-robin), the production path is RCCL ("nccl")
+    backend = os.environ.get("TTD_DIST_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank % ndev)
+    dev = torch.device("cuda", local_rank % ndev)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     build = build_resnet if args.model == "resnet50" else build_bert
     step, B, info = build(args, dev, rank, world)
@@ -166,12 +175,28 @@ def main():
     elapsed = float(t.item())
     sums = step() if graph is None else out
     loss = float(sums[0])
+    # replicas must hold identical weights after synchronous data-parallel steps
+    params = getattr(step, "params", None)
+    replicas_in_sync = None
+    if world > 1 and params is not None:
+        # BN moving statistics are per replica (TF SyncOnRead): average them as a checkpoint
+        # save would, then every variable must be bit-identical across ranks
+        from tensorflow_train_distributed_amd.parallel.collective import sync_on_read_mean_
+        sync_on_read_mean_(params)
+        chk = params.master.double().sum().reshape(1)
+        lo, hi = chk.clone(), chk.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        replicas_in_sync = bool(lo.item() == hi.item())
     ms = elapsed / args.steps * 1e3
     rate = B * world * args.steps / elapsed
     if rank == 0:
         cfg = dict(info["config"])
         cfg["hipgraph"] = bool(use_graph)
         cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+        if replicas_in_sync is not None:
+            cfg["replicas_in_sync"] = replicas_in_sync
+            cfg["dist_backend"] = backend
         cfg["final_loss"] = loss
         print(json.dumps({
             "metric": info["metric"],

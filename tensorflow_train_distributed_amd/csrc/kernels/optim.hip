@@ -118,14 +118,17 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const 
   }
 }
 
-// LAMB phase 1: update direction u = m_hat/(sqrt(v_hat)+eps) + wd*w into `u`, and per-segment
-// sums of w^2 and u^2 (float atomics, one per block and quantity).
+// LAMB phase 1: update direction u = m_hat/(sqrt(v_hat)+eps) + wd*w into `u`, and per-CHUNK
+// sums of w^2 and u^2 (chunk_norms[2*chunk]); lamb_segnorm_kernel folds the chunks of each
+// variable in a fixed order. No float atomics: every replica of a data-parallel job computes
+// bit-identical trust ratios from bit-identical all-reduced gradients, so the replicas never
+// drift apart.
 __global__ __launch_bounds__(256) void lamb_phase1_kernel(const float* __restrict__ w, const float* __restrict__ g,
                                                           float* __restrict__ m, float* __restrict__ v,
                                                           float* __restrict__ u, const Chunk* __restrict__ chunks,
                                                           const float* __restrict__ seg_wd,
                                                           const float* __restrict__ hyper,
-                                                          const float* __restrict__ sumsq, float* __restrict__ seg_norms) {
+                                                          const float* __restrict__ sumsq, float* __restrict__ chunk_norms) {
   __shared__ float red[16];
   const Chunk ch = chunks[blockIdx.x];
   const float b1 = hyper[kMu], b2 = hyper[kBeta2], eps = hyper[kEps];
@@ -148,8 +151,40 @@ __global__ __launch_bounds__(256) void lamb_phase1_kernel(const float* __restric
   sw = block_sum(sw, red);
   su = block_sum(su, red + 8);
   if (threadIdx.x == 0) {
-    atomicAdd(&seg_norms[2 * ch.seg], sw);
-    atomicAdd(&seg_norms[2 * ch.seg + 1], su);
+    chunk_norms[2 * blockIdx.x] = sw;
+    chunk_norms[2 * blockIdx.x + 1] = su;
+  }
+}
+
+// seg_norms[2*seg + {0,1}] = sum of chunk_norms over the (consecutive) chunks of segment `seg`
+// (block per segment; the chunk range is found by binary search on the sorted seg ids).
+__global__ __launch_bounds__(256) void lamb_segnorm_kernel(const Chunk* __restrict__ chunks, int n_chunks,
+                                                           const float* __restrict__ chunk_norms,
+                                                           float* __restrict__ seg_norms) {
+  __shared__ float red[16];
+  const int seg = blockIdx.x;
+  int lo = 0, hi = n_chunks;  // first chunk with seg >= this
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (chunks[mid].seg < seg) lo = mid + 1; else hi = mid;
+  }
+  const int first = lo;
+  hi = n_chunks;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (chunks[mid].seg <= seg) lo = mid + 1; else hi = mid;
+  }
+  const int last = lo;
+  float sw = 0.f, su = 0.f;
+  for (int c = first + threadIdx.x; c < last; c += blockDim.x) {
+    sw += chunk_norms[2 * c];
+    su += chunk_norms[2 * c + 1];
+  }
+  sw = block_sum(sw, red);
+  su = block_sum(su, red + 8);
+  if (threadIdx.x == 0) {
+    seg_norms[2 * seg] = sw;
+    seg_norms[2 * seg + 1] = su;
   }
 }
 
@@ -169,14 +204,26 @@ __global__ __launch_bounds__(256) void lamb_phase2_kernel(float* __restrict__ w,
   }
 }
 
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n, float* __restrict__ out) {
+// Global sum of squares (gradient clipping): per-block partials, then one block folds them in
+// a fixed order (deterministic, no atomics).
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n,
+                                                    float* __restrict__ partial) {
   __shared__ float red[16];
   float s = 0.f;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<long long>(gridDim.x) * blockDim.x)
     s += x[i] * x[i];
   s = block_sum(s, red);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partial, int n,
+                                                           float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) *out = s;
 }
 
 // In-graph learning-rate schedule + step counter.
@@ -239,27 +286,27 @@ TTDK_EXPORT int ttdk_opt_adam(float* w, const float* g, float* m, float* v, bf16
   return hipGetLastError();
 }
 
-// u: scratch of the flat size; seg_norms: fp32[2*n_segments] (zeroed here).
+// u: scratch of the flat size; seg_norms: fp32[2*n_segments]; chunk_norms: fp32[2*n_chunks].
 TTDK_EXPORT int ttdk_opt_lamb(float* w, const float* g, float* m, float* v, float* u, bf16_t* wbf, const void* chunks,
                               int n_chunks, int n_segments, const float* seg_wd, const float* hyper, const float* sumsq,
-                              float* seg_norms, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(seg_norms, 0, sizeof(float) * 2 * n_segments, st);
-  if (e != hipSuccess) return e;
+                              float* seg_norms, float* chunk_norms, hipStream_t st) {
+  if (!chunk_norms) return hipErrorInvalidValue;
   const Chunk* c = static_cast<const Chunk*>(chunks);
   hipLaunchKernelGGL(lamb_phase1_kernel, dim3(n_chunks), dim3(256), 0, st, w, g, m, v, u, c, seg_wd, hyper, sumsq,
-                     seg_norms);
+                     chunk_norms);
+  hipLaunchKernelGGL(lamb_segnorm_kernel, dim3(n_segments), dim3(256), 0, st, c, n_chunks, chunk_norms, seg_norms);
   hipLaunchKernelGGL(lamb_phase2_kernel, dim3(n_chunks), dim3(256), 0, st, w, u, wbf, c, hyper, seg_norms);
   return hipGetLastError();
 }
 
-// out (fp32 scalar) = sum x^2 (zeroed here).
-TTDK_EXPORT int ttdk_sumsq(const float* x, long long n, float* out, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(out, 0, sizeof(float), st);
-  if (e != hipSuccess) return e;
+// out (fp32 scalar) = sum x^2; `partial`: scratch of >= 2048 floats.
+TTDK_EXPORT int ttdk_sumsq(const float* x, long long n, float* out, float* partial, hipStream_t st) {
+  if (!partial) return hipErrorInvalidValue;
   long long blocks = (n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(static_cast<int>(blocks)), dim3(256), 0, st, x, n, out);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(static_cast<int>(blocks)), dim3(256), 0, st, x, n, partial);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, partial, static_cast<int>(blocks), out);
   return hipGetLastError();
 }
 

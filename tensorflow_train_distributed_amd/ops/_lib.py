@@ -80,8 +80,8 @@ _SIGS = {
     # optim.hip
     "ttdk_opt_sgd": [P, P, P, P, P, I, P, P, P, I, P],
     "ttdk_opt_adam": [P, P, P, P, P, P, I, P, P, P, I, P],
-    "ttdk_opt_lamb": [P, P, P, P, P, P, P, I, I, P, P, P, P, P],
-    "ttdk_sumsq": [P, L, P, P],
+    "ttdk_opt_lamb": [P, P, P, P, P, P, P, I, I, P, P, P, P, P, P],
+    "ttdk_sumsq": [P, L, P, P, P],
     "ttdk_lr_schedule": [P, P, I, P, F, F, I, P],
     # elementwise.hip
     "ttdk_f32_to_bf16": [P, P, L, P],

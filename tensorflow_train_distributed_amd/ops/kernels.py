@@ -320,5 +320,6 @@ def dequant_fp8(q, scale, e5m2=False, out=None):
 def sumsq(x, out=None):
     if out is None:
         out = torch.empty(1, dtype=torch.float32, device=x.device)
-    _lib.call("ttdk_sumsq", x.data_ptr(), x.numel(), out.data_ptr(), _s())
+    partial = torch.empty(2048, dtype=torch.float32, device=x.device)  # per-block partials (fixed-order fold)
+    _lib.call("ttdk_sumsq", x.data_ptr(), x.numel(), out.data_ptr(), partial.data_ptr(), _s())
     return out

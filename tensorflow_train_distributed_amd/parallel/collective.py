@@ -86,6 +86,12 @@ class BucketedAllReducer:
             self._launch(self._next)
             self._next += 1
 
+    def sync_on_read(self):
+        """TF SyncOnRead(MEAN) semantics for the non-trainable variables (BatchNorm moving
+        mean/variance): every replica updates its own copy from its own batch; reading them in
+        cross-replica context (checkpoint save, evaluation) first averages them across replicas."""
+        sync_on_read_mean_(self.flat, self.group)
+
     def finish(self):
         while self._next < len(self.buckets):
             self._launch(self._next)
@@ -117,3 +123,21 @@ def broadcast_flat_(flat, src: int = 0, group=None):
         return
     dist.broadcast(flat.master, src=src, group=group)
     flat.refresh_compute()
+
+
+def sync_on_read_mean_(flat, group=None):
+    """Average the non-trainable variables of a FlatParams store across replicas (one packed
+    all-reduce; see BucketedAllReducer.sync_on_read)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    names = [s.name for s in flat.specs if not s.trainable]
+    if not names:
+        return
+    packed = torch.cat([flat.var[n].reshape(-1) for n in names])
+    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+    packed /= dist.get_world_size(group)
+    o = 0
+    for n in names:
+        k = flat.var[n].numel()
+        flat.var[n].copy_(packed[o:o + k].view_as(flat.var[n]))
+        o += k

@@ -366,12 +366,14 @@ class FlatLAMB(FlatOptimizer):
         if self.is_cuda:
             from ..ops import _lib
             chunks, n, _ = self.p.chunk_table()
+            if getattr(self, "_chunk_norms", None) is None or self._chunk_norms.numel() < 2 * n:
+                self._chunk_norms = torch.empty(2 * max(1, n), dtype=torch.float32, device=self.p.device)
             _lib.call("ttdk_opt_lamb", self.p.master.data_ptr(), self.p.grad.data_ptr(), self.m.data_ptr(),
                       self.v.data_ptr(), self.u.data_ptr(),
                       self.p.compute.data_ptr() if self.p.compute is not None else None, chunks.data_ptr(), n,
                       len(self.p.specs), self.seg_wd().data_ptr(), self.hyper.data_ptr(),
                       self._sumsq.data_ptr() if self.max_grad_norm > 0 else None, self.seg_norms.data_ptr(),
-                      _lib.stream())
+                      self._chunk_norms.data_ptr(), _lib.stream())
             return
         with torch.no_grad():
             lr = float(self.hyper[H_LR])

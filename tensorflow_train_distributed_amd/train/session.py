@@ -199,6 +199,10 @@ class _CoreSession:
         return Saver(items, extra=extra)
 
     def save_checkpoint(self, saver, basename, step):
+        for op in self.train_ops:  # Mirrored: BN moving statistics are SyncOnRead(MEAN)
+            red = getattr(op, "reducer", None)
+            if red is not None:
+                red.sync_on_read()
         if self.ps_ops:
             n = self.client.n_ps
             return saver.save(None, basename, global_step=step,
