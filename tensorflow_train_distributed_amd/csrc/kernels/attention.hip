@@ -179,20 +179,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       m[qb] = mnew;
       float rs = 0.f;
       const int qrow = q0 + qb * 16 + i16;
+      const uint32_t rterm = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) : 0u;
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb) {
+        uint32_t hp[2] = {0u, 0u};
+        if constexpr (DROP) {  // keys kbase + kb*16 + 4g + {0,1 | 2,3}: two key pairs
+          const uint32_t pair0 = static_cast<uint32_t>(kbase + kb * 16 + 4 * g) >> 1;
+          hp[0] = attn_pair_hash(key, rterm, pair0);
+          hp[1] = attn_pair_hash(key, rterm, pair0 + 1);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float p = fast_exp2(s[qb][kb][i] - msub);
           rs += p;
           float pd = p;
-          if constexpr (DROP) {
-            const unsigned long long idx =
-                (static_cast<unsigned long long>(bh) * P.S + qrow) * P.S + (kbase + kb * 16 + 4 * g + i);
-            pd = drop_keep(key, idx, P.drop_thr) ? p : 0.f;
-          }
+          if constexpr (DROP) pd = attn_keep(hp[i >> 1], static_cast<uint32_t>(i), P.drop_thr) ? p : 0.f;
           s[qb][kb][i] = pd;
         }
+      }
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
       l[qb] = l[qb] * alpha + rs;
@@ -356,9 +360,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
             float dpv = dp[qb][kb][i];
             float pd = p;
             if constexpr (DROP) {
-              const unsigned long long idx =
-                  (static_cast<unsigned long long>(bh) * P.S + (qt * KT + ql)) * P.S + kcol;
-              const bool kp = drop_keep(key, idx, P.drop_thr);
+              const uint32_t h = attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * P.S + qt * KT + ql)),
+                                                static_cast<uint32_t>(kcol) >> 1);
+              const bool kp = attn_keep(h, static_cast<uint32_t>(kcol), P.drop_thr);
               pd = kp ? p * P.drop_scale : 0.f;
               dpv = kp ? dpv * P.drop_scale : 0.f;
             }
@@ -483,19 +487,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const int qrow = q0 + qb * 16 + i16;
+      const uint32_t rterm = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) : 0u;
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb) {
+        uint32_t hp[2] = {0u, 0u};
+        if constexpr (DROP) {
+          const uint32_t pair0 = static_cast<uint32_t>(kbase + kb * 16 + 4 * g) >> 1;
+          hp[0] = attn_pair_hash(key, rterm, pair0);
+          hp[1] = attn_pair_hash(key, rterm, pair0 + 1);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int kcol = kbase + kb * 16 + 4 * g + i;
           const float p = kcol < len ? fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2[qb]) : 0.f;
           float dpv = dp[qb][kb][i];
-          if constexpr (DROP) {
-            const unsigned long long idx = (static_cast<unsigned long long>(bh) * P.S + qrow) * P.S + kcol;
-            dpv = drop_keep(key, idx, P.drop_thr) ? dpv * P.drop_scale : 0.f;
-          }
+          if constexpr (DROP) dpv = attn_keep(hp[i >> 1], static_cast<uint32_t>(i), P.drop_thr) ? dpv * P.drop_scale : 0.f;
           sc[qb][kb][i] = p * (dpv - del[qb]);
         }
+      }
       sfr[qb][0] = pack_frag(sc[qb][0], sc[qb][1]);
       sfr[qb][1] = pack_frag(sc[qb][2], sc[qb][3]);
     }
@@ -533,8 +542,9 @@ AttnParams make_params(int B, int H, int S, const int* seqlen, float p_drop, con
   P.seqlen = seqlen;
   P.scale = 0.125f;  // 1/sqrt(64)
   P.scale_log2 = 0.125f * 1.4426950408889634f;
-  P.drop_thr = drop_threshold(p_drop);
-  P.drop_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  P.drop_thr = drop_threshold16(p_drop);
+  // unbiased for the keep probability the 16-bit threshold actually realises
+  P.drop_scale = p_drop > 0.f ? static_cast<float>(65536.0 / (65536.0 - static_cast<double>(P.drop_thr))) : 1.f;
   P.rng = rng;
   P.site = site;
   return P;

@@ -88,6 +88,25 @@ __device__ __forceinline__ bool drop_keep(uint32_t key, unsigned long long idx, 
   return h >= thr;
 }
 
+// Attention-probability dropout: one hash per PAIR of adjacent keys of a query row, each key
+// taking one 16-bit half (keep iff half >= thr16 = floor(p * 2^16)). The hash input is
+// rowid * C1 + (key >> 1) * C2 with rowid = (b*H + h)*S + q, so a lane derives its row term
+// once and pays one fmix32 per two probabilities (the per-element 64-bit index + hash made
+// the dropout variant of the kernels VALU-bound). ops/transformer.attention_keep_mask mirrors it.
+__device__ __forceinline__ uint32_t attn_row_term(uint32_t rowid) { return rowid * 0x9E3779B1u; }
+__device__ __forceinline__ uint32_t attn_pair_hash(uint32_t key, uint32_t row_term, uint32_t pair) {
+  return fmix32(key ^ (row_term + pair * 0x7FEB352Du));
+}
+__device__ __forceinline__ bool attn_keep(uint32_t h, uint32_t key_index, uint32_t thr16) {
+  return ((key_index & 1u) ? (h >> 16) : (h & 0xffffu)) >= thr16;
+}
+
+inline uint32_t drop_threshold16(float p) {
+  if (p <= 0.f) return 0u;
+  if (p >= 1.f) return 0x10000u;
+  return static_cast<uint32_t>(static_cast<double>(p) * 65536.0);
+}
+
 inline uint32_t drop_threshold(float p) {
   if (p <= 0.f) return 0u;
   if (p >= 1.f) return 0xffffffffu;

@@ -204,3 +204,24 @@ def keep_mask(seed: int, step: int, site: int, p: float, idx) -> np.ndarray:
     mixed = ((lo * np.uint64(0x9E3779B1)) + (hi * np.uint64(0x7FEB352D))) & M32
     h = _fmix32(key ^ mixed)
     return h >= np.uint64(drop_threshold(p))
+
+
+def attention_keep_mask(seed: int, step: int, site: int, p: float, B: int, H: int, S: int) -> np.ndarray:
+    """Keep mask [B, H, S(query), S(key)] of the attention-probability dropout (mirror of
+    tile_common.h attn_pair_hash / attn_keep: one hash per pair of adjacent keys, 16-bit halves)."""
+    key = np.uint64(drop_key(seed, step, site))
+    thr = 0 if p <= 0 else (0x10000 if p >= 1 else int(float(np.float32(p)) * 65536.0))
+    rowid = np.arange(B * H * S, dtype=np.uint64).reshape(B * H, S, 1)
+    k = np.arange(S, dtype=np.uint64).reshape(1, 1, S)
+    mixed = ((rowid * np.uint64(0x9E3779B1)) + ((k >> np.uint64(1)) * np.uint64(0x7FEB352D))) & M32
+    h = _fmix32(key ^ mixed)
+    half = np.where((k & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    return (half >= np.uint64(thr)).reshape(B, H, S, S)
+
+
+def attention_drop_scale(p: float) -> float:
+    """The kernels' 1/keep-probability for the realised 16-bit threshold."""
+    if p <= 0:
+        return 1.0
+    thr = int(float(np.float32(p)) * 65536.0)
+    return 65536.0 / (65536.0 - thr)

@@ -33,14 +33,22 @@ def _attn_ref(q, k, v, B, H, S, seqlen=None, keep=None, p=0.0):
         sc = sc.masked_fill(~m[:, None, None, :], float("-inf"))
     pr = sc.softmax(-1)
     if keep is not None:
-        pr = pr * keep / (1 - p)
+        pr = pr * keep * T.attention_drop_scale(p)
     return (pr @ vh).transpose(1, 2).reshape(B * S, H * 64)
 
 
 def _keep_tensor(rng_state, site, p, B, H, S, device):
     seed, step = rng_state
-    idx = np.arange(B * H * S * S, dtype=np.int64)
-    return torch.from_numpy(T.keep_mask(seed, step, site, p, idx).reshape(B, H, S, S)).float().to(device)
+    return torch.from_numpy(T.attention_keep_mask(seed, step, site, p, B, H, S)).float().to(device)
+
+
+def test_attention_dropout_pair_hash_statistics():
+    keep = T.attention_keep_mask(1234, 7, 3, 0.1, 2, 4, 256)
+    assert abs(keep.mean() - 0.9) < 0.005
+    # the two keys of a pair use different halves of one hash: not correlated
+    a, b = keep[..., 0::2].ravel(), keep[..., 1::2].ravel()
+    assert abs(np.mean(a & b) - np.mean(a) * np.mean(b)) < 0.01
+    assert abs(T.attention_drop_scale(0.1) - 1 / 0.9) < 1e-4
 
 
 @gpu
