@@ -467,9 +467,32 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
                                          int N, bool vst, bool vres, const float (&bias8)[8], float (&s8)[8],
                                          float (&q8)[8], float (&r8)[8]) {
   constexpr int NR = (BM + RPP - 1) / RPP;
-  constexpr int EB = !PF ? 1 : (NR < 8 ? NR : 8);
+  constexpr int EB = !PF ? 1 : (NR < 8 ? NR : 8);  // 16 spills (measured +12 % step time)
   bf16_t* out = static_cast<bf16_t*>(E.out);
   if (n >= N) return;
+  if (!PF && !E.bias && !E.residual && !E.aux && E.act == kActNone && !E.remap && vst) {
+    // plain store (+ BN statistics): the staged tile already holds the rounded bf16 result, so
+    // each 16-B chunk goes LDS -> global untouched (no unpack / bias / repack per element) and
+    // the row pointer advances by a constant instead of a 64-bit multiply per row
+    bf16_t* op = out + static_cast<long long>(m0 + r0) * E.ldo + n;
+    const long long step = static_cast<long long>(RPP) * E.ldo;
+    const int rmax = min(BM, M - m0);
+#pragma unroll 4
+    for (int r = r0; r < rmax; r += RPP, op += step) {
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16);
+      *reinterpret_cast<uint4*>(op) = v;
+      if (E.stat) {
+        float sv[8];
+        unpack8(v, sv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s8[j] += sv[j];
+          q8[j] += sv[j] * sv[j];
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll 1
   for (int rb = r0; rb < BM; rb += RPP * EB) {
     uint4 pres[EB], pold[EB], pby[EB], pby2[EB];
