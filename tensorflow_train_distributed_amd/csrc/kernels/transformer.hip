@@ -101,90 +101,162 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 // ds = dL/ds (goes to the residual branch), dx = ds * mask_in * scale_in (the sub-layer
 // output gradient; null when there is no input dropout). part: [gridDim.x][2][H] partial
 // (dgamma, dbeta) rows.
-template <int NV>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
-                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-                                                     const float* __restrict__ gamma, bf16_t* __restrict__ ds_out,
-                                                     bf16_t* __restrict__ dx_out, float* __restrict__ part, int rows,
-                                                     int rows_per_block, DropSpec dsp) {
-  constexpr int H = NV * 512;
-  __shared__ float red[4][2][H / 4];  // reduced in 4 column quarters to bound LDS
+// Each row needs two dependent wave reductions between its loads and its stores, so one wave
+// per SIMD working one row at a time (the first version) was latency-bound at ~0.6 TB/s.
+// H = 512: 16 waves per block (4 per SIMD, < 128 VGPRs), one row each; H >= 1024: 8 waves
+// per block (2 per SIMD, ~230 VGPRs at H = 1024) with two rows in flight per wave and their
+// reductions interleaved (16 x 1 would spill at H = 1024).
+
+__device__ __forceinline__ void wave_sum4(float& a, float& b, float& c, float& d) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c += __shfl_xor(c, o, 64);
+    d += __shfl_xor(d, o, 64);
+  }
+}
+
+template <int NV, int W, int U>  // W waves per block, U rows in flight per wave
+__global__ __launch_bounds__(W * 64) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+                                                             const float* __restrict__ mean_in,
+                                                             const float* __restrict__ rstd_in,
+                                                             const float* __restrict__ gamma, bf16_t* __restrict__ ds_out,
+                                                             bf16_t* __restrict__ dx_out, float* __restrict__ part,
+                                                             int rows, int rows_per_block, DropSpec dsp) {
+  constexpr int H = NV * 512, CH = 512;  // a wave's columns for one v: lane * 8 + j
+  __shared__ __attribute__((aligned(16))) float red[W][2][CH];  // 64 KB
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t kin = dsp.thr_in ? drop_key(dsp.rng, dsp.site_in) : 0u;
   const uint32_t kout = dsp.thr_out ? drop_key(dsp.rng, dsp.site_out) : 0u;
-  float dg[NV][8], db[NV][8], gm[NV][8];
+  float dg[NV][8], db[NV][8];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    *reinterpret_cast<f32x4_t*>(gm[v]) = *reinterpret_cast<const f32x4_t*>(gamma + (lane + 64 * v) * 8);
-    *reinterpret_cast<f32x4_t*>(gm[v] + 4) = *reinterpret_cast<const f32x4_t*>(gamma + (lane + 64 * v) * 8 + 4);
+  for (int v = 0; v < NV; ++v)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[v][j] = db[v][j] = 0.f;
-  }
+  // gamma is re-read (L1/L2-resident) where used rather than held in 8*NV VGPRs
+  auto load_g = [&](int c, float (&gm)[8]) {
+    *reinterpret_cast<f32x4_t*>(gm) = *reinterpret_cast<const f32x4_t*>(gamma + c);
+    *reinterpret_cast<f32x4_t*>(gm + 4) = *reinterpret_cast<const f32x4_t*>(gamma + c + 4);
+  };
   const long long r0 = static_cast<long long>(blockIdx.x) * rows_per_block;
   const long long r1 = min(static_cast<long long>(rows), r0 + rows_per_block);
-  for (long long row = r0 + w; row < r1; row += 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float g[NV][8], xh[NV][8];
-    float c1 = 0.f, c2 = 0.f;
+  // dy after the output dropout (recomputed in both passes; the mask is a hash, not stored)
+  auto load_d = [&](const uint4& pk, long long row, int c, float (&d)[8]) {
+    unpack8(pk, d);
+    if (dsp.thr_out) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = (lane + 64 * v) * 8;
-      float d[8], sv[8];
-      unpack8(ldg16(dy + row * H + c), d);
-      unpack8(ldg16(s + row * H + c), sv);
+      for (int j = 0; j < 8; ++j)
+        d[j] = drop_keep(kout, static_cast<unsigned long long>(row) * H + c + j, dsp.thr_out) ? d[j] * dsp.scale_out : 0.f;
+    }
+  };
+#pragma unroll 1
+  for (long long ra = r0 + w; ra < r1; ra += U * W) {
+    long long rw[U];
+    bool has[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (dsp.thr_out)
-          d[j] = drop_keep(kout, static_cast<unsigned long long>(row) * H + c + j, dsp.thr_out) ? d[j] * dsp.scale_out
-                                                                                                 : 0.f;
-        xh[v][j] = (sv[j] - mean) * rstd;
-        dg[v][j] += d[j] * xh[v][j];
-        db[v][j] += d[j];
-        g[v][j] = d[j] * gm[v][j];
-        c1 += g[v][j];
-        c2 += g[v][j] * xh[v][j];
+    for (int u = 0; u < U; ++u) {
+      rw[u] = ra + u * W;
+      has[u] = rw[u] < r1;
+    }
+    uint4 pd[U][NV], ps[U][NV];
+    float mean[U], rstd[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int c = (lane + 64 * v) * 8;
+        pd[u][v] = has[u] ? ldg16(dy + rw[u] * H + c) : make_uint4(0, 0, 0, 0);
+        ps[u][v] = has[u] ? ldg16(s + rw[u] * H + c) : make_uint4(0, 0, 0, 0);
+      }
+      mean[u] = has[u] ? mean_in[rw[u]] : 0.f;
+      rstd[u] = has[u] ? rstd_in[rw[u]] : 0.f;
+    }
+    float c1[U], c2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c1[u] = c2[u] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int c = (lane + 64 * v) * 8;
+        float d[8], sv[8], gm[8];
+        load_d(pd[u][v], rw[u], c, d);
+        unpack8(ps[u][v], sv);
+        load_g(c, gm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (sv[j] - mean[u]) * rstd[u];
+          dg[v][j] += d[j] * xh;  // a missing second row has d == 0
+          db[v][j] += d[j];
+          const float g = d[j] * gm[j];
+          c1[u] += g;
+          c2[u] += g * xh;
+        }
+      }
+    // opaque to the optimiser: pass 2 re-derives d / x-hat from the packed rows instead of
+    // keeping pass 1's unpacked floats alive across the reductions (which spilled)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        asm volatile("" : "+v"(pd[u][v].x), "+v"(pd[u][v].y), "+v"(pd[u][v].z), "+v"(pd[u][v].w));
+        asm volatile("" : "+v"(ps[u][v].x), "+v"(ps[u][v].y), "+v"(ps[u][v].z), "+v"(ps[u][v].w));
+      }
+    if constexpr (U == 2) {
+      wave_sum4(c1[0], c2[0], c1[1], c2[1]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        c1[u] = wave_sum(c1[u]);
+        c2[u] = wave_sum(c2[u]);
       }
     }
-    c1 = wave_sum(c1) * (1.f / H);
-    c2 = wave_sum(c2) * (1.f / H);
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = (lane + 64 * v) * 8;
-      float o[8];
+    for (int u = 0; u < U; ++u) {
+      if (!has[u]) break;
+      const float m1 = c1[u] * (1.f / H), m2 = c2[u] * (1.f / H);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = rstd * (g[v][j] - c1 - xh[v][j] * c2);
-      *reinterpret_cast<uint4*>(ds_out + row * H + c) = pack8(o);
-      if (dx_out) {
-        if (dsp.thr_in) {
+      for (int v = 0; v < NV; ++v) {
+        const int c = (lane + 64 * v) * 8;
+        float d[8], sv[8], o[8], gm[8];
+        load_d(pd[u][v], rw[u], c, d);
+        unpack8(ps[u][v], sv);
+        load_g(c, gm);
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            o[j] = drop_keep(kin, static_cast<unsigned long long>(row) * H + c + j, dsp.thr_in) ? o[j] * dsp.scale_in
-                                                                                                 : 0.f;
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (sv[j] - mean[u]) * rstd[u];
+          o[j] = rstd[u] * (d[j] * gm[j] - m1 - xh * m2);
         }
-        *reinterpret_cast<uint4*>(dx_out + row * H + c) = pack8(o);
+        *reinterpret_cast<uint4*>(ds_out + rw[u] * H + c) = pack8(o);
+        if (dx_out) {
+          if (dsp.thr_in) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              o[j] = drop_keep(kin, static_cast<unsigned long long>(rw[u]) * H + c + j, dsp.thr_in) ? o[j] * dsp.scale_in
+                                                                                                    : 0.f;
+          }
+          *reinterpret_cast<uint4*>(dx_out + rw[u] * H + c) = pack8(o);
+        }
       }
     }
   }
-  // block reduce of (dg, db) over the 4 waves, one column quarter at a time
+  // block reduce of (dg, db) over the W waves in fixed order, one 512-column slice (v) at a time
   float* out = part + static_cast<long long>(blockIdx.x) * 2 * H;
 #pragma unroll
-  for (int qtr = 0; qtr < 4; ++qtr) {
+  for (int v = 0; v < NV; ++v) {
     __syncthreads();
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = (lane + 64 * v) * 8 + j;
-        if (c / (H / 4) == qtr) {
-          red[w][0][c % (H / 4)] = dg[v][j];
-          red[w][1][c % (H / 4)] = db[v][j];
-        }
-      }
+    *reinterpret_cast<f32x4_t*>(&red[w][0][lane * 8]) = *reinterpret_cast<const f32x4_t*>(dg[v]);
+    *reinterpret_cast<f32x4_t*>(&red[w][0][lane * 8 + 4]) = *reinterpret_cast<const f32x4_t*>(dg[v] + 4);
+    *reinterpret_cast<f32x4_t*>(&red[w][1][lane * 8]) = *reinterpret_cast<const f32x4_t*>(db[v]);
+    *reinterpret_cast<f32x4_t*>(&red[w][1][lane * 8 + 4]) = *reinterpret_cast<const f32x4_t*>(db[v] + 4);
     __syncthreads();
-    for (int i = threadIdx.x; i < 2 * (H / 4); i += 256) {
-      const int which = i / (H / 4), col = i % (H / 4);
-      const float t = red[0][which][col] + red[1][which][col] + red[2][which][col] + red[3][which][col];
-      out[which * H + qtr * (H / 4) + col] = t;
+    for (int i = threadIdx.x; i < 2 * CH; i += W * 64) {
+      const int which = i / CH, col = i % CH;
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < W; ++k) t += red[k][which][col];
+      out[which * H + v * CH + col] = t;
     }
   }
 }
@@ -472,6 +544,16 @@ using namespace ttdk;
     default: return hipErrorInvalidValue;                                               \
   }
 
+#define TTDK_LN_BWD_DISPATCH(...)                                                        \
+  switch (H) {                                                                           \
+    case 512: hipLaunchKernelGGL((ln_bwd_kernel<1, 16, 1>), dim3(nb), dim3(16 * 64), __VA_ARGS__); break; \
+    case 1024: hipLaunchKernelGGL((ln_bwd_kernel<2, 8, 2>), dim3(nb), dim3(8 * 64), __VA_ARGS__); break;  \
+    case 1536: hipLaunchKernelGGL((ln_bwd_kernel<3, 8, 1>), dim3(nb), dim3(8 * 64), __VA_ARGS__); break;  \
+    case 2048: hipLaunchKernelGGL((ln_bwd_kernel<4, 4, 1>), dim3(nb), dim3(4 * 64), __VA_ARGS__); break;  \
+    case 4096: hipLaunchKernelGGL((ln_bwd_kernel<8, 4, 1>), dim3(nb), dim3(4 * 64), __VA_ARGS__); break;  \
+    default: return hipErrorInvalidValue;                                                \
+  }
+
 TTDK_EXPORT int ttdk_ln_fwd(const bf16_t* x, const bf16_t* res, bf16_t* s_out, bf16_t* y, float* mean, float* rstd,
                             const float* gamma, const float* beta, int rows, int H, float eps, float p_in,
                             unsigned site_in, float p_out, unsigned site_out, const long long* rng, hipStream_t st) {
@@ -493,8 +575,7 @@ TTDK_EXPORT int ttdk_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean
   DropSpec d = make_drop(rng, site_in, p_in, site_out, p_out);
   const int nb = ttdk_ln_bwd_num_blocks(rows);
   const int rpb = (rows + nb - 1) / nb;
-  TTDK_LN_DISPATCH(ln_bwd_kernel, dim3(nb), dim3(256), 0, st, dy, s, mean, rstd, gamma, ds_out, dx_out, part, rows, rpb,
-                   d);
+  TTDK_LN_BWD_DISPATCH(0, st, dy, s, mean, rstd, gamma, ds_out, dx_out, part, rows, rpb, d);
   // part rows are [dgamma(H) | dbeta(H)]; one launch when the outputs are adjacent (flat store)
   if (dbeta == dgamma + H) {
     hipLaunchKernelGGL(colreduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, st, part, nb, 2 * H, 2 * H, dgamma,

@@ -91,11 +91,13 @@ def test_attention_fwd_bwd_matches_reference(masked, p):
 
 
 @gpu
-@pytest.mark.parametrize("H", [512, 1024])
-def test_layernorm_residual_dropout_fwd_bwd(H):
+@pytest.mark.parametrize("H,rows", [(512, 300), (1024, 300), (1024, 5003), (512, 4099), (1536, 300), (2048, 77),
+                                    (4096, 300)])
+def test_layernorm_residual_dropout_fwd_bwd(H, rows):
+    # rows >= 4096 take the many-rows-per-block backward path (odd tails: a wave's second row
+    # missing, a short last block); each H has its own (waves, rows-in-flight) variant
     torch.manual_seed(1)
     dev = "cuda"
-    rows = 300
     x = torch.randn(rows, H, device=dev).bfloat16()
     res = torch.randn(rows, H, device=dev).bfloat16()
     gamma = torch.randn(H, device=dev) * 0.5 + 1

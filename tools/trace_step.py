@@ -3,7 +3,8 @@
 at the last dispatch whose name contains --start, default pad_channels). Prints total kernel
 time, step wall time and the top kernels, plus the ordered list of BN streaming passes with
 their durations (for per-layer bandwidth checks).
-usage: trace_step.py <run_kernel_trace.csv> [--start NAME] [--seq SUBSTR]"""
+--streams adds a per-HIP-stream table (busy time and top kernels of each stream).
+usage: trace_step.py <run_kernel_trace.csv> [--start NAME] [--seq SUBSTR] [--streams]"""
 import csv
 import re
 import sys
@@ -37,6 +38,15 @@ def main():
     print("step: kernel %.1f us, wall %.1f us, %d dispatches" % (s, wall, len(last)))
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:30]:
         print("%9.1f us %5.1f%% n=%4d %s" % (v, 100 * v / s, cnt[k], k))
+    if "--streams" in sys.argv:
+        per = defaultdict(lambda: defaultdict(float))
+        for r in last:
+            per[r["Stream_Id"]][short(r["Kernel_Name"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        for sid, d in sorted(per.items()):
+            busy = sum(d.values())
+            print("\nstream %s: busy %.1f us (%.1f%% of wall)" % (sid, busy, 100 * busy / wall))
+            for k, v in sorted(d.items(), key=lambda kv: -kv[1])[:25]:
+                print("%9.1f us %5.1f%% %s" % (v, 100 * v / busy, k))
 
 
 if __name__ == "__main__":
