@@ -877,6 +877,12 @@ hipError_t splitk_reduce(const float* ws_c, int splits, long long n, float* out,
   return hipGetLastError();
 }
 
+// integer environment switch (A/B runs)
+inline int getenv_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 // ------------------------------------------------------------------ 256-row LDS-DMA GEMM
 // Large-GEMM / large-conv path: 256 x BN x (128 B of K) tile, BN in {256, 128}, 8 waves,
 // ~1 workgroup per CU. Operand tiles stream global -> LDS with global_load_lds_dwordx4 (no
@@ -938,17 +944,18 @@ struct ConvP {  // implicit-GEMM geometry: source tensor [Nimg, Hs, Ws, Cs]; GEM
 };
 
 // ---- dense K-major: half = HROWS rows x 128 B
-template <int HROWS, int ESZ>
+template <int HROWS, int ESZ, int T = THR>
 struct OpDenseK {
   using Params = DenseP;
-  static constexpr int G = HROWS / 64;  // glds per wave per half
+  static constexpr int THREADS = T;
+  static constexpr int G = HROWS * 8 / T;  // glds per wave per half
   const char* src[2][G];
   __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < G; ++i) {
-        const int q = i * THR + tid;
+        const int q = i * T + tid;
         const int row = q >> 3, slot = q & 7;
         const int chunk = slot ^ ((row >> 1) & 7);
         const int r = min(row0 + h * HROWS + row, P.rows - 1);
@@ -958,15 +965,16 @@ struct OpDenseK {
   template <int H>
   __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
 #pragma unroll
-    for (int i = 0; i < G; ++i) glds(src[H][i] + static_cast<long long>(kt) * 128, lds + (i * THR + wave * 64) * 16);
+    for (int i = 0; i < G; ++i) glds(src[H][i] + static_cast<long long>(kt) * 128, lds + (i * T + wave * 64) * 16);
   }
 };
 
 // ---- dense MN-major (bf16): half = HROWS cols x 64 k
-template <int HROWS>
+template <int HROWS, int T = THR>
 struct OpDenseMN {
   using Params = DenseP;
-  static constexpr int G = HROWS / 64;
+  static constexpr int THREADS = T;
+  static constexpr int G = HROWS * 8 / T;
   static constexpr int CPR = HROWS / 8;  // 16-B chunks per k-row
   const char* src[2][G];
   long long kstep;
@@ -975,7 +983,7 @@ struct OpDenseMN {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < G; ++i) {
-        const int q = i * THR + tid;
+        const int q = i * T + tid;
         const int k = q / CPR, j = q % CPR;
         const int col = ((((j >> 1) ^ swz_mn<HROWS>(k))) << 4) + (j & 1) * 8;
         const int c = min(row0 + h * HROWS + col, P.rows - 8);
@@ -986,16 +994,17 @@ struct OpDenseMN {
   template <int H>
   __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
 #pragma unroll
-    for (int i = 0; i < G; ++i) glds(src[H][i] + kt * kstep, lds + (i * THR + wave * 64) * 16);
+    for (int i = 0; i < G; ++i) glds(src[H][i] + kt * kstep, lds + (i * T + wave * 64) * 16);
   }
 };
 
 // ---- implicit-GEMM conv rows (K-major): row = output pixel of the (P, Q) grid, k = (r, s, c);
 // one K-tile (128 B) lies inside one tap (requires Cs*ESZ % 128 == 0).
-template <int HROWS, int ESZ, bool DGRAD, bool UNIT_STRIDE = false>
+template <int HROWS, int ESZ, bool DGRAD, bool UNIT_STRIDE = false, int T = THR>
 struct OpConvK {
   using Params = ConvP;
-  static constexpr int G = HROWS / 64;
+  static constexpr int THREADS = T;
+  static constexpr int G = HROWS * 8 / T;
   static constexpr int KT = 128 / ESZ;  // elements per K-tile
   const char* x;
   int Hs, Ws, Cs, S, sh, sw, dh, dw, tid;
@@ -1009,7 +1018,7 @@ struct OpConvK {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < G; ++i) {
-        const int row = (i * THR + tid) >> 3;
+        const int row = (i * T + tid) >> 3;
         const int m = row0 + h * HROWS + row;
         const bool ok = m < P.rows;
         const int mm = ok ? m : 0;
@@ -1032,7 +1041,7 @@ struct OpConvK {
     const int rr = tap / S, ss = tap - rr * S;
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-      const int row = (i * THR + tid) >> 3;
+      const int row = (i * T + tid) >> 3;
       const int coff = (((tid & 7) ^ ((row >> 1) & 7))) * 16;
       int hh, ww;
       bool v = img[H][i] >= 0;
@@ -1053,16 +1062,17 @@ struct OpConvK {
       v = v && hh < Hs && ww < Ws;
       const char* s = v ? x + ((static_cast<long long>(img[H][i] + hh) * Ws + ww) * Cs + c0) * ESZ + coff
                         : reinterpret_cast<const char*>(g_zero) + coff;
-      glds(s, lds + (i * THR + wave * 64) * 16);
+      glds(s, lds + (i * T + wave * 64) * 16);
     }
   }
 };
 
 // ---- weight-gradient im2col columns (MN-major, bf16): k = output pixel, column = (r, s, c)
-template <int HROWS>
+template <int HROWS, int T = THR>
 struct OpWgradMN {
   using Params = ConvP;
-  static constexpr int G = HROWS / 64;
+  static constexpr int THREADS = T;
+  static constexpr int G = HROWS * 8 / T;
   static constexpr int CPR = HROWS / 8;
   const char* x;
   int H, W, C, pq, Q, sh, sw;
@@ -1077,7 +1087,7 @@ struct OpWgradMN {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < G; ++i) {
-        const int q = i * THR + tid;
+        const int q = i * T + tid;
         const int k = q / CPR, j = q % CPR;
         const int col = row0 + h * HROWS + ((((j >> 1) ^ swz_mn<HROWS>(k))) << 4) + (j & 1) * 8;
         krow[h][i] = k;
@@ -1101,7 +1111,7 @@ struct OpWgradMN {
       const bool v = cok[HH][i] && hh >= 0 && ww >= 0 && hh < H && ww < W;
       const char* s = v ? x + ((static_cast<long long>(n * H + hh) * W + ww) * C + cc[HH][i]) * 2
                         : reinterpret_cast<const char*>(g_zero);
-      glds(s, lds + (i * THR + wave * 64) * 16);
+      glds(s, lds + (i * T + wave * 64) * 16);
     }
   }
 };
@@ -1110,12 +1120,12 @@ template <class OP>
 struct Traits {
   static constexpr bool kmaj = true;
 };
-template <int HR>
-struct Traits<OpDenseMN<HR>> {
+template <int HR, int T>
+struct Traits<OpDenseMN<HR, T>> {
   static constexpr bool kmaj = false;
 };
-template <int HR>
-struct Traits<OpWgradMN<HR>> {
+template <int HR, int T>
+struct Traits<OpWgradMN<HR, T>> {
   static constexpr bool kmaj = false;
 };
 
@@ -1154,19 +1164,26 @@ struct Geo {
   static constexpr int AH = 128 * 128;        // A half bytes
   static constexpr int BH = BNH * 128;        // B half bytes
   static constexpr int STAGE = 2 * AH + 2 * BH;
-  static constexpr int NB = BNH / 64;         // 16-col blocks per wave per B half
   static constexpr int PITCH = BN * 2 + 16;
   static constexpr int EPI = BM * PITCH + 8 * 3 * BN * 4;  // staged tile + [8 waves][3][BN] statistics
   static constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
 };
 
 // F8: 0 = bf16, 1 = fp8 e4m3 x e4m3, 2 = e5m2 (A) x e4m3 (B)  (dgrad: gradients in e5m2)
-template <int BN, class OA, class OB, int F8>
-__global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa, typename OB::Params pb, EpiParams E,
+// PP: ping-pong schedule — every quadrant phase is {fragment reads + DMA issue} barrier
+// {MFMA cluster} barrier, with the wm = 1 wave half one barrier behind the wm = 0 half, so
+// the two waves of a SIMD alternate MFMA clusters and load segments.
+template <int BN, class OA, class OB, int F8, int PP = 0>
+__global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Params pa, typename OB::Params pb, EpiParams E,
                                                          int M, int N, int K, int tiles_m, int tiles_n,
                                                          int kt_per_split) {
   using Gm = Geo<BN>;
-  constexpr int BNH = Gm::BNH, NB = Gm::NB, GA = 2, GB = BNH / 64;
+  // T threads = NW waves in a 2 x WN grid: 8 waves (2 per SIMD, 128 x BN/4 each; the shipped
+  // shape) or 4 waves (1 per SIMD, 128 x BN/2 each: half the LDS fragment reads per MFMA, but
+  // at BN = 256 hipcc spills the 128 fragment + 256 accumulator registers: 5x slower, unused)
+  constexpr int T = OA::THREADS, NW = T / 64, WN = NW / 2;
+  static_assert(OB::THREADS == T && (NW == 8 || NW == 4), "operand policies must agree on the block size");
+  constexpr int BNH = Gm::BNH, WC = BNH / WN, NB = WC / 16, GA = OA::G, GB = OB::G;
   constexpr bool AK = Traits<OA>::kmaj, BKM = Traits<OB>::kmaj;
   static_assert(F8 == 0 || (AK && BKM), "fp8 operands must be K-major");
   __shared__ __attribute__((aligned(16))) char smem[Gm::SMEM];
@@ -1175,14 +1192,14 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
   const int tile_n = t % tiles_n, tile_m = t / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WN, wn = wave % WN;
 
   OA la;
   OB lb;
   la.init(pa, m0, tid);
   lb.init(pb, n0, tid);
 
-  // acc[ha][hb][a][b]: rows ha*128 + wm*64 + a*16, cols hb*BNH + wn*(BNH/4) + b*16
+  // acc[ha][hb][a][b]: rows ha*128 + wm*64 + a*16, cols hb*BNH + wn*WC + b*16
   f32x4_t acc[2][2][4][NB];
 #pragma unroll
   for (int ha = 0; ha < 2; ++ha)
@@ -1218,9 +1235,9 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        if constexpr (F8 != 0) f[ks][b] = frag_k8(sB, wn * (BNH / 4) + b * 16, lane);
-        else if constexpr (BKM) f[ks][b] = frag_k(sB, wn * (BNH / 4) + b * 16, ks, lane);
-        else f[ks][b] = frag_mn<BNH>(sB, wn * (BNH / 4) + b * 16, ks, lane);
+        if constexpr (F8 != 0) f[ks][b] = frag_k8(sB, wn * WC + b * 16, lane);
+        else if constexpr (BKM) f[ks][b] = frag_k(sB, wn * WC + b * 16, ks, lane);
+        else f[ks][b] = frag_mn<BNH>(sB, wn * WC + b * 16, ks, lane);
       }
   };
   auto mma = [&](const frag_t (&x)[KS][4], const frag_t (&y)[KS][NB], f32x4_t (&c)[4][NB]) {
@@ -1244,6 +1261,71 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
   // issue order per tile: A0, B1, A1, B0 (B0 last) => one counted wait retires a whole tile
   // (a deeper stream — every half issued 4-7 phases ahead with counted waits + barriers at
   // q0/q1/q3 — measured 10-40 % slower on every shape, so the shallow schedule stays)
+  if constexpr (PP) {
+    // ping-pong: the half with wm = 1 runs one barrier behind. Per K-tile kt (cb = its stage):
+    //   P0 (A0,B0): issue (kt+1).A1      P1 (A0,B1): -
+    //   P2 (A1,B1): issue (kt+2).A0, (kt+2).B0
+    //   P3 (A1,B0): counted wait retiring tile kt+1 (the two kt+2 halves stay in flight),
+    //               issue (kt+2).B1
+    // RAW: tile kt+1 is read from P0 of kt+1 on, >= 2 barriers after every wave's wait (one
+    // more than lockstep needs, for the lag). WAR: a half is re-staged >= 2 phases after the
+    // phase that read it (its reads complete before that phase's MFMAs), which with the lag
+    // still trails the slower half's reads. The last half of tile kt+1 is issued 3 phases
+    // before its wait.
+    const bool lag = __builtin_amdgcn_readfirstlane(wm) == 1;
+    if (kt0 < kt1) {
+      char* b0 = buf(kt0);
+      la.template issue<0>(b0 + A0, kt0, wave);
+      lb.template issue<0>(b0 + B0, kt0, wave);
+      lb.template issue<1>(b0 + B1, kt0, wave);
+      la.template issue<1>(b0 + A1, kt0, wave);
+      if (kt0 + 1 < kt1) {
+        char* b1 = buf(kt0 + 1);
+        la.template issue<0>(b1 + A0, kt0 + 1, wave);
+        lb.template issue<0>(b1 + B0, kt0 + 1, wave);
+        lb.template issue<1>(b1 + B1, kt0 + 1, wave);
+        wait_vm<GA + 2 * GB>();
+      } else {
+        wait_vm<0>();
+      }
+      barrier();
+      if (lag) barrier();
+    }
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool has1 = kt + 1 < kt1, has2 = kt + 2 < kt1;
+      char* cb = buf(kt);
+      // P0: (A0, B0)
+      read_a(cb + A0, fa[0]);
+      read_b(cb + B0, fb[0]);
+      if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
+      barrier();
+      mma(fa[0], fb[0], acc[0][0]);
+      barrier();
+      // P1: (A0, B1)
+      read_b(cb + B1, fb[1]);
+      barrier();
+      mma(fa[0], fb[1], acc[0][1]);
+      barrier();
+      // P2: (A1, B1)
+      read_a(cb + A1, fa[1]);
+      if (has2) {
+        la.template issue<0>(cb + A0, kt + 2, wave);
+        lb.template issue<0>(cb + B0, kt + 2, wave);
+      }
+      barrier();
+      mma(fa[1], fb[1], acc[1][1]);
+      barrier();
+      // P3: (A1, B0)
+      if (has1) {
+        if (has2) wait_vm<GA + GB>(); else wait_vm<0>();
+      }
+      if (has2) lb.template issue<1>(cb + B1, kt + 2, wave);
+      barrier();
+      mma(fa[1], fb[0], acc[1][0]);
+      barrier();
+    }
+    if (kt0 < kt1 && !lag) barrier();
+  } else {
   if (kt0 < kt1) {
     char* b0 = buf(kt0);
     la.template issue<0>(b0 + A0, kt0, wave);
@@ -1290,6 +1372,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
       read_b(nb + B0, fb[0]);
     }
   }
+  }
   wait_vm<0>();
   __syncthreads();
 
@@ -1308,7 +1391,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
         for (int hb = 0; hb < 2; ++hb)
 #pragma unroll
           for (int b = 0; b < NB; ++b) {
-            const int n = n0 + hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
+            const int n = n0 + hb * BNH + wn * WC + b * 16 + 4 * g;
             f32x4_t v = acc[ha][hb][a][b] * alpha_e;
             float* o = out + out_row(E, m) * E.ldo + n;
             if (n + 3 < N && (E.ldo & 3) == 0) {
@@ -1332,14 +1415,14 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-          const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * BNH + wn * (BNH / 4) + b * 16 + 4 * g;
+          const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * BNH + wn * WC + b * 16 + 4 * g;
           const f32x4_t v = acc[ha][hb][a][b] * alpha_e;
           *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) =
               make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         }
   __syncthreads();
   constexpr int CPR = BN / 8;     // 16-B chunks per row
-  constexpr int RPP = THR / CPR;  // rows per pass
+  constexpr int RPP = T / CPR;    // rows per pass
   const int c = tid % CPR, r0 = tid / CPR;
   const int n = n0 + c * 8;
   const bool nfull = n + 8 <= N;
@@ -1366,7 +1449,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
         if (E.stat2) r8[j] += __shfl_xor(r8[j], o, 64);
       }
     }
-    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [8 waves][3][BN]
+    float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [NW waves][3][BN]
     if (lane < CPR) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1376,11 +1459,11 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
       }
     }
     __syncthreads();
-    for (int t2 = tid; t2 < BN; t2 += THR) {
+    for (int t2 = tid; t2 < BN; t2 += T) {
       if (n0 + t2 < N) {
         float ss = 0.f, qq = 0.f, rr = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < NW; ++k) {
           ss += red[(k * 3 + 0) * BN + t2];
           qq += red[(k * 3 + 1) * BN + t2];
           rr += red[(k * 3 + 2) * BN + t2];
@@ -1396,7 +1479,7 @@ __global__ __launch_bounds__(THR, 1) void gemm256_kernel(typename OA::Params pa,
   }
 }
 
-template <int BN, class OA, class OB, int F8 = 0>
+template <int BN, class OA, class OB, int F8 = 0, int PP = 0>
 hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, const EpiParams& pe, int M, int N,
                   int K, int splits, hipStream_t st) {
   const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
@@ -1405,21 +1488,35 @@ hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, 
   if (splits > ktiles) splits = ktiles;
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);
-  hipLaunchKernelGGL((gemm256_kernel<BN, OA, OB, F8>), dim3(tm * tn, splits), dim3(THR), 0, st, pa, pb, pe, M, N, K,
-                     tm, tn, per);
+  hipLaunchKernelGGL((gemm256_kernel<BN, OA, OB, F8, PP>), dim3(tm * tn, splits), dim3(OA::THREADS), 0, st, pa, pb, pe, M, N,
+                     K, tm, tn, per);
   return hipGetLastError();
 }
 
-// dense GEMM entry: A (M rows) and B (N rows), each K-major or MN-major, bf16
+// dense GEMM entry: A (M rows) and B (N rows), each K-major or MN-major, bf16. Long-K 256-wide
+// tiles take the ping-pong schedule (BERT-Large shapes +2-5 % standalone, +1.3 % per step);
+// short K keeps the two-barrier schedule (ping-pong everywhere cost ResNet-50 2 %).
+template <int BN, int PP>
+hipError_t dense_pp(const bf16_t* A, long long lda, bool ak, const bf16_t* B, long long ldb, bool bk,
+                    const EpiParams& pe, int M, int N, int K, int splits, hipStream_t st) {
+  DenseP pa{A, lda, M}, pb{B, ldb, N};
+  constexpr int BH = BN / 2;
+  if (ak && bk) return launch<BN, OpDenseK<128, 2>, OpDenseK<BH, 2>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
+  if (ak) return launch<BN, OpDenseK<128, 2>, OpDenseMN<BH>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
+  if (bk) return launch<BN, OpDenseMN<128>, OpDenseK<BH, 2>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
+  return launch<BN, OpDenseMN<128>, OpDenseMN<BH>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
+}
+
 template <int BN>
 hipError_t dense(const bf16_t* A, long long lda, bool ak, const bf16_t* B, long long ldb, bool bk,
                  const EpiParams& pe, int M, int N, int K, int splits, hipStream_t st) {
-  DenseP pa{A, lda, M}, pb{B, ldb, N};
-  constexpr int BH = BN / 2;
-  if (ak && bk) return launch<BN, OpDenseK<128, 2>, OpDenseK<BH, 2>>(pa, pb, pe, M, N, K, splits, st);
-  if (ak) return launch<BN, OpDenseK<128, 2>, OpDenseMN<BH>>(pa, pb, pe, M, N, K, splits, st);
-  if (bk) return launch<BN, OpDenseMN<128>, OpDenseK<BH, 2>>(pa, pb, pe, M, N, K, splits, st);
-  return launch<BN, OpDenseMN<128>, OpDenseMN<BH>>(pa, pb, pe, M, N, K, splits, st);
+  if constexpr (BN == 256) {
+    static const int pp_on = getenv_int("TTD_BIG_PP", 1);
+    const int kts = K / 64 / (splits > 1 ? splits : 1);  // K-tiles per workgroup
+    if (kts >= 16 && pp_on)
+      return dense_pp<BN, 1>(A, lda, ak, B, ldb, bk, pe, M, N, K, splits, st);
+  }
+  return dense_pp<BN, 0>(A, lda, ak, B, ldb, bk, pe, M, N, K, splits, st);
 }
 
 }  // namespace big
