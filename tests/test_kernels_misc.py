@@ -197,6 +197,19 @@ def test_colsum_and_dgrad_accumulate():
     torch.manual_seed(6)
     x = torch.randn(1000, 100, device="cuda").bfloat16()
     assert _rel(K.colsum(x), x.float().sum(0)) < 1e-4
+    # many row slices: vector bf16 path + parallel fold (C % 4 == 0), scalar paths, accumulate
+    for rows, C, dt in ((20000, 1024, torch.bfloat16), (5000, 100, torch.float32), (3000, 90, torch.bfloat16),
+                        (40000, 3072, torch.bfloat16)):
+        x = torch.randn(rows, C, device="cuda").to(dt)
+        ref = x.double().sum(0)
+        got = K.colsum(x)
+        assert float((got.double() - ref).abs().max()) < 1e-3 * float(ref.abs().max()) + 1e-2, (rows, C)
+        again = K.colsum(x)
+        assert torch.equal(got, again), (rows, C)  # fixed-order folds
+        base = torch.randn(C, device="cuda")
+        acc = base.clone()
+        K.colsum(x, out=acc, beta=1)
+        assert float((acc.double() - ref - base.double()).abs().max()) < 1e-3 * float(ref.abs().max()) + 1e-2
     dy = torch.randn(2, 8, 8, 64, device="cuda").bfloat16()
     w = (torch.randn(64, 3, 3, 32, device="cuda") / 24).bfloat16()
     base = torch.randn(2, 8, 8, 32, device="cuda").bfloat16()
