@@ -324,7 +324,17 @@ class MonitoredSession:
         self._create()
 
     def _create(self):
-        self._sess = self._creator.create_session(self._graph)
+        # as TF's _RecoverableSession._create_session: creating (or re-creating) the session
+        # retries while a task is still unreachable (e.g. a replacement PS that is starting)
+        delay = 0.2
+        while True:
+            try:
+                self._sess = self._creator.create_session(self._graph)
+                break
+            except errors.PREEMPTION_ERRORS as e:
+                log.warning("%s while creating the session: %s — retrying", type(e).__name__, e)
+                time.sleep(delay)
+                delay = min(2 * delay, 5.0)
         self._hooked = _HookedSession(self._sess, self._hooks)
         for h in self._hooks:
             h.after_create_session(self._sess, self.coord)
