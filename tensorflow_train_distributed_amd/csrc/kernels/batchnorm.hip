@@ -325,27 +325,36 @@ __global__ __launch_bounds__(kThreads) void finalize_kernel(const float* __restr
 // the same channel group, so its per-channel coefficients live in registers (FIXED), and all
 // kUnroll loads are issued before any math so each lane keeps several 16 B reads in flight.
 
-// out = act(y*scale[c] + shift[c] (+ residual)); 8 channels per vector.
+// out = act(y*scale[c] + shift[c] (+ residual)); 8 channels per vector. With rscale/rshift
+// the residual is itself a raw conv output whose BN is applied here (projection shortcut:
+// its normalised tensor is never stored).
 template <bool FIXED>
 __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
-                                                         const bf16_t* __restrict__ residual, bf16_t* __restrict__ out,
+                                                         const bf16_t* __restrict__ residual,
+                                                         const float* __restrict__ rscale,
+                                                         const float* __restrict__ rshift, bf16_t* __restrict__ out,
                                                          uint8_t* __restrict__ mask, uint8_t* __restrict__ q8,
                                                          float* __restrict__ q8_slot, long long n8, int C, int relu) {
   const int cg = C >> 3;
   // fp8 e4m3 copy with the slot's delayed scale; this step's amax goes to q8_slot[1]
   const float qs = q8 ? q8_slot[2] : 1.f;
   float qmax = 0.f;
-  float sc[8], sh[8];
-  auto load_coef = [&](int c0) {
-    const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(scale + c0), s1 = *reinterpret_cast<const f32x4_t*>(scale + c0 + 4);
-    const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(shift + c0), h1 = *reinterpret_cast<const f32x4_t*>(shift + c0 + 4);
+  float sc[8], sh[8], rsc[8], rsh[8];
+  auto load8 = [](const float* p, int c0, float (&d)[8]) {
+    const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p + c0), b = *reinterpret_cast<const f32x4_t*>(p + c0 + 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      sc[j] = s0[j];
-      sc[4 + j] = s1[j];
-      sh[j] = h0[j];
-      sh[4 + j] = h1[j];
+      d[j] = a[j];
+      d[4 + j] = b[j];
+    }
+  };
+  auto load_coef = [&](int c0) {
+    load8(scale, c0, sc);
+    load8(shift, c0, sh);
+    if (rscale) {
+      load8(rscale, c0, rsc);
+      load8(rshift, c0, rsh);
     }
   };
   if (FIXED) load_coef((threadIdx.x % cg) * 8);
@@ -372,8 +381,13 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
       if (residual) {
         float r[8];
         unpack8(rv[u], r);
+        if (rscale) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += r[j];
+          for (int j = 0; j < 8; ++j) f[j] += r[j] * rsc[j] + rsh[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] += r[j];
+        }
       }
       if (relu) {
 #pragma unroll
@@ -552,17 +566,17 @@ TTDK_EXPORT int ttdk_bn_bwd_finalize(const float* sums, float count, int C, cons
 
 // q8/q8_slot (optional): also write an fp8 e4m3 copy of `out` (delayed scaling, see fp8.hip).
 TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* shift, const bf16_t* residual,
-                              bf16_t* out, uint8_t* mask, uint8_t* q8, float* q8_slot, long long n, int C, int relu,
-                              hipStream_t st) {
-  if (C % 8 || n % 8 || (q8 && !q8_slot)) return hipErrorInvalidValue;
+                              const float* rscale, const float* rshift, bf16_t* out, uint8_t* mask, uint8_t* q8,
+                              float* q8_slot, long long n, int C, int relu, hipStream_t st) {
+  if (C % 8 || n % 8 || (q8 && !q8_slot) || (rscale && (!residual || !rshift))) return hipErrorInvalidValue;
   const long long n8 = n / 8;
   const int grid = grid_for(n8, kThreads * kUnroll);
   if (kThreads % (C >> 3) == 0)
-    hipLaunchKernelGGL(apply_kernel<true>, dim3(grid), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, q8,
-                       q8_slot, n8, C, relu);
+    hipLaunchKernelGGL(apply_kernel<true>, dim3(grid), dim3(kThreads), 0, st, y, scale, shift, residual, rscale, rshift, out,
+                       mask, q8, q8_slot, n8, C, relu);
   else
-    hipLaunchKernelGGL(apply_kernel<false>, dim3(grid), dim3(kThreads), 0, st, y, scale, shift, residual, out, mask, q8,
-                       q8_slot, n8, C, relu);
+    hipLaunchKernelGGL(apply_kernel<false>, dim3(grid), dim3(kThreads), 0, st, y, scale, shift, residual, rscale, rshift, out,
+                       mask, q8, q8_slot, n8, C, relu);
   return hipGetLastError();
 }
 

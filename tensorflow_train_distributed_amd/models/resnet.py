@@ -86,6 +86,9 @@ class ResNet:
         self.device = torch.device(device)
         # weight gradients on a second HIP stream (TTD_WGRAD_STREAM=0: single stream)
         self.wgrad_stream = os.environ.get("TTD_WGRAD_STREAM", "1") != "0" and self.device.type == "cuda"
+        # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
+        # never stored: two HBM passes of the stage's largest tensor saved; TTD_FUSE_PROJ=0: off)
+        self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
         self._wgrad_stream = None
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -196,9 +199,12 @@ class ResNet:
         return out
 
     # ----------------------------------------------------------------- GPU engine
-    def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False, pool=False):
+    def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False, pool=False, defer=False,
+                    residual_bn=None):
         """conv + BN (+residual) (+ReLU). x8 = (fp8 copy of x, its scale slot) selects the fp8
         forward GEMM; want8 makes the BN-apply pass also emit an fp8 copy of the output.
+        defer=True: no apply pass — returns the raw conv output (the consumer applies this BN
+        through residual_bn = (scale, shift) of its own apply pass).
         pool=True (stem): BN + ReLU + 3x3/s2 max pooling in one pass that never stores the
         BN+ReLU output; returns (pooled, ctx, argmax).
         Returns (out, ctx) or (out, ctx, out8) when want8."""
@@ -234,6 +240,8 @@ class ResNet:
         if pool:
             pooled, arg, mask = K.bn_relu_maxpool(y, st.scale, st.shift)
             return pooled, (x, y, mask, st), arg
+        if defer:
+            return y, (x, y, None, st)
         y2 = y.view(M, c.cout)
         mask = torch.empty(M * c.cout // 8, dtype=torch.uint8, device=x.device) if relu else None
         q8 = slot = None
@@ -241,7 +249,7 @@ class ResNet:
             q8 = torch.empty((N, Pp, Q, c.cout), dtype=torch.uint8, device=x.device)
             slot = self._new_a_slot()
         out = K.bn_apply(y2, st.scale, st.shift, residual=None if residual is None else residual.view(M, c.cout),
-                         relu=relu, mask=mask, q8=q8, q8_slot=slot).view(N, Pp, Q, c.cout)
+                         residual_bn=residual_bn, relu=relu, mask=mask, q8=q8, q8_slot=slot).view(N, Pp, Q, c.cout)
         if want8:
             return out, (x, y, mask, st), (q8, slot)
         return out, (x, y, mask, st)
@@ -332,8 +340,9 @@ class ResNet:
         if fp8:
             self._fp8_step_begin()
 
-        def unit(c, inp, relu, residual=None, inp8=None, want8=False):
-            r = self._convbn_fwd(c, inp, relu, residual=residual, x8=inp8, want8=want8)
+        def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None):
+            r = self._convbn_fwd(c, inp, relu, residual=residual, x8=inp8, want8=want8, defer=defer,
+                                 residual_bn=residual_bn)
             return r if want8 else (r[0], r[1], None)
 
         from ..utils import tracing
@@ -360,7 +369,7 @@ class ResNet:
                 ev.record()
                 side.wait_event(ev)
                 with torch.cuda.stream(side):
-                    sc, cd, _ = unit(blk["cd"], h, False, inp8=h8)
+                    sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
                 # h / h8 stay referenced (c1's ctx) past the join below; cd's outputs were made on
                 # the side stream, whose next work is always ordered after this step's main stream
             o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]))
@@ -368,10 +377,11 @@ class ResNet:
             if blk["cd"] is not None and side is not None:
                 main.wait_stream(side)
             elif blk["cd"] is not None:
-                sc, cd, _ = unit(blk["cd"], h, False, inp8=h8)
+                sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
             else:
                 sc, cd = h, None
-            o3, c3, h8 = unit(blk["c3"], o2, True, residual=sc, inp8=o2_8,
+            sc_bn = (cd[3].scale, cd[3].shift) if cd is not None and self.fuse_proj else None
+            o3, c3, h8 = unit(blk["c3"], o2, True, residual=sc, inp8=o2_8, residual_bn=sc_bn,
                               want8=fp8 and nxt is not None and self._fp8_conv(nxt["c1"]))
             ctxs.append((c1, c2, c3, cd))
             h = o3

@@ -65,7 +65,7 @@ _SIGS = {
     "ttdk_bn_finalize_slices": [I],
     "ttdk_bn_reduce_finalize": [P, I, I, P, I, F, P, P, F, F, P, P, P, P, P, P, P, P, P, I, P],
     "ttdk_bn_bwd_finalize": [P, F, I, P, P, P, P, P, P, I, P],
-    "ttdk_bn_apply": [P, P, P, P, P, P, P, P, L, I, I, P],
+    "ttdk_bn_apply": [P, P, P, P, P, P, P, P, P, P, L, I, I, P],
     "ttdk_bn_bwd_apply": [P, P, P, P, P, P, L, I, P],
     # pool.hip
     "ttdk_maxpool_fwd": [P, P, P] + [I] * 12 + [P],

@@ -77,15 +77,19 @@ def bn_fwd_finalize(sums, count, gamma, beta, eps, momentum, running_mean, runni
               state.scale.data_ptr(), state.shift.data_ptr(), _s())
 
 
-def bn_apply(y2d, scale, shift, *, residual=None, relu=False, out=None, mask=None, q8=None, q8_slot=None):
-    """out = act(y*scale + shift (+ residual)); `mask` (uint8 [M*C/8]) optionally receives the
-    ReLU mask as bits so the backward need not re-read `out`; `q8` (uint8 like out) an fp8
-    e4m3 copy quantised with the delayed scale of `q8_slot` (fp32[FP8_SLOT], see fp8.hip)."""
+def bn_apply(y2d, scale, shift, *, residual=None, residual_bn=None, relu=False, out=None, mask=None, q8=None,
+             q8_slot=None):
+    """out = act(y*scale + shift (+ residual)); `residual_bn` = (rscale, rshift) applies a BN
+    affine to the residual first (a raw projection-shortcut conv output); `mask` (uint8
+    [M*C/8]) optionally receives the ReLU mask as bits so the backward need not re-read `out`;
+    `q8` (uint8 like out) an fp8 e4m3 copy quantised with the delayed scale of `q8_slot`
+    (fp32[FP8_SLOT], see fp8.hip)."""
     M, C = y2d.shape
     if out is None:
         out = torch.empty_like(y2d)
-    _lib.call("ttdk_bn_apply", y2d.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(residual), out.data_ptr(),
-              _p(mask), _p(q8), _p(q8_slot), M * C, C, int(relu), _s())
+    rs, rh = residual_bn if residual_bn is not None else (None, None)
+    _lib.call("ttdk_bn_apply", y2d.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(residual), _p(rs), _p(rh),
+              out.data_ptr(), _p(mask), _p(q8), _p(q8_slot), M * C, C, int(relu), _s())
     return out
 
 

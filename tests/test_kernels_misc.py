@@ -55,6 +55,25 @@ def test_batchnorm_fwd_bwd_relu_residual():
     torch.testing.assert_close(dg2, dg) and torch.testing.assert_close(db2, db)
 
 
+@pytest.mark.parametrize("C", [96, 4096])
+def test_bn_apply_with_residual_bn_affine(C):
+    """Projection-shortcut fusion: act(y*s + h + (r*rs + rh)) in one pass against the fp32
+    reference and against applying the residual's BN as its own pass first."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(3)
+    M = 2000
+    y = torch.randn(M, C, device="cuda").bfloat16()
+    r = (torch.randn(M, C, device="cuda") * 3 + 1).bfloat16()
+    s, h = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+    rs, rh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+    out = K.bn_apply(y, s, h, residual=r, residual_bn=(rs, rh), relu=True)
+    ref = torch.relu(y.float() * s + h + r.float() * rs + rh)
+    assert _rel(out, ref) < 1e-2
+    unfused = K.bn_apply(y, s, h, residual=K.bn_apply(r, rs, rh), relu=True)
+    # the unfused path rounds the normalised residual to bf16 once more: fused is never worse
+    assert float((out.float() - ref).abs().max()) <= float((unfused.float() - ref).abs().max()) + 1e-6
+
+
 @pytest.mark.parametrize("M,C", [(3000, 96), (200000, 40), (50000, 2048)])
 def test_bn_fused_reduce_finalize_matches_unfused(M, C):
     """Slice reduction + finalize (two launches, no atomics) == the memset/atomic-reduce/finalize
