@@ -161,36 +161,37 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     bf16x8_t pf[2][2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
+      // max over the raw scores (scale > 0 commutes with max); the scale rides in the exp2 FMA
       float mx = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float v = s[qb][kb][i] * P.scale_log2;
-          if (!full && kbase + kb * 16 + 4 * g + i >= len) v = -INFINITY;
-          s[qb][kb][i] = v;
-          mx = fmaxf(mx, v);
+          if (!full && kbase + kb * 16 + 4 * g + i >= len) s[qb][kb][i] = -INFINITY;
+          mx = fmaxf(mx, s[qb][kb][i]);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m[qb], mx);
+      const float mnew = fmaxf(m[qb], mx * P.scale_log2);
       const float msub = mnew == -INFINITY ? 0.f : mnew;
       const float alpha = fast_exp2(m[qb] - msub);
       m[qb] = mnew;
       float rs = 0.f;
       const int qrow = q0 + qb * 16 + i16;
-      const uint32_t rterm = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) : 0u;
+      // hash input of key pair (kbase + kb*16 + 4g)/2 + j: a per-tile base plus constants
+      const uint32_t hbase = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) +
+                                        (static_cast<uint32_t>(kbase >> 1) + 2u * g) * kAttnPairMul
+                                  : 0u;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         uint32_t hp[2] = {0u, 0u};
         if constexpr (DROP) {  // keys kbase + kb*16 + 4g + {0,1 | 2,3}: two key pairs
-          const uint32_t pair0 = static_cast<uint32_t>(kbase + kb * 16 + 4 * g) >> 1;
-          hp[0] = attn_pair_hash(key, rterm, pair0);
-          hp[1] = attn_pair_hash(key, rterm, pair0 + 1);
+          hp[0] = attn_hash_input(key, hbase + (8u * kb) * kAttnPairMul);
+          hp[1] = attn_hash_input(key, hbase + (8u * kb + 1u) * kAttnPairMul);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = fast_exp2(s[qb][kb][i] - msub);
+          const float p = fast_exp2(__builtin_fmaf(s[qb][kb][i], P.scale_log2, -msub));
           rs += p;
           float pd = p;
           if constexpr (DROP) pd = attn_keep(hp[i >> 1], static_cast<uint32_t>(i), P.drop_thr) ? p : 0.f;
@@ -346,6 +347,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
           dp[qb][kb] = mfma(d1f, vf[kb][1], dp[qb][kb]);
         }
       }
+      // dropout hashes: lanes i16 and i16 ^ 1 hold keys 2j and 2j + 1 (one pair, one hash) of
+      // the same query rows, for kb = 0 and kb = 1: the even lane hashes the kb = 0 pairs, the
+      // odd lane the kb = 1 pairs, and they swap (16 hashes per lane instead of 32)
+      uint32_t hk[4][4][2];
+      if constexpr (DROP) {
+        const bool odd = (i16 & 1) != 0;
+        const uint32_t pair = static_cast<uint32_t>(k0 + (odd ? 16 : 0) + i16) >> 1;
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int ql = qb * 16 + 4 * g + i;
+            const uint32_t mine =
+                attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * P.S + qt * KT + ql)), pair);
+            const uint32_t other = __shfl_xor(mine, 1, 64);
+            hk[qb][i][0] = odd ? other : mine;
+            hk[qb][i][1] = odd ? mine : other;
+          }
+      }
       // P, dS (in place: sc <- P*keep*scale, dp <- dS)
 #pragma unroll
       for (int qb = 0; qb < 4; ++qb)
@@ -360,8 +380,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
             float dpv = dp[qb][kb][i];
             float pd = p;
             if constexpr (DROP) {
-              const uint32_t h = attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * P.S + qt * KT + ql)),
-                                                static_cast<uint32_t>(kcol) >> 1);
+              const uint32_t h = hk[qb][i][kb];
               const bool kp = attn_keep(h, static_cast<uint32_t>(kcol), P.drop_thr);
               pd = kp ? p * P.drop_scale : 0.f;
               dpv = kp ? dpv * P.drop_scale : 0.f;
@@ -487,14 +506,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const int qrow = q0 + qb * 16 + i16;
-      const uint32_t rterm = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) : 0u;
+      const uint32_t hbase = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) +
+                                        (static_cast<uint32_t>(kbase >> 1) + 2u * g) * kAttnPairMul
+                                  : 0u;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         uint32_t hp[2] = {0u, 0u};
         if constexpr (DROP) {
-          const uint32_t pair0 = static_cast<uint32_t>(kbase + kb * 16 + 4 * g) >> 1;
-          hp[0] = attn_pair_hash(key, rterm, pair0);
-          hp[1] = attn_pair_hash(key, rterm, pair0 + 1);
+          hp[0] = attn_hash_input(key, hbase + (8u * kb) * kAttnPairMul);
+          hp[1] = attn_hash_input(key, hbase + (8u * kb + 1u) * kAttnPairMul);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

@@ -93,9 +93,13 @@ __device__ __forceinline__ bool drop_keep(uint32_t key, unsigned long long idx, 
 // rowid * C1 + (key >> 1) * C2 with rowid = (b*H + h)*S + q, so a lane derives its row term
 // once and pays one fmix32 per two probabilities (the per-element 64-bit index + hash made
 // the dropout variant of the kernels VALU-bound). ops/transformer.attention_keep_mask mirrors it.
+constexpr uint32_t kAttnPairMul = 0x7FEB352Du;
 __device__ __forceinline__ uint32_t attn_row_term(uint32_t rowid) { return rowid * 0x9E3779B1u; }
+// hash of a precomputed input row_term + pair * kAttnPairMul (kernels walking consecutive pairs
+// form it incrementally instead of multiplying per pair)
+__device__ __forceinline__ uint32_t attn_hash_input(uint32_t key, uint32_t input) { return fmix32(key ^ input); }
 __device__ __forceinline__ uint32_t attn_pair_hash(uint32_t key, uint32_t row_term, uint32_t pair) {
-  return fmix32(key ^ (row_term + pair * 0x7FEB352Du));
+  return attn_hash_input(key, row_term + pair * kAttnPairMul);
 }
 __device__ __forceinline__ bool attn_keep(uint32_t h, uint32_t key_index, uint32_t thr16) {
   return ((key_index & 1u) ? (h >> 16) : (h & 0xffffu)) >= thr16;
