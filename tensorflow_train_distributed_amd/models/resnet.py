@@ -118,7 +118,12 @@ class ResNet:
 
     # ----------------------------------------------------------------- fp8 state
     def _fp8_conv(self, c: ConvSpec) -> bool:
-        return self.precision == "fp8" and c.cin_store % 128 == 0
+        # fp8 where it pays end to end: the 3x3 convs (compute-bound: fp8 MFMA at 2x the bf16
+        # rate, 15-43 % faster at the b1024 shapes, tools/fp8_conv_ab.py), K in 128-element
+        # tiles, >= 128 output channels. The 1x1 convs are store-bound (5-23 % faster alone),
+        # and the fp8 copy of their input that the producing BN pass must write cost more than
+        # that: every eligible conv in fp8 measured 1 % slower per step than bf16.
+        return self.precision == "fp8" and c.k > 1 and c.cin_store % 128 == 0 and c.cout >= 128
 
     def _init_fp8(self):
         P = self.params

@@ -149,16 +149,17 @@ def test_resnet_step_hipgraph_replay_matches_eager():
 
 @pytest.mark.gpu
 def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
-    """precision="fp8": 128-channel-input convs run the fp8 block-scaled MFMA forward with
-    delayed activation scaling; the step must track the bf16 engine and train with LAMB."""
+    """precision="fp8": the 3x3 convs with 128-multiple input channels run the fp8 block-scaled
+    MFMA forward with delayed activation scaling; the step must track the bf16 engine and train
+    with LAMB."""
     from tensorflow_train_distributed_amd.train.flat import FlatLAMB, Schedule
     torch.manual_seed(0)
-    stages = ((64, 2, 1), (128, 2, 2))
+    stages = ((64, 2, 1), (128, 2, 2), (256, 1, 2))
     x = torch.randn(16, 64, 64, 3, device="cuda").bfloat16()
     y = torch.randint(0, 10, (16,), device="cuda", dtype=torch.int32)
     ref = ResNet(stages, num_classes=10, device="cuda", seed=7)
     f8 = ResNet(stages, num_classes=10, device="cuda", seed=7, precision="fp8")
-    assert sum(f8._fp8_conv(c) for c in f8.conv_list()) >= 5
+    assert sum(f8._fp8_conv(c) for c in f8.conv_list()) >= 3
     s_ref = ref.forward_backward(x, y).clone()
     f8.forward_backward(x, y)  # step 1 calibrates the delayed activation scales
     s8 = f8.forward_backward(x, y).clone()
