@@ -317,6 +317,9 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     return out
 
 
+_WGRAD_GATHER_X3 = _os.environ.get("TTD_WGRAD_GATHER_X3", "1") != "0"  # A/B switch
+
+
 def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
     """Split-K factor for the weight gradient: enough blocks to fill 256 CUs twice, but every
     split keeps >= min_ktiles K-steps (the slab write + reduce is pure overhead)."""
@@ -331,6 +334,11 @@ def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
     ktiles = -(-K // 64)
+    if tiles <= 8 and (g.R > 1 or g.S > 1) and _WGRAD_GATHER_X3:
+        # im2col-gather wgrads with a handful of output tiles (stem 7x7, 64-channel 3x3): the
+        # gather is latency-bound, so ~3x the blocks hides it (b1024 stem 2.10 -> 1.64 ms, the
+        # last kernel of every backward; 3x3 64->64 0.70 -> 0.58 ms; tools/wgrad_split_sweep.py)
+        target_blocks *= 3
     s = max(1, min(ktiles // min_ktiles, -(-target_blocks // tiles)))
     return s
 
