@@ -728,7 +728,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, t
                                                       int M, int N, int K, int tiles_m, int tiles_n, int kt_per_split) {
   __shared__ __attribute__((aligned(16))) char smem[2 * (LA::BYTES + LB::BYTES)];
   const int nblk = tiles_m * tiles_n;
-  const int t = xcd_remap(blockIdx.x, nblk);
+  // split-K (gridDim.y > 1): the XCD-aware order runs over (tile, split) so the output tiles of
+  // one K-split — which read the same K rows of both operands (a weight gradient's dy and
+  // im2col slices) — share an XCD's L2; with few tiles (stem 7x7: 4) each slice was otherwise
+  // fetched from HBM by up to 4 XCDs
+  int t, split;
+  if (gridDim.y == 1) {
+    t = xcd_remap(blockIdx.x, nblk);
+    split = 0;
+  } else {
+    const int w = xcd_remap(blockIdx.x + blockIdx.y * nblk, nblk * gridDim.y);
+    t = w % nblk;
+    split = w / nblk;
+  }
   const int tile_n = t % tiles_n, tile_m = t / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -745,7 +757,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, t
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int ktiles = (K + BK - 1) / BK;
-  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt0 = split * kt_per_split;
   const int kt1 = min(kt0 + kt_per_split, ktiles);
 
   LA la;
@@ -787,7 +799,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, t
     __syncthreads();
     cur ^= 1;
   }
-  epilogue<BM, BN>(pe, acc, m0, n0, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane, M, N, blockIdx.y, tile_m, smem);
+  epilogue<BM, BN>(pe, acc, m0, n0, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane, M, N, split, tile_m, smem);
 }
 
 // Split-K reduction of fp32 slabs ws[splits][n] into out (+= when beta), deterministic, no

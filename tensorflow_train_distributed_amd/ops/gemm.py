@@ -334,11 +334,12 @@ def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
     ktiles = -(-K // 64)
-    if tiles <= 8 and (g.R > 1 or g.S > 1) and _WGRAD_GATHER_X3:
-        # im2col-gather wgrads with a handful of output tiles (stem 7x7, 64-channel 3x3): the
-        # gather is latency-bound, so ~3x the blocks hides it (b1024 stem 2.10 -> 1.64 ms, the
-        # last kernel of every backward; 3x3 64->64 0.70 -> 0.58 ms; tools/wgrad_split_sweep.py)
-        target_blocks *= 3
+    if (g.R > 1 or g.S > 1) and tiles <= 16 and _WGRAD_GATHER_X3:
+        # im2col-gather wgrads with few output tiles (stem 7x7: 4, 3x3 64->64: 5, 128->128: 9)
+        # are latency-bound on the gather: more blocks hide it (b1024, with the kernel's
+        # split-major XCD order: stem 2.10 -> 1.6-1.8 ms — the last kernel of every backward —,
+        # 3x3 64->64 0.70 -> 0.52 ms, 128->128 0.47 -> 0.42 ms; tools/wgrad_split_sweep.py)
+        target_blocks *= 3 if tiles <= 8 else 2
     s = max(1, min(ktiles // min_ktiles, -(-target_blocks // tiles)))
     return s
 
