@@ -47,3 +47,38 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
   if (e != hipSuccess || splits == 1) return e;
   return splitk_reduce(ws, splits, static_cast<long long>(M) * N, dw, beta, st);
 }
+
+// Weight gradient whose dy is the output of a BatchNorm backward applied on the fly:
+// dy = coef[0]*g + coef[1]*y + coef[2] per output channel (see MNDenseBN). Only the 4-wave
+// im2col-gather path (non-pointwise convs too small for the 256-row kernel, e.g. the stem);
+// returns hipErrorInvalidValue where ttdk_conv_wgrad would pick another kernel.
+TTDK_EXPORT int ttdk_conv_wgrad_bn(const bf16_t* x, const bf16_t* g, const bf16_t* y, const float* coef,
+                                   const TtdkConv* gm, float* dw, float* ws, int splits, int beta, int bm, int bn,
+                                   hipStream_t st) {
+  const int M = gm->K, N = gm->R * gm->S * gm->C, K = gm->N * gm->P * gm->Q;
+  if (gm->C % 8 || gm->K % 8 || is_pointwise(gm) || big_bn_wgrad(M, N, K)) return hipErrorInvalidValue;
+  if (bm == 0 || bn == 0 || bm == 256) pick_tile(M, N, &bm, &bn);
+  const int ktiles = ceil_div(K, BK);
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  if (splits > 1 && !ws) return hipErrorInvalidValue;
+  EpiParams pe{};
+  pe.alpha = 1.f;
+  pe.ldo = N;
+  if (splits > 1) {
+    pe.mode = 1;
+    pe.out = ws;
+    pe.slab_stride = static_cast<long long>(M) * N;
+  } else {
+    pe.mode = 2;
+    pe.out = dw;
+    pe.beta = beta;
+  }
+  DenseBNParams pa{g, gm->K, M, K, y, coef};
+  GatherParams pb{x, gm->H, gm->W, gm->C, gm->P, gm->Q, gm->R, gm->S, gm->sh, gm->sw, gm->ph, gm->pw, gm->dh, gm->dw, N, K};
+  hipError_t e = dispatch<MNDenseBN, MNConvGather>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
+  if (e != hipSuccess || splits == 1) return e;
+  return splitk_reduce(ws, splits, static_cast<long long>(M) * N, dw, beta, st);
+}

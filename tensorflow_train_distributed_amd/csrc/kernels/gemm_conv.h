@@ -313,6 +313,77 @@ struct MNDense {  // element (k, row) at p[k * ld + row]; VEC: rows % 8 == 0, ld
   }
 };
 
+// MN-major operand produced on the fly from a BatchNorm backward: element (k, row) =
+// a[row] * g[k][row] + b[row] * y[k][row] + c[row] (coef = [3][rows] fp32, rounded to bf16 as
+// ttdk_bn_bwd_apply rounds dz). Lets a weight gradient consume the BN-backward output without
+// that pass storing it (the stem: the last kernels of every backward). rows % 8 == 0.
+struct DenseBNParams {
+  const bf16_t* p;  // g: already ReLU-masked output gradient
+  long long ld;
+  int rows, K;
+  const bf16_t* y;  // BN input, same layout as g
+  const float* coef;
+};
+
+template <int ROWS>
+struct MNDenseBN {
+  using Params = DenseBNParams;
+  static constexpr int CPR = ROWS / 8;
+  static constexpr int KPP = NTHR / CPR;
+  static constexpr int N = BK / KPP;
+  static constexpr int BYTES = ROWS * BK * 2;
+  const bf16_t* p;
+  const bf16_t* y;
+  long long ld;
+  int K, cc, kr;
+  bool cok;
+  float ca[8], cb[8], c0[8];
+  uint4 r[N];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    cc = tid % CPR;
+    kr = tid / CPR;
+    ld = P.ld;
+    K = P.K;
+    const int m = row0 + cc * 8;
+    cok = m < P.rows;
+    p = P.p + m;
+    y = P.y + m;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = cok ? P.coef[m + j] : 0.f;
+      cb[j] = cok ? P.coef[P.rows + m + j] : 0.f;
+      c0[j] = cok ? P.coef[2 * P.rows + m + j] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void load(int k0) {
+    uint4 gv[N], yv[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int k = k0 + kr + KPP * i;
+      const bool ok = cok && k < K;
+      gv[i] = ok ? ldg16(p + static_cast<long long>(k) * ld) : make_uint4(0, 0, 0, 0);
+      yv[i] = ok ? ldg16(y + static_cast<long long>(k) * ld) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int k = k0 + kr + KPP * i;
+      float g[8], yf[8];
+      unpack8(gv[i], g);
+      unpack8(yv[i], yf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = ca[j] * g[j] + cb[j] * yf[j] + c0[j];
+      r[i] = (cok && k < K) ? pack8(g) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + mnmaj_off<ROWS>(kr + KPP * i, cc * 8)) = r[i];
+  }
+  static __device__ __forceinline__ bf16x8_t frag(const char* lds, int colbase, int ks, int lane) {
+    return mn_frag<ROWS>(lds, colbase, ks, lane);
+  }
+};
+
 // Weight-gradient im2col operand, MN-major: k = output pixel (n, p, q), column = (r, s, c),
 // element = x[n, p*sh - ph + r*dh, q*sw - pw + s*dw, c]. Each thread's k-rows advance by BK
 // per step; their (n, p, q) are carried forward with adds and wraps instead of two integer

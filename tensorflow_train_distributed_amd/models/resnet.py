@@ -275,6 +275,22 @@ class ResNet:
         N, Pp, Q, Kc = y.shape
         M = N * Pp * Q
         pre = c.name + "_bn/"
+        wname = c.name + "_conv/kernel"
+        wshape = tuple(P.var[wname].shape)
+        if (not need_dx and dstat is not None and self.fuse_bn_bwd
+                and G.conv_wgrad_bn_fusable(tuple(x.shape), wshape, (c.stride, c.stride), (c.pad, c.pad))):
+            # weight gradient only (the stem): the BN backward is applied inside the weight
+            # gradient's operand load, its output never stored (one HBM pass less at the very end
+            # of the backward, where nothing else runs)
+            coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
+                                      dstat[0], dstat[1])
+            G.conv_wgrad_bn(x, dout, y, coef, wshape, (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+            if self._wgrad_stream is not None:
+                # the bucket this completes may hold side-stream gradients: collectives issued
+                # from here must order after that stream too
+                torch.cuda.current_stream().wait_stream(self._wgrad_stream)
+            self._ready(c.name + "_bn/moving_variance")
+            return None, None
         if dstat is not None:
             dz = K.bn_backward_from_partial(dout.view(M, Kc), y.view(M, Kc), P.var[pre + "gamma"], st,
                                             P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1]).view(N, Pp, Q, Kc)
@@ -282,7 +298,6 @@ class ResNet:
             dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
                                P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
                                mask=mask).view(N, Pp, Q, Kc)
-        wname = c.name + "_conv/kernel"
         side = self._wgrad_stream
         if side is not None:
             # weight gradient on the side stream, concurrent with this unit's data gradient and

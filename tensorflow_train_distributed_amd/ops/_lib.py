@@ -55,6 +55,7 @@ _SIGS = {
     "ttdk_conv_dgrad_subpixel": [P, P, G, P, E, P],
     "ttdk_conv_dgrad_subpixel_stat_rows": [G],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
+    "ttdk_conv_wgrad_bn": [P, P, P, P, G, P, P, I, I, I, I, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
     # batchnorm.hip
     "ttdk_bn_num_partials": [L, I],

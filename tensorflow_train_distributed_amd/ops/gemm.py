@@ -363,6 +363,34 @@ def conv_wgrad(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=
     return out
 
 
+def conv_wgrad_bn_fusable(x_shape, w_shape, stride=(1, 1), padding=(0, 0)):
+    """Whether conv_wgrad_bn runs for this conv (non-pointwise, 4-wave im2col-gather kernel)."""
+    g = conv_geom(x_shape, w_shape, stride, padding)
+    M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
+    pointwise = g.R == 1 and g.S == 1 and g.sh == 1 and g.sw == 1 and g.ph == 0 and g.pw == 0
+    return not pointwise and g.C % 8 == 0 and g.K % 8 == 0 and not big_bn_wgrad(M, N, K)
+
+
+def conv_wgrad_bn(x, g_out, y, coef, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, splits=None):
+    """conv_wgrad(x, dy) with dy = coef[0]*g_out + coef[1]*y + coef[2] per output channel (the
+    BatchNorm backward of the conv's output, coef from ops.kernels.bn_backward_coef) applied as
+    the kernel loads dy: the BN-backward result is never stored. conv_wgrad_bn_fusable() shapes."""
+    _check(x, torch.bfloat16, "x")
+    _check(g_out, torch.bfloat16, "g_out")
+    _check(y, torch.bfloat16, "y")
+    g = conv_geom(x.shape, w_shape, stride, padding)
+    if out is None:
+        out = torch.empty(tuple(w_shape), dtype=torch.float32, device=x.device)
+    if splits is None:
+        splits = wgrad_splits(g)
+    ws = None
+    if splits > 1:
+        ws = torch.empty((splits,) + tuple(w_shape), dtype=torch.float32, device=x.device)
+    _lib.call("ttdk_conv_wgrad_bn", x.data_ptr(), g_out.data_ptr(), y.data_ptr(), coef.data_ptr(), ctypes.byref(g),
+              out.data_ptr(), ws.data_ptr() if ws is not None else None, splits, beta, 0, 0, _lib.stream())
+    return out
+
+
 # ------------------------------------------------------------------ fp8 (gfx950 block-scaled MFMA)
 _lib.register({
     "ttdk_conv_fwd_fp8": [_lib.P, _lib.P, _lib.G, _lib.I, _lib.E, _lib.P],

@@ -126,14 +126,21 @@ def bn_backward(dout, out_for_relu, y, gamma, state, dgamma, dbeta, *, g_out=Non
     return dz
 
 
+def bn_backward_coef(M, C, gamma, state, dgamma, dbeta, partial, T, *, accumulate=False, device=None):
+    """BN-backward finalize from per-tile sums (sum g, sum g*y): writes dgamma/dbeta and returns
+    coef [3, C] with dz = coef[0]*g + coef[1]*y + coef[2] (for a consumer that applies it)."""
+    coef = torch.empty((3, C), dtype=torch.float32, device=device if device is not None else gamma.device)
+    _bn_reduce_finalize(partial, T, C, True, M, gamma, state=state, dgamma=dgamma, dbeta=dbeta, coef=coef,
+                        accumulate=accumulate)
+    return coef
+
+
 def bn_backward_from_partial(g, y, gamma, state, dgamma, dbeta, partial, T, *, dz=None, accumulate=False):
     """BN backward when the producer of the (already ReLU-masked) gradient g also emitted the
     per-tile sums (sum g, sum g*y) — ops.gemm.conv_dgrad(bn_stat=...): finalize + one apply
     pass, no separate statistics pass over g and y."""
     M, C = y.shape
-    coef = torch.empty((3, C), dtype=torch.float32, device=y.device)
-    _bn_reduce_finalize(partial, T, C, True, M, gamma, state=state, dgamma=dgamma, dbeta=dbeta, coef=coef,
-                        accumulate=accumulate)
+    coef = bn_backward_coef(M, C, gamma, state, dgamma, dbeta, partial, T, accumulate=accumulate, device=y.device)
     if dz is None:
         dz = torch.empty_like(y)
     _lib.call("ttdk_bn_bwd_apply", g.data_ptr(), None, None, y.data_ptr(), coef.data_ptr(), dz.data_ptr(), M * C, C,

@@ -292,3 +292,34 @@ def test_splitk_reduce_many_slabs_with_accumulate(splits):
     assert _rel(out, ref + base) < 1e-4
     out2 = G.gemm(a, b, trans_a=True, out_dtype=torch.float32, splits=splits)
     assert _rel(out2, ref) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [((2, 32, 32, 8), (64, 7, 7, 8), 2, 3), ((4, 16, 16, 64), (64, 3, 3, 64), 1, 1)])
+def test_conv_wgrad_with_fused_bn_backward_operand(shape):
+    """conv_wgrad_bn (BN backward applied in the dy operand load) matches bn_backward_from_partial
+    followed by conv_wgrad (same bf16 rounding of dy, same split-K partition)."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    xs, ws, st, pd = shape
+    torch.manual_seed(11)
+    x = torch.randn(xs, device="cuda").bfloat16()
+    y = G.conv_fwd(x, (torch.randn(ws, device="cuda") * 0.1).bfloat16(), (st, st), (pd, pd))
+    N, P, Q, C = y.shape
+    M = N * P * Q
+    g = torch.randn_like(y)
+    partial, T = K.bn_stats_partial(y.view(M, C))  # any per-tile partial sums will do for the plumbing
+    gamma = torch.rand(C, device="cuda") + 0.5
+    state = K.BNState(C, "cuda")
+    K.bn_fwd_finalize(K.bn_reduce_partials(partial, T, C), M, gamma, torch.zeros(C, device="cuda"), 1e-5, 0.9,
+                      torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"), state)
+    dg1, db1, dg2, db2 = (torch.empty(C, device="cuda") for _ in range(4))
+    dz = K.bn_backward_from_partial(g.view(M, C), y.view(M, C), gamma, state, dg1, db1, partial, T).view(y.shape)
+    ref = G.conv_wgrad(x, dz, ws, (st, st), (pd, pd))
+    assert G.conv_wgrad_bn_fusable(x.shape, ws, (st, st), (pd, pd))
+    coef = K.bn_backward_coef(M, C, gamma, state, dg2, db2, partial, T)
+    got = G.conv_wgrad_bn(x, g, y, coef, ws, (st, st), (pd, pd))
+    # the two kernels may contract a*g + b*y + c into FMAs differently: dy can differ by one
+    # bf16 ulp in a few elements
+    assert float((got - ref).norm() / ref.norm()) < 2e-3
+    assert torch.equal(dg1, dg2) and torch.equal(db1, db2)
