@@ -511,7 +511,18 @@ struct EpiParams {
   // receives per-tile (sum g, sum g*by2)
   const bf16_t* by2;
   float* stat2;
+  // beta (accumulate) only at output rows m = (n, h, w) of an [bH, bW] grid with h and w even:
+  // the other rows of `out` hold no data yet (the stride-2 1x1 projection dgrad wrote only the
+  // pixels it samples), so the accumulated tensor needs no zero fill. 0 = every row.
+  int bH, bW;
 };
+
+__device__ __forceinline__ bool beta_row(const EpiParams& E, int m) {
+  if (!E.bH) return true;
+  const int hw = m % (E.bH * E.bW);
+  const int h = hw / E.bW, w = hw - h * E.bW;
+  return !((h | w) & 1);
+}
 
 __device__ __forceinline__ float epi_alpha(const EpiParams& E) {
   float a = E.alpha;
@@ -573,7 +584,10 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
       const int r = rb + u * RPP, m = m0 + r;
       if (r < BM && m < M) {
         if (E.residual && vres) pres[u] = *reinterpret_cast<const uint4*>(E.residual + static_cast<long long>(m) * E.ldr + n);
-        if (E.beta && vst) pold[u] = *reinterpret_cast<const uint4*>(out + out_row(E, m) * E.ldo + n);
+        if (E.beta && vst) {
+          pold[u] = beta_row(E, m) ? *reinterpret_cast<const uint4*>(out + out_row(E, m) * E.ldo + n)
+                                   : make_uint4(0, 0, 0, 0);
+        }
         if (E.by) {  // vst is guaranteed by the host (N % 8 == 0, ldo % 8 == 0)
           const long long o = out_row(E, m) * E.ldo + n;
           pby[u] = *reinterpret_cast<const uint4*>(E.by + o);
@@ -613,8 +627,9 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
         if (vst) {
           unpack8(pold[u], ov);
         } else {
+          const bool br = beta_row(E, m);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) ov[j] = n + j < N ? bf2f(op[j]) : 0.f;
+          for (int j = 0; j < 8; ++j) ov[j] = (br && n + j < N) ? bf2f(op[j]) : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] += ov[j];
@@ -1691,6 +1706,7 @@ struct TtdkEpilogue {
   const uint8_t* bmask;
   const bf16_t* by2;     // optional second statistics source (EpiParams::by2 / stat2)
   float* stat2;
+  int bH, bW;            // EpiParams::bH/bW (stride-2-sampled beta)
 };
 
 inline EpiParams to_epi(const TtdkEpilogue* e) {
@@ -1719,6 +1735,8 @@ inline EpiParams to_epi(const TtdkEpilogue* e) {
   p.bmask = e->bmask;
   p.by2 = e->by2;
   p.stat2 = e->stat2;
+  p.bH = e->bH;
+  p.bW = e->bW;
   return p;
 }
 

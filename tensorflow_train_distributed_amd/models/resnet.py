@@ -89,6 +89,8 @@ class ResNet:
         # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
         # never stored: two HBM passes of the stage's largest tensor saved; TTD_FUSE_PROJ=0: off)
         self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
+        # stride-2 projection dgrad without the zero fill of its output (TTD_SAMPLED_DGRAD=0: A/B)
+        self.sampled_dgrad = os.environ.get("TTD_SAMPLED_DGRAD", "1") != "0"
         self._wgrad_stream = None
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -260,13 +262,15 @@ class ResNet:
         return out, (x, y, mask, st)
 
     def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0, dstat=None,
-                    feeds=None, feeds2=None):
+                    feeds=None, feeds2=None, sampled_only=False, dx_sampled=False):
         """Backward of one conv+BN(+ReLU) unit. dout: gradient of the unit's output; with
         dstat = (partial, T) it is already ReLU-masked and its BN-backward sums came from the
         producing dgrad's epilogue. feeds: ctx of the conv+BN unit whose output is this conv's
         input — the dgrad epilogue then emits that unit's masked gradient + sums; feeds2: a
         second unit (projection shortcut BN) fed by the same gradient, whose sums come back as
-        the third element of dstat_of_dx.
+        the third element of dstat_of_dx. sampled_only: a strided 1x1 dgrad leaves the pixels
+        it does not sample unwritten (no zero fill); dx_sampled: dx (accumulated with dx_beta)
+        is such a gradient, read only at its sampled (even h, w) pixels.
         Returns (dx, dstat_of_dx)."""
         from ..ops import gemm as G
         from ..ops import kernels as K
@@ -319,16 +323,19 @@ class ResNet:
             return None, None
         wt = K.krsc_to_crsk(P.c[wname])
         stride, pad = (c.stride, c.stride), (c.pad, c.pad)
+        bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
         if (feeds is not None and self.fuse_bn_bwd
                 and G.dgrad_stat_rows(tuple(x.shape), tuple(wt.shape), stride, pad) is not None):
             _, fy, fmask, _ = feeds
             if feeds2 is not None and stride == (1, 1):
                 out, partial, T, partial2 = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta,
-                                                         bn_stat=(fy, fmask), bn_stat2=feeds2[1])
+                                                         bn_stat=(fy, fmask), bn_stat2=feeds2[1], beta_s2=bs2)
                 return out, (partial, T, partial2)
-            out, partial, T = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, bn_stat=(fy, fmask))
+            out, partial, T = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, bn_stat=(fy, fmask),
+                                           beta_s2=bs2)
             return out, (partial, T)
-        return G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta), None
+        return G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, sampled_only=sampled_only,
+                            beta_s2=bs2), None
 
     def _ready(self, name):
         if self._grad_hook is not None:
@@ -433,11 +440,13 @@ class ResNet:
             d1, st1 = self._convbn_bwd(blk["c2"], d2, c2, dstat=st2, feeds=c1)
             if blk["cd"] is not None:
                 cd_stat = (dh_stat[2], dh_stat[1]) if dh_stat is not None and len(dh_stat) == 3 else None
-                dx, _ = self._convbn_bwd(blk["cd"], g_sc, cd, dstat=cd_stat)
+                # a stride-2 projection writes only the pixels it samples; c1's accumulate reads it there
+                sampled = self.sampled_dgrad and blk["cd"].stride != 1 and blk["cd"].pad == 0
+                dx, _ = self._convbn_bwd(blk["cd"], g_sc, cd, dstat=cd_stat, sampled_only=sampled)
             else:
-                dx = g_sc
+                dx, sampled = g_sc, False
             dh, dh_stat = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1, dstat=st1, feeds=prev_c3,
-                                           feeds2=prev_cd)
+                                           feeds2=prev_cd, dx_sampled=sampled)
         if pool_fused:
             g, partial, T = K.maxpool_bwd_bnstat(dh, arg, s_ctx[2], s_ctx[1])
             self._convbn_bwd(self.stem, g, s_ctx, need_dx=False, dstat=(partial, T))

@@ -33,7 +33,7 @@ class Epilogue(ctypes.Structure):
         ("beta", c_int), ("remap", c_int), ("rP", c_int), ("rQ", c_int), ("rOH", c_int),
         ("rOW", c_int), ("rs", c_int), ("stat", c_void_p), ("alpha", c_float), ("aux", c_void_p),
         ("ascale0", c_void_p), ("ascale1", c_void_p), ("by", c_void_p), ("bmask", c_void_p),
-        ("by2", c_void_p), ("stat2", c_void_p),
+        ("by2", c_void_p), ("stat2", c_void_p), ("bH", c_int), ("bW", c_int),
     ]
 
 

@@ -33,7 +33,8 @@ def _log(kind, M, N, K, splits=1):
 
 
 def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,
-         slab_stride=0, aux=None, ascale=(None, None), by=None, bmask=None, by2=None, stat2=None):
+         slab_stride=0, aux=None, ascale=(None, None), by=None, bmask=None, by2=None, stat2=None,
+         beta_s2=None):
     e = _lib.Epilogue()
     e.mode = mode
     e.out = out.data_ptr()
@@ -53,6 +54,7 @@ def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat
     e.bmask = bmask.data_ptr() if bmask is not None else None
     e.by2 = by2.data_ptr() if by2 is not None else None
     e.stat2 = stat2.data_ptr() if stat2 is not None else None
+    e.bH, e.bW = beta_s2 if beta_s2 is not None else (0, 0)
     return e
 
 
@@ -250,11 +252,16 @@ def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
 
 
 def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
-               tile=(0, 0), bn_stat=None, bn_stat2=None):
+               tile=(0, 0), bn_stat=None, bn_stat2=None, sampled_only=False, beta_s2=None):
     """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
 
     For strided 1x1 convs only the sampled pixels are written: pass a zero-initialised `out`
-    or beta=1 with `out` already holding another gradient contribution.
+    or beta=1 with `out` already holding another gradient contribution. sampled_only=True
+    leaves the other pixels of a fresh `out` unwritten (no zero fill): its consumer must read
+    it with beta_s2.
+
+    beta_s2=(H, W): with beta=1, `out` is such a sampled-only gradient of an [N, H, W, C]
+    tensor — the accumulate reads it only at pixels with h and w even and takes 0 elsewhere.
 
     bn_stat=(y, mask): dx is the output gradient of a conv+BN(+ReLU) unit whose pre-BN conv
     output is y (same shape as dx) and ReLU bit mask is `mask` (or None). The epilogue then
@@ -268,7 +275,7 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     g = conv_geom(x_shape, (K, R, S, C), stride, padding)
     strided_pw = R == 1 and S == 1 and padding == (0, 0) and tuple(stride) != (1, 1)
     if out is None:
-        alloc = torch.zeros if (strided_pw and not beta) else torch.empty
+        alloc = torch.zeros if (strided_pw and not beta and not sampled_only) else torch.empty
         out = alloc(tuple(x_shape), dtype=torch.bfloat16, device=dy.device)
     if bn_stat is not None:
         y, mask = bn_stat
@@ -283,7 +290,8 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
             if tuple(bn_stat2.shape) != tuple(x_shape) or tuple(stride) != (1, 1):
                 raise ValueError("conv_dgrad: second BN statistics need a unit-stride dgrad of the same shape")
             partial2 = torch.empty((T, 2, C), dtype=torch.float32, device=dy.device)
-        e = _epi(out, ldo=C, beta=beta, stat=partial, by=y, bmask=mask, by2=bn_stat2, stat2=partial2)
+        e = _epi(out, ldo=C, beta=beta, stat=partial, by=y, bmask=mask, by2=bn_stat2, stat2=partial2,
+                 beta_s2=beta_s2 if beta else None)
         if tuple(stride) != (1, 1):
             if _LOG is not None:
                 for pa in _phases(g.sh, g.ph, R, g.H):
@@ -299,7 +307,7 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
             _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), bm, bn, ctypes.byref(e),
                       _lib.stream())
         return (out, partial, T) if partial2 is None else (out, partial, T, partial2)
-    e = _epi(out, ldo=C, beta=beta, residual=residual)
+    e = _epi(out, ldo=C, beta=beta, residual=residual, beta_s2=beta_s2 if beta else None)
     if _subpixel_ok(g, R, S, stride, padding) and residual is None and tile == (0, 0):
         # strided dgrad as s*s unit-stride phase GEMMs (skips the zero taps of the direct gather)
         if _LOG is not None:  # one GEMM per phase, in ttdk_conv_dgrad_subpixel's launch order

@@ -238,6 +238,35 @@ def test_colsum_and_dgrad_accumulate():
     assert _rel(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 16, 16, 64), (3, 14, 10, 128)])
+def test_sampled_projection_dgrad_then_stride2_beta(shape):
+    """The stride-2 1x1 projection dgrad with sampled_only=True leaves the pixels it does not
+    sample unwritten (here: NaN garbage); the unit-stride dgrad that accumulates into it with
+    beta_s2 reads only the sampled (even h, w) pixels, so the sum equals the zero-filled path."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(7)
+    N, H, W, C = shape
+    K = 2 * C
+    dy_p = torch.randn(N, H // 2, W // 2, K, device="cuda").bfloat16()
+    w_p = (torch.randn(K, 1, 1, C, device="cuda") / 16).bfloat16()
+    dy_1 = torch.randn(N, H, W, 96, device="cuda").bfloat16()
+    w_1 = (torch.randn(96, 1, 1, C, device="cuda") / 10).bfloat16()
+    wt_p = w_p.permute(3, 1, 2, 0).contiguous()
+    wt_1 = w_1.permute(3, 1, 2, 0).contiguous()
+    ref = G.conv_dgrad(dy_p, wt_p, (N, H, W, C), (2, 2), (0, 0))  # zero-filled
+    ref = G.conv_dgrad(dy_1, wt_1, (N, H, W, C), out=ref, beta=1).float()
+    out = torch.full((N, H, W, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+    G.conv_dgrad(dy_p, wt_p, (N, H, W, C), (2, 2), (0, 0), out=out, sampled_only=True)
+    assert torch.isnan(out[:, 1::2].float()).all()  # unsampled rows untouched
+    G.conv_dgrad(dy_1, wt_1, (N, H, W, C), out=out, beta=1, beta_s2=(H, W))
+    assert not torch.isnan(out.float()).any()
+    assert torch.equal(out.float(), ref)
+    full = F.conv_transpose2d(dy_p.float().permute(0, 3, 1, 2), w_p.float().permute(0, 3, 1, 2), stride=2,
+                              output_padding=(H % 2 == 0 and 1 or 0, W % 2 == 0 and 1 or 0))
+    full = full + F.conv2d(dy_1.float().permute(0, 3, 1, 2), w_1.float().permute(3, 0, 1, 2))
+    assert _rel(out.permute(0, 3, 1, 2), full) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(4, 16, 16, 64), (2, 12, 10, 32), (3, 8, 8, 256)])
 def test_stem_fused_bn_relu_maxpool_and_backward_stats(shape):
     """Fused BN+ReLU+maxpool (stem) equals bn_apply followed by maxpool_fwd bit for bit; the
