@@ -59,7 +59,8 @@ def build_resnet(args, dev, rank, world):
     step.params = model.params
 
     info = {
-        "metric": "images/sec (whole node) ResNet-50 %s MirroredStrategy" % args.precision,
+        # BASELINE.json's headline metric string, verbatim
+        "metric": "images/sec (whole node) ResNet-50 %s MirroredStrategy at 1/2/4/8 MI355X" % args.precision,
         "unit": "images/sec",
         "data": "synthetic (random NHWC images + labels resident on GPU; random-init weights)",
         "config": {"model": "ResNet-50 v1.5", "global_batch": B * world, "per_gpu_batch": B, "image_size": S,
