@@ -3,6 +3,7 @@
 MirroredStrategy-style data parallelism, one process per MI355X (BASELINE.json).
 
     python bench.py --gpus 1 --steps 20 --warmup 5
+    python bench.py --gpus 8 --steps 20 --warmup 5          # self-launches 8 ranks
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
 
@@ -11,12 +12,22 @@ RCCL all-reduce of all gradients (overlapped with backward), in-graph LR schedul
 fused optimizer update (+ bf16 weight refresh). Weak scaling: per-GPU batch fixed.
 Data: one synthetic batch resident on each GPU; weights random-init.
 
+Launch: with --gpus N > 1 and no WORLD_SIZE in the environment, this process starts N rank
+processes itself (torch.distributed.run on 127.0.0.1, before it touches any GPU), relays their
+output and exits non-zero unless rank 0 reports an N-rank process group whose replicas stayed
+bit-identical. Under an external launcher (WORLD_SIZE set) every rank runs the step directly.
+
 --model bert runs BASELINE config 4 instead (BERT-Large seq 512 pre-training, MLM+NSP,
-dropout on, LAMB; sequences/sec).
+dropout on, LAMB; sequences/sec). --model mlp runs the reference's own workload (the
+784-200-100-50-25-10 MNIST MLP of /root/reference/distribute_training.py:39-110, batch 128
+per replica, GradientDescent + staircase exponential decay, :136-152); with --device cpu the
+ranks talk over gloo (BASELINE config 1, the CPU plumbing run).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,7 +53,7 @@ def build_resnet(args, dev, rank, world):
     else:
         opt = FlatSGD(model.params, Schedule(kind=2, base_lr=0.1 * B * world / 256, warmup_steps=5, end_lr=0.0,
                                              power=2.0, total_steps=10000), momentum=0.9, weight_decay=5e-5)
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb)
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
     g = torch.Generator(device=dev)
     g.manual_seed(rank)
     S = args.image_size
@@ -57,6 +68,7 @@ def build_resnet(args, dev, rank, world):
         opt.step()
         return sums
     step.params = model.params
+    step.reducer = reducer
 
     info = {
         # BASELINE.json's headline metric string, verbatim
@@ -88,7 +100,7 @@ def build_bert(args, dev, rank, world):
     broadcast_flat_(model.params)
     opt = FlatLAMB(model.params, Schedule(kind=2, base_lr=4e-3, warmup_steps=100, end_lr=0.0, power=1.0,
                                           total_steps=10000), weight_decay=0.01, max_grad_norm=1.0)
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb)
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
     batch = synthetic_batch(cfg, B, S, max_predictions=80 if S >= 512 else 20, device=dev, seed=rank)
 
     def step():
@@ -98,6 +110,7 @@ def build_bert(args, dev, rank, world):
         opt.step()
         return sums
     step.params = model.params
+    step.reducer = reducer
 
     info = {
         "metric": "sequences/sec (whole node) BERT-Large seq%d bf16 MirroredStrategy" % S,
@@ -110,51 +123,149 @@ def build_bert(args, dev, rank, world):
     return step, B, info
 
 
+def build_mlp(args, dev, rank, world):
+    """The reference workload (distribute_training.py:39-152) as a MirroredStrategy job."""
+    from tensorflow_train_distributed_amd.models.mlp import mnist_mlp
+    from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer, broadcast_flat_
+    from tensorflow_train_distributed_amd.train.flat import FlatSGD, Schedule
+
+    B = args.batch or 128  # BATCH_SIZE (:10), per replica
+    model = mnist_mlp(device=dev, seed=1234 + rank)  # different init per rank: the broadcast must fix it
+    broadcast_flat_(model.params)
+    opt = FlatSGD(model.params, Schedule(kind=1, base_lr=0.01, decay_steps=468, decay_rate=0.96, staircase=True))
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, first_bucket_mb=0.25,
+                                 compress_bf16=args.compress_bf16)
+    g = torch.Generator(device=dev)
+    g.manual_seed(rank)
+    feed = {"x-input": torch.rand((B, 784), generator=g, device=dev),
+            "y-input": torch.randint(0, 10, (B,), generator=g, device=dev)}
+
+    def step():
+        reducer.begin()
+        out = model.forward_backward(feed, grad_scale=1.0 / (B * world), grad_hook=reducer.mark_ready)
+        reducer.finish()
+        opt.step()
+        return torch.stack([torch.as_tensor(out["loss"]).float().reshape(()),
+                            torch.as_tensor(out["accuracy"]).float().reshape(())])
+    step.params = model.params
+    step.reducer = reducer
+    info = {
+        "metric": "examples/sec (whole job) MNIST MLP MirroredStrategy",
+        "unit": "examples/sec",
+        "data": "synthetic (uniform [0,1) 784-pixel images + labels; random-init weights)",
+        "config": {"model": "MNIST MLP 784-200-100-50-25-10 (ELU, dropout 0.01)", "global_batch": B * world,
+                   "per_gpu_batch": B, "seq_len": None, "parallelism": "dp%d" % world,
+                   "optimizer": "GradientDescent, exponential_decay(0.01, 468, 0.96, staircase)"},
+    }
+    return step, B, info
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(args) -> int:
+    """Start args.gpus rank processes (one per GPU) and relay their output. Runs before this
+    process touches a GPU; returns the exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    result = None
+    for line in proc.stdout:  # relay (the JSON line is printed by rank 0 only)
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        if line.startswith("{"):
+            try:
+                result = json.loads(line)
+            except ValueError:
+                pass
+    rc = proc.wait()
+    if rc != 0:
+        return rc
+    if result is None:
+        print("bench: no result line from rank 0", file=sys.stderr)
+        return 3
+    d = result.get("dist") or {}
+    if result.get("n_gpus") != args.gpus or d.get("world_size") != args.gpus:
+        print("bench: asked for %d ranks, the process group had %s" % (args.gpus, d.get("world_size")),
+              file=sys.stderr)
+        return 4
+    if d.get("replicas_in_sync") is False:
+        print("bench: replicas diverged", file=sys.stderr)
+        return 5
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert"])
-    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = model default: 1024 images / 128 sequences)")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert", "mlp"])
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
+                    help="cpu: gloo ranks on the host (the CPU plumbing config; --model mlp)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="per-GPU batch (0 = model default: 1024 images / 128 sequences / 128 examples)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--graph", type=int, default=-1, help="hipGraph-capture the step (1/0, -1 = auto)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--compress-bf16", action="store_true", help="all-reduce gradients in bf16")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"], help="ResNet conv forward precision")
     ap.add_argument("--optimizer", default="momentum", choices=["momentum", "lamb"], help="ResNet optimizer")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
-    # one process per GPU; TTD_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs
-    # (ranks share devices round-robin), the production path is RCCL ("nccl")
-    backend = os.environ.get("TTD_DIST_BACKEND", "nccl")
-    ndev = max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank % ndev)
-    dev = torch.device("cuda", local_rank % ndev)
+        print("bench: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    on_cpu = args.device == "cpu" or (args.device == "auto" and not torch.cuda.is_available())
+    if on_cpu and args.model != "mlp":
+        print("bench: --device cpu runs --model mlp only", file=sys.stderr)
+        sys.exit(2)
+    # one process per GPU over RCCL ("nccl"); gloo on the CPU. TTD_DIST_BACKEND=gloo rehearses
+    # several GPU ranks on fewer GPUs (ranks share devices round-robin)
+    backend = "gloo" if on_cpu else os.environ.get("TTD_DIST_BACKEND", "nccl")
+    if on_cpu:
+        dev = torch.device("cpu")
+    else:
+        ndev = max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local_rank % ndev)
+        dev = torch.device("cuda", local_rank % ndev)
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
+    sync = (lambda: None) if on_cpu else torch.cuda.synchronize
 
-    build = build_resnet if args.model == "resnet50" else build_bert
+    build = {"resnet50": build_resnet, "bert": build_bert, "mlp": build_mlp}[args.model]
     step, B, info = build(args, dev, rank, world)
 
     # hipGraph capture of the whole step pays only when the host cannot keep ahead of the GPU;
     # measured neutral for ResNet-50 at batch 256 (GPU-bound), so auto = off.
     use_graph = args.graph if args.graph >= 0 else 0
+    if on_cpu or world > 1:
+        use_graph = 0  # collectives are issued eagerly (bucket order follows backward)
     graph = None
     out = None
     if use_graph:
         from tensorflow_train_distributed_amd.utils.graphs import capture
         for _ in range(2):
             step()
-        torch.cuda.synchronize()
+        sync()
         graph, out = capture(step)
         run = graph.replay
     else:
@@ -165,7 +276,7 @@ def main():
     # ResNet-50 b1024 82.1 -> 81.4 ms (3 pairs); BERT 190.9 -> 191.8 ms, so auto = ResNet only.
     main_prio = os.environ.get("TTD_MAIN_PRIO", "auto")
     main_prio = (args.model == "resnet50") if main_prio == "auto" else main_prio != "0"
-    if main_prio and graph is None:
+    if main_prio and graph is None and not on_cpu:
         prio = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
         prio.wait_stream(torch.cuda.current_stream())
         inner = run
@@ -176,22 +287,25 @@ def main():
 
     for _ in range(args.warmup):
         run()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    per_rank = [elapsed]
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        per_rank = [float(p.item()) for p in parts]
+    elapsed = max(per_rank)
     sums = step() if graph is None else out
     loss = float(sums[0])
     # replicas must hold identical weights after synchronous data-parallel steps
@@ -212,11 +326,22 @@ def main():
     if rank == 0:
         cfg = dict(info["config"])
         cfg["hipgraph"] = bool(use_graph)
-        cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
-        if replicas_in_sync is not None:
-            cfg["replicas_in_sync"] = replicas_in_sync
-            cfg["dist_backend"] = backend
+        if not on_cpu:
+            cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         cfg["final_loss"] = loss
+        red = getattr(step, "reducer", None)
+        dinfo = {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None,
+                 "per_rank_ms": [round(e / args.steps * 1e3, 3) for e in per_rank],
+                 "replicas_in_sync": replicas_in_sync}
+        if red is not None:
+            dinfo["allreduce_bytes_per_step"] = red.bytes_per_step() if world > 1 else 0
+            dinfo["buckets"] = len(red.buckets)
+            dinfo["allreduce_dtype"] = "bf16" if red.compress else "fp32"
+        if backend == "nccl" and world > 1:
+            try:
+                dinfo["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+            except Exception:  # noqa: BLE001
+                pass
         print(json.dumps({
             "metric": info["metric"],
             "value": round(rate, 2),
@@ -228,9 +353,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp8+bf16" if args.precision == "fp8" else "bf16",
+            "dtype": ("fp32" if args.model == "mlp" and on_cpu else
+                      "fp8+bf16" if args.precision == "fp8" else "bf16"),
             "data": info["data"],
             "config": cfg,
+            "dist": dinfo,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

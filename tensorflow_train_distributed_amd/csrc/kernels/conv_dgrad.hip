@@ -18,7 +18,8 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
     const int M = g->N * g->P * g->Q;
     DenseParams pa{dy, g->K, M, K};
     if (g->sh != 1 || g->sw != 1) {
-      if (g->sh != g->sw) return hipErrorInvalidValue;
+      // the stride-2-sampled beta (bH) tests the GEMM row, which a remap no longer equals
+      if (g->sh != g->sw || pe.bH) return hipErrorInvalidValue;
       pe.remap = 1;
       pe.rP = g->P;
       pe.rQ = g->Q;
@@ -112,7 +113,7 @@ TTDK_EXPORT int ttdk_conv_dgrad_subpixel(const bf16_t* dy, const bf16_t* wt, con
   if (g->sw != s || s < 2 || g->dh != 1 || g->dw != 1 || g->R < s || g->S < s || g->K % 8 || g->C % 8)
     return hipErrorInvalidValue;
   EpiParams pe = to_epi(epi);
-  if (pe.remap || pe.residual || pe.aux || pe.mode == 1 || pe.by2 || pe.stat2) return hipErrorInvalidValue;
+  if (pe.remap || pe.residual || pe.aux || pe.mode == 1 || pe.by2 || pe.stat2 || pe.bH) return hipErrorInvalidValue;
   if ((pe.stat != nullptr) != (pe.by != nullptr) || (pe.by && (pe.mode != 0 || g->C % 8 || pe.ldo % 8)))
     return hipErrorInvalidValue;
   const int N = g->C, Kc = g->K;

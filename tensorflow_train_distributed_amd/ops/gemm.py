@@ -271,6 +271,10 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     """
     _check(dy, torch.bfloat16, "dy")
     _check(wt, torch.bfloat16, "wt")
+    if beta_s2 is not None and beta and tuple(stride) != (1, 1):
+        # the sampled-beta row test works on the GEMM row index, which only equals the output
+        # pixel for unit-stride dgrads (strided ones remap rows to pixels / sub-pixel phases)
+        raise ValueError("conv_dgrad: beta_s2 needs a unit-stride dgrad")
     C, R, S, K = wt.shape
     g = conv_geom(x_shape, (K, R, S, C), stride, padding)
     strided_pw = R == 1 and S == 1 and padding == (0, 0) and tuple(stride) != (1, 1)

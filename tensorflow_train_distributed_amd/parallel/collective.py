@@ -43,6 +43,8 @@ class BucketedAllReducer:
             for d in s.shape:
                 n *= int(d)
             ends.append(o + n)
+        if ends:  # the alignment padding after the last variable rides in the last bucket
+            ends[-1] = flat.numel
         self._var_end = {s.name: e for s, e in zip(flat.specs, ends)}
         # greedy buckets on variable boundaries
         self.buckets: List[Tuple[int, int]] = []
@@ -59,6 +61,10 @@ class BucketedAllReducer:
         self._next = 0
         self._works = []
         self.launch_log: List[int] = []
+
+    def bytes_per_step(self) -> int:
+        """Bytes each rank hands to the collectives per step (all buckets)."""
+        return sum(e - s for s, e in self.buckets) * (2 if self.compress else 4)
 
     def begin(self):
         self._next = 0
@@ -141,3 +147,34 @@ def sync_on_read_mean_(flat, group=None):
         k = flat.var[n].numel()
         flat.var[n].copy_(packed[o:o + k].view_as(flat.var[n]))
         o += k
+
+
+def broadcast_state_(flat, opt=None, src: int = 0, group=None):
+    """Make every replica hold replica `src`'s training state: master weights (then the bf16
+    compute copy), the optimizer's slot buffers and its step counter. Used after a restore
+    (only `src` read the checkpoint) and after a recovery (MonitoredTrainingSession)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    dist.broadcast(flat.master, src=src, group=group)
+    flat.refresh_compute()
+    if opt is None:
+        return
+    for name in ("mom", "m", "v"):
+        buf = getattr(opt, name, None)
+        if isinstance(buf, torch.Tensor):
+            dist.broadcast(buf, src=src, group=group)
+    step = torch.tensor([int(opt._host_step)], dtype=torch.int64, device=flat.master.device)
+    dist.broadcast(step, src=src, group=group)
+    opt.set_step(int(step.item()))
+
+
+def broadcast_flag(flag: bool, src: int = 0, group=None, device=None) -> bool:
+    """Replica `src`'s value of a host boolean on every replica (e.g. "the checkpoint timer
+    fired"), so that decisions taken from per-process clocks stay collective-consistent."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return bool(flag)
+    dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
+                                             if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.broadcast(t, src=src, group=group)
+    return bool(t.item())

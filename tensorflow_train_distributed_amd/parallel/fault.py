@@ -185,7 +185,8 @@ def as_preemption_error(exc: BaseException) -> BaseException:
     backend_err = getattr(dist, "DistBackendError", None)
     msg = str(exc)
     if (backend_err is not None and isinstance(exc, backend_err)) or any(
-            s in msg for s in ("NCCL", "RCCL", "Connection reset", "Gloo", "timed out", "aborted")):
+            s in msg for s in ("NCCL", "RCCL", "Connection reset", "Connection closed", "Gloo", "gloo",
+                                 "timed out", "aborted", "closed by peer")):
         err = errors.UnavailableError("collective failed: %s" % msg)
         err.__cause__ = exc
         return err

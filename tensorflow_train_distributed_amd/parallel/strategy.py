@@ -223,6 +223,12 @@ class Strategy:
         if dist.is_initialized():
             dist.barrier(group=self.group)
 
+    def recover(self):
+        """Rebuild this strategy's communicator after a collective failure (next process-group
+        generation, same ranks). The caller then restores + broadcasts the training state."""
+        if self.group is None and reinit_process_group():
+            self.recoveries = getattr(self, "recoveries", 0) + 1
+
     def experimental_local_results(self, value):
         return (value,)
 
@@ -247,15 +253,53 @@ class Strategy:
         return self._cm.__exit__(*a)
 
 
+_PG = {"store": None, "generation": 0, "args": None}
+
+
+def _base_store(rank, world, init_method, timeout):
+    """The rendezvous key-value store, created once per process and kept across process-group
+    generations (recovery re-creates the group, not the store)."""
+    if _PG["store"] is None:
+        if init_method and init_method.startswith("tcp://"):
+            host, port = init_method[len("tcp://"):].rsplit(":", 1)
+            is_master, port = rank == 0, int(port)
+        else:  # env:// (torch.distributed.run, or a launcher exporting MASTER_ADDR/PORT)
+            host, port = os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ.get("MASTER_PORT", "29500"))
+            # under torch.distributed.run the agent hosts the store; ranks are clients
+            is_master = rank == 0 and os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() != "true"
+        _PG["store"] = dist.TCPStore(host, port, world, is_master, timeout=timeout,
+                                     wait_for_workers=False)
+    return _PG["store"]
+
+
 def _init_pg(rank, world, init_method=None, timeout_s=1800):
+    """Default process group of this replica (RCCL on GPUs, gloo on the CPU), on a key prefix
+    of the current generation so `reinit_process_group` can build a fresh one after a failure."""
     if dist.is_initialized():
         return
     backend = "nccl" if torch.cuda.is_available() else "gloo"
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", rank % max(1, torch.cuda.device_count()))))
-    dist.init_process_group(backend, rank=rank, world_size=world, init_method=init_method or "env://",
-                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    timeout = datetime.timedelta(seconds=timeout_s)
+    store = dist.PrefixStore("ttd_pg_gen%d" % _PG["generation"], _base_store(rank, world, init_method, timeout))
+    _PG["args"] = (rank, world, init_method, timeout_s)
+    dist.init_process_group(backend, store=store, rank=rank, world_size=world, timeout=timeout, **kw)
+
+
+def reinit_process_group():
+    """Tear down the (failed) default process group and build the next generation with the same
+    ranks — the collective-side half of MonitoredTrainingSession's recovery."""
+    if _PG["args"] is None:
+        return False
+    try:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001 - an aborted communicator may fail to shut down cleanly
+        pass
+    _PG["generation"] += 1
+    _init_pg(*_PG["args"])
+    return True
 
 
 class MirroredStrategy(Strategy):

@@ -340,10 +340,13 @@ class Saver:
     """
 
     def __init__(self, var_list=None, max_to_keep: int = 5, keep_checkpoint_every_n_hours: float = 10000.0,
-                 extra: Optional[dict] = None, latest_filename: str = "checkpoint"):
+                 extra: Optional[dict] = None, latest_filename: str = "checkpoint", on_restore=None):
         self.var_list = var_list
         self.max_to_keep = max_to_keep
         self.extra = extra or {}
+        # called after every restore: e.g. FlatParams.refresh_compute, so the bf16 compute
+        # copy the GPU engines run on follows the restored fp32 master weights
+        self.on_restore = list(on_restore or [])
         self.latest_filename = latest_filename
         self._last: List[Tuple[str, float]] = []
 
@@ -408,9 +411,14 @@ class Saver:
             for name in self.extra:
                 if name in keys:
                     out[name] = r.read(name)
-            return out
         finally:
             r.close()
+        from .flat import FlatParams
+        if isinstance(self.var_list, FlatParams):
+            self.var_list.refresh_compute()
+        for fn in self.on_restore:
+            fn()
+        return out
 
     def recover_last_checkpoints(self, paths: List[str]):
         self._last = [(p, time.time()) for p in paths if checkpoint_exists(p)]
@@ -587,9 +595,22 @@ class Checkpoint:
                 raise CheckpointError("missing keys: %s" % missing[:5])
         finally:
             r.close()
+        for fp in self._flat_params():  # the bf16 compute copies follow the restored masters
+            fp.refresh_compute()
         return self
 
     read = restore
+
+    def _flat_params(self):
+        from .flat import FlatParams, FlatOptimizer
+        out = []
+        for obj in self._objs.values():
+            fp = obj if isinstance(obj, FlatParams) else getattr(obj, "params", None)
+            if isinstance(obj, FlatOptimizer):
+                fp = obj.p
+            if isinstance(fp, FlatParams) and all(fp is not o for o in out):
+                out.append(fp)
+        return out
 
 
 def _slots(opt):

@@ -158,7 +158,8 @@ class CheckpointSaverHook(SessionRunHook):
         self.saved_paths: List[str] = []
 
     def begin(self):
-        os.makedirs(self._dir, exist_ok=True)
+        if self._dir:
+            os.makedirs(self._dir, exist_ok=True)
         self._gs = G.get_global_step()
         for l in self._listeners:
             l.begin()
@@ -175,7 +176,11 @@ class CheckpointSaverHook(SessionRunHook):
 
     def after_run(self, run_context, run_values):
         step = run_values.results
-        if self._timer.should_trigger_for_step(step):
+        fire = self._timer.should_trigger_for_step(step)
+        agree = getattr(run_context.session, "agree", None)
+        if agree is not None and self._timer._every_secs is not None:
+            fire = agree(fire)  # all-reduce replicas: replica 0's clock decides for everyone
+        if fire:
             self._timer.update_last_triggered_step(step)
             if self._save(run_context.session, step):
                 run_context.request_stop()
@@ -190,9 +195,10 @@ class CheckpointSaverHook(SessionRunHook):
     def _save(self, session, step):
         for l in self._listeners:
             l.before_save(session, step)
-        path = session.save_checkpoint(self._saver, os.path.join(self._dir, self._basename), step)
-        self.saved_paths.append(path)
-        log.info("Saving checkpoints for %d into %s.", step, path)
+        path = session.save_checkpoint(self._saver, os.path.join(self._dir or ".", self._basename), step)
+        if path is not None:  # None: an all-reduce replica other than replica 0 (not a writer)
+            self.saved_paths.append(path)
+            log.info("Saving checkpoints for %d into %s.", step, path)
         stop = False
         for l in self._listeners:
             stop = l.after_save(session, step) or stop

@@ -209,7 +209,8 @@ class TrainOp:
         self.local_step = 0          # SyncReplicas local step (token value)
         self._host_params = None
         self._host_grads = None
-        if self.mode == "local" and self.flat is not None:
+        if self.mode in ("local", "mirrored") and self.flat is not None:
+            # the optimizer's step counter is the global step (identical on every replica)
             self.global_step.bind(lambda: self.flat._host_step, self._set_step_local)
         g = G.get_default_graph()
         g.add_to_collection(G.TRAIN_OP, self)

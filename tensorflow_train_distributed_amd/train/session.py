@@ -127,6 +127,10 @@ class _CoreSession:
         self.checkpoint_dir = checkpoint_dir
         self.train_ops = graph.get_collection(G.TRAIN_OP)
         self.ps_ops = [op for op in self.train_ops if op.mode == "ps"]
+        # all-reduce replicas (Mirrored / MultiWorkerMirrored): replica 0 restores and writes
+        # checkpoints, every replica takes part in the state broadcast and the save collectives
+        self.strategy = mirrored_strategy(self.train_ops)
+        self.replica_id = self.strategy.replica_id if self.strategy is not None else 0
         self.client = None
         self._closed = False
         self.scaffold = scaffold
@@ -176,12 +180,29 @@ class _CoreSession:
 
     def _prepare_local(self):
         from .checkpoint import latest_checkpoint
-        if not self.checkpoint_dir:
-            return
-        ckpt = latest_checkpoint(self.checkpoint_dir)
-        if ckpt:
-            self.default_saver().restore(None, ckpt, strict=False)
-            log.info("Restored from %s", ckpt)
+        if self.checkpoint_dir and self.replica_id == 0:
+            ckpt = latest_checkpoint(self.checkpoint_dir)
+            if ckpt:
+                self.default_saver().restore(None, ckpt, strict=False)
+                log.info("Restored from %s", ckpt)
+        if self.strategy is not None:
+            # replica 0's (restored or initial) weights, optimizer slots and global step
+            from ..parallel.collective import broadcast_state_
+            for op in self.train_ops:
+                if op.mode == "mirrored":
+                    broadcast_state_(op.params, op.flat, group=self.strategy.group)
+                    op.reducer = None  # rebuilt against the current process group on first use
+
+    @property
+    def is_checkpoint_writer(self) -> bool:
+        return self.replica_id == 0
+
+    def agree(self, flag: bool) -> bool:
+        """Replica 0's value of a per-process decision (a timer firing) on every replica."""
+        if self.strategy is None:
+            return bool(flag)
+        from ..parallel.collective import broadcast_flag
+        return broadcast_flag(flag, group=self.strategy.group)
 
     # -- checkpointing
     def default_saver(self):
@@ -196,13 +217,19 @@ class _CoreSession:
         if gs is not None and not any(n == "global_step" for n, _, _ in items):
             items.append(("global_step", lambda: np.asarray(gs.value(), dtype=np.int64),
                           lambda a: gs.assign(int(np.asarray(a)))))
-        return Saver(items, extra=extra)
+        return Saver(items, extra=extra, on_restore=[op.params.refresh_compute for op in self.train_ops])
 
     def save_checkpoint(self, saver, basename, step):
-        for op in self.train_ops:  # Mirrored: BN moving statistics are SyncOnRead(MEAN)
-            red = getattr(op, "reducer", None)
-            if red is not None:
-                red.sync_on_read()
+        """Collective on all-reduce replicas: every replica averages its SyncOnRead variables
+        (BN moving statistics), replica 0 alone writes, then all wait for the write."""
+        if self.strategy is not None:
+            from ..parallel.collective import sync_on_read_mean_
+            for op in self.train_ops:
+                if op.mode == "mirrored":
+                    sync_on_read_mean_(op.params, self.strategy.group)
+            path = saver.save(None, basename, global_step=step) if self.replica_id == 0 else None
+            self.strategy.barrier()
+            return path
         if self.ps_ops:
             n = self.client.n_ps
             return saver.save(None, basename, global_step=step,
@@ -250,6 +277,15 @@ class _CoreSession:
         self._closed = True
         if self.client is not None:
             self.client.close()
+
+
+def mirrored_strategy(train_ops):
+    """The strategy of the first train op that all-reduces over more than one replica."""
+    for op in train_ops:
+        if getattr(op, "mode", None) == "mirrored" and op.strategy is not None \
+                and op.strategy.num_replicas_in_sync > 1:
+            return op.strategy
+    return None
 
 
 def _saver_items(op):
@@ -354,10 +390,15 @@ class MonitoredSession:
             except errors.PREEMPTION_ERRORS as e:
                 log.warning("%s: %s — recreating the session", type(e).__name__, e)
                 self.recoveries += 1
+                strategy = getattr(self._sess, "strategy", None)
                 try:
                     self._sess.close()
                 except Exception:  # noqa: BLE001
                     pass
+                if strategy is not None:
+                    # a failed collective leaves the communicator unusable: rebuild the process
+                    # group (next generation) before the new session restores + broadcasts
+                    strategy.recover()
                 self._create()
             except Exception as e:
                 self.coord.request_stop(e)
@@ -445,10 +486,20 @@ def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaf
     elif save_checkpoint_steps is USE_DEFAULT:
         save_checkpoint_steps = None
     all_hooks = []
+    mirror = mirrored_strategy(G.get_default_graph().get_collection(G.TRAIN_OP))
+    if mirror is not None and checkpoint_dir and ((save_checkpoint_secs and save_checkpoint_secs > 0) or
+                                                  (save_checkpoint_steps and save_checkpoint_steps > 0)):
+        # all-reduce replicas: the checkpoint hook runs on EVERY replica (its save is a
+        # collective; replica 0 writes), whichever of them the caller marked chief
+        all_hooks.append(CheckpointSaverHook(checkpoint_dir, save_secs=save_checkpoint_secs,
+                                             save_steps=save_checkpoint_steps))
+        save_checkpoint_secs = save_checkpoint_steps = None
     if is_chief:
         creator = ChiefSessionCreator(scaffold, master, config, checkpoint_dir)
         all_hooks.extend(chief_only_hooks or [])
         summary_dir = summary_dir or checkpoint_dir
+        if mirror is not None and mirror.replica_id != 0:
+            summary_dir = None  # one event-file writer per job
         if summary_dir:
             if log_step_count_steps and log_step_count_steps > 0:
                 all_hooks.append(StepCounterHook(output_dir=summary_dir, every_n_steps=log_step_count_steps))

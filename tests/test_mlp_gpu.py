@@ -103,25 +103,74 @@ def test_reference_mlp_step_hipgraph_replay_is_bit_identical():
 
 
 def test_bucketed_allreduce_through_rccl_single_rank(tmp_path):
+    """The RCCL launch path of the reducer on a real (1-rank) communicator: buckets are issued
+    during backward in order and reduce in place (SUM over one rank leaves the gradient as the
+    backward wrote it). Multi-rank averaging is tested in test_collective_multirank.py (gloo)
+    and test_two_gpu_ranks_over_gloo_stay_in_sync below."""
     import torch.distributed as dist
     from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer
     store = dist.FileStore(str(tmp_path / "store"), 1)
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
         m = ttd.models.mnist_mlp(device="cuda", seed=4, dropout_rate=0.0)
-        red = BucketedAllReducer(m.params, bucket_mb=0.25, first_bucket_mb=0.05)
-        red.world = 2  # force the collective path on a single-rank communicator (SUM over 1 rank == identity)
-        assert len(red.buckets) >= 3
         x, y = _batch(2)
+        feed = {"x-input": x.cuda(), "y-input": y.cuda()}
+        m.forward_backward(feed)
+        want = m.params.grad.clone()  # the gradient before any collective touched it
+        m.params.grad.zero_()
+        red = BucketedAllReducer(m.params, bucket_mb=0.25, first_bucket_mb=0.05)
+        red.world = 2  # force the collective path on the single-rank communicator
+        assert len(red.buckets) >= 3
         red.begin()
-        m.forward_backward({"x-input": x.cuda(), "y-input": y.cuda()}, grad_hook=red.mark_ready)
+        m.forward_backward(feed, grad_hook=red.mark_ready)
         early = list(red.launch_log)
         red.finish()
-        ref = m.params.grad.clone()
         torch.cuda.synchronize()
         assert early and early == list(range(len(early)))  # buckets launched during backward, in order
         assert red.launch_log == list(range(len(red.buckets)))
-        assert torch.equal(m.params.grad, ref)
-        assert float(ref.abs().sum()) > 0
+        assert float(want.abs().sum()) > 0
+        assert torch.equal(m.params.grad, want)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model", ["mlp", "resnet50"])
+def test_two_gpu_ranks_over_gloo_stay_in_sync(model):
+    """bench.py --gpus 2 launches its own two ranks; here both share cuda:0 and talk over gloo
+    (RCCL needs one GPU per rank): the data-parallel step with bucketed all-reduce keeps the
+    replicas bit-identical and reports a 2-rank process group."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["TTD_DIST_BACKEND"] = "gloo"
+    extra = ["--batch", "16", "--image-size", "64"] if model == "resnet50" else []
+    p = subprocess.run([sys.executable, "bench.py", "--model", model, "--gpus", "2", "--steps", "2", "--warmup", "1"]
+                       + extra, cwd=repo, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and r["dist"]["world_size"] == 2 and r["dist"]["replicas_in_sync"] is True
+
+
+def test_restore_refreshes_bf16_compute_copy(tmp_path):
+    """A restored model computes with the restored weights: the GPU engine runs on the bf16
+    compute copy, which Saver/Checkpoint restores refresh from the restored fp32 masters."""
+    x, y = _batch(3)
+    feed = {"x-input": x.cuda(), "y-input": y.cuda()}
+    a = ttd.models.mnist_mlp(device="cuda", seed=1, dropout_rate=0.0)
+    opt = ttd.train.GradientDescentOptimizer(0.1).build(a.params)
+    for _ in range(2):
+        a.forward_backward(feed)
+        opt.step()
+    want = float(a.forward_backward(feed)["loss"])
+    p1 = ttd.train.Saver(a.params).save(None, str(tmp_path / "s" / "model.ckpt"), global_step=2)
+    p2 = ttd.train.Checkpoint(model=a.params).save(str(tmp_path / "c" / "ckpt"))
+    for restore in (lambda m: ttd.train.Saver(m.params).restore(None, p1),
+                    lambda m: ttd.train.Checkpoint(model=m.params).restore(p2)):
+        b = ttd.models.mnist_mlp(device="cuda", seed=2, dropout_rate=0.0)
+        restore(b)
+        assert torch.equal(b.params.compute, a.params.compute)
+        assert float(b.forward_backward(feed)["loss"]) == want
