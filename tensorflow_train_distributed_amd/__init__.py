@@ -19,3 +19,4 @@ from .utils import app, errors, flags, tracing  # noqa: E402
 from .utils import tracing as debugging  # noqa: E402  (tf.debugging.check_numerics)
 from .utils import tracing as profiler  # noqa: E402  (roctx ranges)
 from .train.graph import placeholder  # noqa: E402
+from .train.tape import GradientTape  # noqa: E402

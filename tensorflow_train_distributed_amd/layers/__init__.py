@@ -24,6 +24,7 @@ from .. import initializers as I
 from .. import nn as N
 
 _name_uid: Dict[str, int] = collections.defaultdict(int)
+_depth = [0]  # nesting depth of Layer calls (the outermost call owns the model)
 _generator = torch.Generator(device="cpu")
 _generator.manual_seed(0)
 
@@ -92,7 +93,33 @@ class Layer(torch.nn.Module):
             self.built = True
             if x.is_cuda:
                 self.to(x.device)
-        return self.call(x, **kw)
+        top = _depth[0] == 0
+        _depth[0] += 1
+        try:
+            out = self.call(x, **kw)
+        finally:
+            _depth[0] -= 1
+        if top and getattr(self, "params", None) is None and self._var_names_all():
+            from ..parallel.strategy import get_strategy, has_strategy
+            if has_strategy():
+                # built inside strategy.scope(): the model's variables become one flat store
+                # (fused optimizer, bucketed all-reduce overlapped with the backward), mirrored
+                # from replica 0 like tf.distribute's variable creation; the building call is
+                # then re-run on the flat variables so its autograd graph feeds them
+                fp = self.to_flat(x.device)
+                st = get_strategy()
+                if st is not None and st.num_replicas_in_sync > 1:
+                    from ..parallel.collective import broadcast_flat_
+                    broadcast_flat_(fp, group=st.group)
+                _depth[0] += 1
+                try:
+                    out = self.call(x, **kw)
+                finally:
+                    _depth[0] -= 1
+        return out
+
+    def _var_names_all(self):
+        return bool(self._var_names) or any(m._var_names for m in self.modules() if isinstance(m, Layer))
 
     @property
     def losses(self):
@@ -131,12 +158,16 @@ class Layer(torch.nn.Module):
                 fp.var[name].copy_(t.detach().to(dev))
         fp.refresh_compute()
         # point the module parameters at the flat views (fp32 master; grads land in the flat buffer)
+        fp._ttd_vars = {}
         for m in self.modules():
             if isinstance(m, Layer):
                 for full, key in m._var_names:
                     p = torch.nn.Parameter(fp.var[full], requires_grad=getattr(m, key).requires_grad)
                     p.grad = fp.g[full]
+                    p._ttd_flat, p._ttd_name = fp, full  # GradientTape / apply_gradients routing
+                    fp._ttd_vars[full] = p
                     setattr(m, key, p)
+        self.params = fp
         return fp
 
 

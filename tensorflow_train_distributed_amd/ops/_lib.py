@@ -129,8 +129,28 @@ class HipKernelError(RuntimeError):
     pass
 
 
+# Per-launch timing for profiling tools (TTD_OP_TIMING=1): every call is bracketed by HIP
+# events on the current stream and labelled with the GEMM shapes ops.gemm logged for it.
+import os as _os
+TIMING = [] if _os.environ.get("TTD_OP_TIMING") else None
+_labels = []
+
+
+def label(x):
+    if TIMING is not None:
+        _labels.append(x)
+
+
 def call(name, *args):
-    rc = fn(name)(*args)
+    if TIMING is not None:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = fn(name)(*args)
+        e.record()
+        TIMING.append((name, list(_labels), s, e))
+        _labels.clear()
+    else:
+        rc = fn(name)(*args)
     if rc != 0:
         raise HipKernelError("%s failed with hipError_t %d" % (name, rc))
 

@@ -30,6 +30,7 @@ def gemm_log(reset=False):
 def _log(kind, M, N, K, splits=1):
     if _LOG is not None:
         _LOG.append((kind, int(M), int(N), int(K), int(splits)))
+    _lib.label((kind, int(M), int(N), int(K)))
 
 
 def _epi(out, *, mode=0, ldo=None, bias=None, residual=None, act=0, beta=0, stat=None, alpha=1.0,

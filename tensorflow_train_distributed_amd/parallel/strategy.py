@@ -302,10 +302,38 @@ def reinit_process_group():
     return True
 
 
+def _launch_replicas(n: int):
+    """MirroredStrategy() over n > 1 GPUs in a process that no launcher started: become the
+    launcher (one process per GPU is the MI355X design). The script is re-run as n ranks by
+    torch.distributed.run on 127.0.0.1 and this process exits with their status. Runs before
+    anything touches a GPU (device_count() does not initialise one). TTD_MIRRORED_SPAWN=0
+    raises instead; a script that cannot be re-run (interactive, -c) raises too."""
+    if n <= 1:
+        return
+    import subprocess
+    import sys
+    script = sys.argv[0] if sys.argv else ""
+    if os.environ.get("TTD_MIRRORED_SPAWN", "1") == "0" or not script or script == "-c" or not os.path.exists(script):
+        raise RuntimeError("MirroredStrategy over %d GPUs needs one process per GPU: launch the script with "
+                           "`python -m torch.distributed.run --nproc-per-node %d ...` (or pass devices=[...] "
+                           "with one device)" % (n, n))
+    import socket
+    sck = socket.socket()
+    sck.bind(("127.0.0.1", 0))
+    port = sck.getsockname()[1]
+    sck.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 class MirroredStrategy(Strategy):
     """Synchronous all-reduce data parallelism on one node, one process per GPU."""
 
     def __init__(self, devices=None, cross_device_ops: Optional[CrossDeviceOps] = None):
+        if "WORLD_SIZE" not in os.environ:
+            _launch_replicas(len(devices) if isinstance(devices, (list, tuple)) else
+                             (1 if devices is not None else torch.cuda.device_count()))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))

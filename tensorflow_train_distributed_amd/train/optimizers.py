@@ -93,7 +93,33 @@ class Optimizer:
 
     def minimize(self, model, global_step: Optional[G.GlobalStep] = None, var_list=None, name=None,
                  strategy=None) -> "TrainOp":
+        """`model` with forward_backward (the framework's engines): returns a TrainOp to run
+        in a session / strategy.run. A loss tensor or zero-argument loss callable with
+        var_list (user-defined ttd.layers models, TF2 style): computes and applies the
+        gradients now."""
+        if var_list is not None and (callable(model) and not hasattr(model, "forward_backward")
+                                     or isinstance(model, torch.Tensor)):
+            return self.apply_gradients(self.compute_gradients(model, var_list), global_step=global_step)
         return TrainOp(model, self, global_step, strategy=strategy, name=name or "train_op")
+
+    def compute_gradients(self, loss, var_list=None, **kw):
+        """tf.train.Optimizer.compute_gradients: [(gradient, variable)] of a scalar loss tensor
+        (or a zero-argument callable returning it) w.r.t. var_list (flat-backed model
+        variables: aggregated across replicas, see train/tape.py)."""
+        from .tape import GradientTape
+        if var_list is None:
+            raise errors.InvalidArgumentError("compute_gradients needs var_list (e.g. model.trainable_variables)")
+        var_list = list(var_list)
+        with GradientTape() as tape:
+            value = loss() if callable(loss) else loss
+        return list(zip(tape.gradient(value, var_list), var_list))
+
+    def apply_gradients(self, grads_and_vars, global_step=None, name=None, experimental_aggregate_gradients=True):
+        """Apply (gradient, variable) pairs with the fused flat optimizer; under a multi-replica
+        strategy the gradients are all-reduced (SUM) first unless GradientTape already did it."""
+        from .tape import apply_gradients
+        return apply_gradients(self, grads_and_vars, global_step=global_step,
+                               experimental_aggregate_gradients=experimental_aggregate_gradients)
 
     def variables(self):
         return [] if self.flat is None else [t for t in (getattr(self.flat, k, None) for k in ("mom", "m", "v"))
