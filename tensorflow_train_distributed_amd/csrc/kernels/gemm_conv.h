@@ -544,12 +544,12 @@ __device__ __forceinline__ long long out_row(const EpiParams& E, int m) {
 // residual / accumulate (beta) load of the batch issued before any of them is used: with one
 // workgroup per CU (LDS-bound tiles) a load-use per row left the epilogue latency-bound,
 // which is what capped the K <= 128 ResNet 1x1 GEMMs at ~50% of HBM bandwidth.
-template <int BM, int RPP, int PITCH, bool PF>
+template <int BM, int RPP, int PITCH, bool PF, int EBMAX = 8>
 __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, int c, int r0, int n, int m0, int M,
                                          int N, bool vst, bool vres, const float (&bias8)[8], float (&s8)[8],
                                          float (&q8)[8], float (&r8)[8]) {
   constexpr int NR = (BM + RPP - 1) / RPP;
-  constexpr int EB = !PF ? 1 : (NR < 8 ? NR : 8);  // 16 spills (measured +12 % step time)
+  constexpr int EB = !PF ? 1 : (NR < EBMAX ? NR : EBMAX);  // 16 spills (measured +12 % step time)
   bf16_t* out = static_cast<bf16_t*>(E.out);
   if (n >= N) return;
   if (!PF && !E.bias && !E.residual && !E.aux && E.act == kActNone && !E.remap && vst) {

@@ -91,6 +91,11 @@ class ResNet:
         self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
         # stride-2 projection dgrad without the zero fill of its output (TTD_SAMPLED_DGRAD=0: A/B)
         self.sampled_dgrad = os.environ.get("TTD_SAMPLED_DGRAD", "1") != "0"
+        # streaming pointwise kernel (ops.gemm.pw_conv) with the neighbouring BN pass fused in as its
+        # operand prologue, on the shapes where it measured faster (tools/pw_bench.py); TTD_FUSE_PW=0: off
+        self.fuse_pw = os.environ.get("TTD_FUSE_PW", "1") != "0" and precision == "bf16"
+        # individual switches (A/B and debugging): plain pw forward, c2->c3, c3->next c1, dgrad
+        self.pw_parts = {"plain": True, "c23": True, "c31": True, "dgrad": True}
         self._wgrad_stream = None
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -206,14 +211,40 @@ class ResNet:
         return out
 
     # ----------------------------------------------------------------- GPU engine
+    def _pw_fwd_ok(self, c: ConvSpec, fused_input: bool) -> bool:
+        """Forward 1x1 conv on the streaming kernel: K <= 128 (wide output, short reduction), or
+        K = 256 when it also absorbs the producer's BN apply (tools/pw_bench.py A/B, b1024)."""
+        from ..ops import gemm as G
+        if not (self.fuse_pw and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0):
+            return False
+        if not G.pw_ok(1 << 20, c.cout, c.cin_store):
+            return False
+        return c.cin_store <= 128 or (fused_input and c.cin_store == 256)
+
+    def _pw_part(self, name):
+        return self.fuse_pw and self.pw_parts.get(name, True)
+
+    # (dz channels, dx channels) of the data gradients that run faster on the streaming kernel with
+    # the unit's BN backward as prologue and the LDS-DMA epilogue (tools/pw_bench.py, b1024):
+    # stage-2 c3 (256 -> 64) and c1 (64 -> 256, accumulating into the shortcut gradient)
+    PW_DGRAD_SHAPES = {(256, 64), (64, 256)}
+
+    def _pw_dgrad_ok(self, c: ConvSpec) -> bool:
+        from ..ops import gemm as G
+        return (self.fuse_pw and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0
+                and (c.cout, c.cin_store) in self.PW_DGRAD_SHAPES and G.pw_ok(1 << 20, c.cin_store, c.cout))
+
     def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False, pool=False, defer=False,
-                    residual_bn=None):
+                    residual_bn=None, pro=None):
         """conv + BN (+residual) (+ReLU). x8 = (fp8 copy of x, its scale slot) selects the fp8
         forward GEMM; want8 makes the BN-apply pass also emit an fp8 copy of the output.
         defer=True: no apply pass — returns the raw conv output (the consumer applies this BN
         through residual_bn = (scale, shift) of its own apply pass).
         pool=True (stem): BN + ReLU + 3x3/s2 max pooling in one pass that never stores the
         BN+ReLU output; returns (pooled, ctx, argmax).
+        pro=(scale, shift, res, res_bn, side, side_mask): x is the RAW conv output of the producing
+        unit; its BN apply (+ residual) runs inside this conv's operand load (streaming pointwise
+        kernel) and the applied tensor / its ReLU bits land in side / side_mask (this unit's input).
         Returns (out, ctx) or (out, ctx, out8) when want8."""
         from ..ops import gemm as G
         from ..ops import kernels as K
@@ -231,13 +262,25 @@ class ResNet:
         elif big and c.cin_store % 64 == 0:
             bm, bn = 256, big  # 256-row LDS-DMA kernel (BN stat rows per 256-pixel tile)
         T = -(-M // bm)
-        partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
-        if use8:
+        partial = None
+        if pro is not None or (not use8 and self._pw_part("plain") and self._pw_fwd_ok(c, False)):
+            w2 = P.c[c.name + "_conv/kernel"].view(c.cout, c.cin_store)
+            if pro is not None:
+                psc, psh, pres, pres_bn, side, side_mask = pro
+                rs, rb = pres_bn if pres_bn is not None else (None, None)
+                y, partial, T = G.pw_conv(x, w2, prologue=("bn_fwd", psc, psh, pres, rs, rb, side, side_mask),
+                                          stat=True)
+                x = side  # the unit's input as the backward needs it
+            else:
+                y, partial, T = G.pw_conv(x, w2, stat=True)
+        elif use8:
+            partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
             xq, xslot = x8
             ws = self._w8_slots[self._w8_slot[c.name]]
             y = G.conv_fwd_fp8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
                                ascale=(xslot[3:4], ws[3:4]))
         else:
+            partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
             y = G.conv_fwd(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
                            tile=(bm, bn))
         st = K.BNState(c.cout, x.device)
@@ -248,7 +291,7 @@ class ResNet:
             pooled, arg, mask = K.bn_relu_maxpool(y, st.scale, st.shift)
             return pooled, (x, y, mask, st), arg
         if defer:
-            return y, (x, y, None, st)
+            return y, [x, y, None, st]
         y2 = y.view(M, c.cout)
         mask = torch.empty(M * c.cout // 8, dtype=torch.uint8, device=x.device) if relu else None
         q8 = slot = None
@@ -258,8 +301,8 @@ class ResNet:
         out = K.bn_apply(y2, st.scale, st.shift, residual=None if residual is None else residual.view(M, c.cout),
                          residual_bn=residual_bn, relu=relu, mask=mask, q8=q8, q8_slot=slot).view(N, Pp, Q, c.cout)
         if want8:
-            return out, (x, y, mask, st), (q8, slot)
-        return out, (x, y, mask, st)
+            return out, [x, y, mask, st], (q8, slot)
+        return out, [x, y, mask, st]
 
     def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0, dstat=None,
                     feeds=None, feeds2=None, sampled_only=False, dx_sampled=False):
@@ -295,6 +338,20 @@ class ResNet:
                 torch.cuda.current_stream().wait_stream(self._wgrad_stream)
             self._ready(c.name + "_bn/moving_variance")
             return None, None
+        if (need_dx and dstat is not None and feeds is not None and feeds2 is None
+                and self.fuse_bn_bwd and self._pw_part("dgrad") and self._pw_dgrad_ok(c)):
+            # BN backward applied inside the data gradient's operand load (streaming pointwise
+            # kernel): dz is written once there for the weight gradient, never re-read by the dgrad
+            coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
+                                      dstat[0], dstat[1])
+            dz = torch.empty_like(y)
+            wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
+            _, fy, fmask, _ = feeds
+            bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
+            out, partial, T = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, dz), bn_stat=(fy, fmask),
+                                        out=dx, beta=dx_beta if dx is not None else 0, beta_s2=bs2)
+            self._wgrad(c, x, dz, wname)
+            return out, (partial, T)
         if dstat is not None:
             dz = K.bn_backward_from_partial(dout.view(M, Kc), y.view(M, Kc), P.var[pre + "gamma"], st,
                                             P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1]).view(N, Pp, Q, Kc)
@@ -302,23 +359,7 @@ class ResNet:
             dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
                                P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
                                mask=mask).view(N, Pp, Q, Kc)
-        side = self._wgrad_stream
-        if side is not None:
-            # weight gradient on the side stream, concurrent with this unit's data gradient and
-            # the next units' BN passes (fills the tail waves of the 1-workgroup-per-CU GEMMs)
-            ev = torch.cuda.Event()
-            ev.record()
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
-                self._ready(c.name + "_bn/moving_variance")  # collectives order after the side stream
-            # keep the operands alive until the streams join at the end of the backward (no
-            # record_stream: its deferred frees made the allocator re-malloc when the host ran
-            # several steps ahead)
-            self._side_keep += [x, dz]
-        else:
-            G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
-            self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
+        self._wgrad(c, x, dz, wname)
         if not need_dx:
             return None, None
         wt = K.krsc_to_crsk(P.c[wname])
@@ -336,6 +377,28 @@ class ResNet:
             return out, (partial, T)
         return G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, sampled_only=sampled_only,
                             beta_s2=bs2), None
+
+    def _wgrad(self, c: ConvSpec, x, dz, wname):
+        """Weight gradient of conv c into its flat gradient slice; on the side stream when enabled,
+        concurrent with the data-gradient chain (fills the tail waves of the 1-workgroup-per-CU
+        GEMMs), then the gradient-ready hook (collectives order after the side stream)."""
+        from ..ops import gemm as G
+        P = self.params
+        side = self._wgrad_stream
+        if side is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+                self._ready(c.name + "_bn/moving_variance")
+            # keep the operands alive until the streams join at the end of the backward (no
+            # record_stream: its deferred frees made the allocator re-malloc when the host ran
+            # several steps ahead)
+            self._side_keep += [x, dz]
+        else:
+            G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+            self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
 
     def _ready(self, name):
         if self._grad_hook is not None:
@@ -367,9 +430,9 @@ class ResNet:
         if fp8:
             self._fp8_step_begin()
 
-        def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None):
+        def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None, pro=None):
             r = self._convbn_fwd(c, inp, relu, residual=residual, x8=inp8, want8=want8, defer=defer,
-                                 residual_bn=residual_bn)
+                                 residual_bn=residual_bn, pro=pro)
             return r if want8 else (r[0], r[1], None)
 
         from ..utils import tracing
@@ -386,9 +449,21 @@ class ResNet:
             h, arg = K.maxpool_fwd(s_out, 3, 2, 1)
         h8 = None
         ctxs = []
+        # pend: the previous block's c3 unit whose BN apply (+ residual, ReLU) is deferred into this
+        # block's c1 conv (streaming pointwise kernel prologue): (y3, state, residual, residual_bn, ctx)
+        pend = None
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
             side = self._wgrad_stream
+            c1 = None
+            if pend is not None:
+                # this block's input h = relu(bn3(y3) + shortcut) is produced by c1's operand load
+                y3p, stp, resp, resbnp, ctxp = pend
+                h = torch.empty_like(y3p)
+                hm = torch.empty(h.numel() // 8, dtype=torch.uint8, device=h.device)
+                ctxp[2] = hm  # the producing unit's ReLU bits (its backward reads them)
+                o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm))
+                pend = None
             if blk["cd"] is not None and side is not None:
                 # projection shortcut on the side stream, concurrent with the c1 -> c2 chain
                 main = torch.cuda.current_stream()
@@ -399,8 +474,18 @@ class ResNet:
                     sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
                 # h / h8 stay referenced (c1's ctx) past the join below; cd's outputs were made on
                 # the side stream, whose next work is always ordered after this step's main stream
-            o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]))
-            o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]))
+            if c1 is None:
+                o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]))
+            fuse23 = self._pw_part("c23") and self._pw_fwd_ok(blk["c3"], True)
+            if fuse23:
+                # c2's BN + ReLU are applied inside c3's operand load; o2 and its ReLU bits are
+                # written there (c3's weight gradient and c2's backward read them)
+                y2, c2, _ = unit(blk["c2"], o1, True, inp8=o1_8, defer=True)
+                o2 = torch.empty_like(y2)
+                c2[2] = torch.empty(o2.numel() // 8, dtype=torch.uint8, device=o2.device)
+                o2_8 = None
+            else:
+                o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]))
             if blk["cd"] is not None and side is not None:
                 main.wait_stream(side)
             elif blk["cd"] is not None:
@@ -408,8 +493,16 @@ class ResNet:
             else:
                 sc, cd = h, None
             sc_bn = (cd[3].scale, cd[3].shift) if cd is not None and self.fuse_proj else None
-            o3, c3, h8 = unit(blk["c3"], o2, True, residual=sc, inp8=o2_8, residual_bn=sc_bn,
-                              want8=fp8 and nxt is not None and self._fp8_conv(nxt["c1"]))
+            defer3 = nxt is not None and not fp8 and self._pw_part("c31") and self._pw_fwd_ok(nxt["c1"], True)
+            c3_in = y2 if fuse23 else o2
+            c3_pro = (c2[3].scale, c2[3].shift, None, None, o2, c2[2]) if fuse23 else None
+            if defer3:
+                y3, c3, _ = unit(blk["c3"], c3_in, True, defer=True, pro=c3_pro)
+                pend = (y3, c3[3], sc, sc_bn, c3)
+                o3, h8 = None, None
+            else:
+                o3, c3, h8 = unit(blk["c3"], c3_in, True, residual=sc, inp8=o2_8, residual_bn=sc_bn, pro=c3_pro,
+                                  want8=fp8 and nxt is not None and self._fp8_conv(nxt["c1"]))
             ctxs.append((c1, c2, c3, cd))
             h = o3
         feat_shape = h.shape

@@ -57,6 +57,9 @@ _SIGS = {
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_conv_wgrad_bn": [P, P, P, P, G, P, P, I, I, I, I, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
+    # pw_gemm.hip
+    "ttdk_pw_rows": [I, I, I],
+    "ttdk_pw_conv": [P, P, P, P, P, P, P, P, P, I, I, P, L, I, I, I, E, P],
     # batchnorm.hip
     "ttdk_bn_num_partials": [L, I],
     "ttdk_bn_stats_partial": [P, L, I, P, I, P],

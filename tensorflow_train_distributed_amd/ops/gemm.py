@@ -174,6 +174,84 @@ def conv_geom(x_shape, w_shape, stride, padding, dilation=(1, 1)):
     return g
 
 
+def pw_rows(N, K, dma=False):
+    """Rows per output tile of the streaming pointwise kernel (pw_gemm.hip) for an N x K conv,
+    or 0 when that kernel does not take the shape. dma: the launch has an accumulate / BN-statistics
+    epilogue without residual or second statistics source (the LDS-DMA epilogue configuration)."""
+    return int(_lib.query("ttdk_pw_rows", int(N), int(K), int(bool(dma))))
+
+
+_PW = _os.environ.get("TTD_PW", "1") != "0"
+
+
+def pw_ok(M, N, K):
+    """The streaming pointwise kernel takes this GEMM (and is enabled: TTD_PW=0 turns it off)."""
+    return _PW and pw_rows(N, K) > 0 and N * K <= 65536
+
+
+def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None, bn_stat=None, bn_stat2=None,
+            beta_s2=None):
+    """Unit-stride 1x1 conv / dense GEMM out[M, N] = A'[M, K] . w[N, K]^T on the persistent
+    streaming kernel (pw_gemm.hip), A' = prologue(x):
+
+    prologue None                                    A' = x
+    ("bn_fwd", scale, shift, residual, rscale, rshift, side, side_mask)
+                                                     A' = relu(x*scale+shift [+ residual(*rscale+rshift)])
+                                                     stored into `side` (+ ReLU bits into side_mask)
+    ("bn_bwd", y, mask, coef, side)                  A' = a*(x . mask) + b*y + c, stored into `side`
+
+    x: bf16 [..., K] contiguous (rows = the leading dims); w: bf16 [N, K] (or [N, 1, 1, K]).
+    stat=True: also per-tile BN partial sums of the stored output -> returns (out, partial, T).
+    bn_stat=(y, mask) [+ bn_stat2=y2]: dgrad-style ReLU-masked gradient + BN-backward sums of the
+    consuming unit (see conv_dgrad) -> returns (out, partial, T[, partial2]).
+    beta / residual / beta_s2: as conv_dgrad / gemm."""
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.bfloat16, "w")
+    K = x.shape[-1]
+    M = x.numel() // K
+    N = w.shape[0]
+    if w.numel() != N * K:
+        raise ValueError("pw_conv: weight must be [N, K] = [%d, %d] (got %s)" % (N, K, tuple(w.shape)))
+    dma = bool(beta or bn_stat is not None) and residual is None and bn_stat2 is None
+    bm = pw_rows(N, K, dma)
+    if not bm:
+        raise ValueError("pw_conv: N=%d K=%d not handled by the streaming kernel" % (N, K))
+    if out is None:
+        out = torch.empty(tuple(x.shape[:-1]) + (N,), dtype=torch.bfloat16, device=x.device)
+    T = -(-M // bm)
+    partial = partial2 = None
+    by = bmask = by2 = None
+    if stat or bn_stat is not None:
+        partial = torch.empty((T, 2, N), dtype=torch.float32, device=x.device)
+    if bn_stat is not None:
+        by, bmask = bn_stat
+        _check(by, torch.bfloat16, "bn_stat y")
+        if bn_stat2 is not None:
+            by2 = bn_stat2
+            partial2 = torch.empty((T, 2, N), dtype=torch.float32, device=x.device)
+    e = _epi(out, ldo=N, beta=beta, residual=residual, stat=partial, by=by, bmask=bmask, by2=by2, stat2=partial2,
+             beta_s2=beta_s2 if beta else None)
+    P = _lib.ptr
+    pro, x2, mask_in, s, b, rs, rb, side, side_mask = 0, None, None, None, None, None, None, None, None
+    if prologue is not None:
+        if prologue[0] == "bn_fwd":
+            _, s, b, x2, rs, rb, side, side_mask = prologue
+            pro = 1
+        elif prologue[0] == "bn_bwd":
+            _, x2, mask_in, s, side = prologue
+            pro = 2
+        else:
+            raise ValueError("pw_conv: unknown prologue %r" % (prologue[0],))
+    _log("pw_%s" % ("fwd" if pro != 2 else "dgrad"), M, N, K)
+    _lib.call("ttdk_pw_conv", x.data_ptr(), P(x2), P(mask_in), P(s), P(b), P(rs), P(rb), P(side), P(side_mask), 1, pro,
+              w.data_ptr(), K, M, N, K, ctypes.byref(e), _lib.stream())
+    if partial is None:
+        return out
+    if partial2 is not None:
+        return out, partial, T, partial2
+    return out, partial, T
+
+
 def conv_fwd(x, w, stride=(1, 1), padding=(0, 0), *, out=None, residual=None, act=ACT_NONE,
              bias=None, stat=None, tile=(0, 0)):
     """y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]) with optional fused epilogue.

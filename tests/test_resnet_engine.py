@@ -173,3 +173,36 @@ def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
         losses.append(float(f8.forward_backward(x, y)[0]))
         opt.step()
     assert losses[-1] < losses[0] - 0.5, losses
+
+
+@pytest.mark.gpu
+def test_resnet_streaming_pointwise_fusions_match_unfused_engine():
+    """The BN-prologue fusions on the streaming pointwise kernel (c2 apply -> c3 conv, c3 apply ->
+    next c1 conv, c3 BN backward -> c3 dgrad) evaluate the same per-element expressions as the
+    unfused engine; only accumulation order and fma contraction differ. A deep random-init net
+    amplifies such rounding chaotically (tools/debug_pw_ab.py: both engines sit at the same
+    distance from the fp32 oracle), so this compares both engines with the oracle on the shallow
+    net of the test above (stage 2 with two blocks: every fusion site is exercised)."""
+    torch.manual_seed(0)
+    stages = ((64, 2, 1), (128, 1, 2), (256, 1, 2), (512, 1, 2))
+    x = torch.randn(16, 64, 64, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 100, (16,), device="cuda")
+    res = {}
+    for fuse in (True, False):
+        m = ResNet(stages, num_classes=100, device="cuda", seed=3)
+        m.fuse_pw = fuse
+        sums = m.forward_backward(x, y)
+        torch.cuda.synchronize()
+        g = m.params.grad.clone()
+        leaves = {n: m.params.c[n].float().detach().clone().requires_grad_(m.params.spec(n).trainable)
+                  for n in m.params.names()}
+        loss, _, _ = m.reference_loss(x.float(), y, leaves, bf16_activations=True)
+        loss.backward()
+        names = [n for n in m.params.names() if m.params.spec(n).trainable]
+        a = torch.cat([g[m.params.offsets[n]:m.params.offsets[n] + leaves[n].numel()] for n in names])
+        b = torch.cat([leaves[n].grad.flatten() for n in names])
+        res[fuse] = (float(sums[0]), float(loss), float(torch.dot(a, b) / (a.norm() * b.norm())), g)
+    (lf, rf, cf, gf), (lu, ru, cu, gu) = res[True], res[False]
+    assert abs(lf - lu) < 5e-3 * abs(lu), (lf, lu)
+    assert cf > 0.95 and cf > cu - 0.01, (cf, cu)
+    assert float(torch.dot(gf, gu) / (gf.norm() * gu.norm())) > 0.98
