@@ -20,3 +20,4 @@ from .utils import tracing as debugging  # noqa: E402  (tf.debugging.check_numer
 from .utils import tracing as profiler  # noqa: E402  (roctx ranges)
 from .train.graph import placeholder  # noqa: E402
 from .train.tape import GradientTape  # noqa: E402
+from .nn import reduce_mean, matmul, sigmoid, tanh  # noqa: E402  (tf.reduce_mean / tf.matmul / tf.sigmoid / tf.tanh)

@@ -10,9 +10,12 @@ Parity with /root/reference/distribute_training.py:39-110:
 * accuracy = mean(in_top_k(logits, labels, 1)).
 Variables keep TF names/layouts (kernel [in, out]) so checkpoints match the reference's keys.
 
-GPU path: bf16 MFMA GEMMs (gemm_conv.hip) with fused bias+ELU+Philox-dropout
-(elementwise.hip) and the fused xent/in_top_k kernel, gradients written straight into the
-flat fp32 gradient buffer. CPU path: fp32 PyTorch autograd (the plumbing config).
+GPU path (dtype="float32", the default — the reference trains in fp32): exact-fp32 MFMA GEMMs
+(gemm_f32.hip, v_mfma_f32_32x32x2_f32) on the fp32 master weights, fused bias+ELU+Philox-dropout
+and the fused xent/in_top_k kernel in fp32, gradients written straight into the flat fp32
+gradient buffer; a GPU step matches the CPU fp32 step to ~1e-6 relative. dtype="bfloat16" runs
+the bf16 MFMA GEMMs (gemm_conv.hip) on a bf16 compute copy instead. CPU path: fp32 PyTorch
+autograd (the plumbing config).
 """
 from __future__ import annotations
 
@@ -48,8 +51,12 @@ class MLP:
 
     def __init__(self, layer_hidden_nums: Sequence[int] = (200, 100, 50, 25, 10), input_dim: int = 784,
                  dropout_rate: float = 0.01, regularizer_scale: float = 0.01, apply_regularization: bool = False,
-                 training: bool = True, device="cpu", seed: int = 0, activation: str = "elu"):
+                 training: bool = True, device="cpu", seed: int = 0, activation: str = "elu",
+                 dtype: str = "float32"):
         self.device = torch.device(device)
+        if dtype not in ("float32", "bfloat16"):
+            raise ValueError("MLP dtype must be float32 or bfloat16, got %r" % (dtype,))
+        self.bf16 = dtype == "bfloat16" and self.device.type == "cuda"
         self.sizes = [input_dim] + list(layer_hidden_nums)
         self.names = ["hidden%d" % (i + 1) for i in range(len(layer_hidden_nums) - 1)] + ["output"]
         self.dropout_rate = float(dropout_rate)
@@ -63,7 +70,7 @@ class MLP:
             specs.append(ParamSpec(n + "/kernel", (fi, fo), variance_scaling_init(fi), True))
             specs.append(ParamSpec(n + "/bias", (fo,), zeros_init, False))
         self.params = FlatParams(specs, self.device, seed=seed,
-                                 compute_dtype=torch.bfloat16 if self.device.type == "cuda" else None)
+                                 compute_dtype=torch.bfloat16 if self.bf16 else None)
         self._seed = int(seed) * 7919 + 17
         self._offset = 0
 
@@ -123,7 +130,15 @@ class MLP:
         B = x.shape[0]
         if grad_scale is None:
             grad_scale = 1.0 / B
-        a = K.f32_to_bf16(x.float().contiguous())
+        x = x.float().contiguous()
+        if self.bf16:
+            a = K.f32_to_bf16(x)
+            W = P.c
+            mm = G.gemm
+        else:
+            a = x
+            W = P.var
+            mm = G.gemm_f32
         act = K.ACT_ELU if self.activation == "elu" else K.ACT_RELU
         rate = self.dropout_rate if self.training else 0.0
         seed = self._seed
@@ -132,9 +147,9 @@ class MLP:
         L = len(self.names)
         for i, n in enumerate(self.names):
             if i == L - 1:
-                logits = G.gemm(acts[-1], P.c[n + "/kernel"], bias=P.var[n + "/bias"])
+                logits = mm(acts[-1], W[n + "/kernel"], bias=P.var[n + "/bias"])
                 break
-            z = G.gemm(acts[-1], P.c[n + "/kernel"])
+            z = mm(acts[-1], W[n + "/kernel"])
             off = self._offset
             self._offset += 1
             a = K.bias_act_dropout(z, P.var[n + "/bias"], act, rate, seed, off)
@@ -148,14 +163,14 @@ class MLP:
             a_in = acts[i]
             if i < L - 1:
                 d = K.bias_act_dropout_bwd(d, pres[i], P.var[n + "/bias"], act, rate, seed, offs[i])
-            G.gemm(a_in, d, trans_a=True, out=P.g[n + "/kernel"])
+            mm(a_in, d, trans_a=True, out=P.g[n + "/kernel"])
             K.colsum(d, out=P.g[n + "/bias"])
             if self.apply_regularization and i < L - 1:
                 P.g[n + "/kernel"].add_(self.regularizer_scale * grad_scale * B * torch.sign(P.var[n + "/kernel"]))
             if grad_hook is not None:
                 grad_hook(n + "/bias")
             if i > 0:
-                d = G.gemm(d, P.c[n + "/kernel"], trans_b=True)
+                d = mm(d, W[n + "/kernel"], trans_b=True)
         return {"loss": sums[0], "accuracy": sums[1]}
 
     def forward_backward(self, feed: Dict, grad_scale: Optional[float] = None, grad_hook=None):

@@ -57,6 +57,8 @@ _SIGS = {
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_conv_wgrad_bn": [P, P, P, P, G, P, P, I, I, I, I, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
+    # gemm_f32.hip
+    "ttdk_gemm_f32": [P, L, I, P, L, I, P, L, P, I, I, I, I, P],
     # pw_gemm.hip
     "ttdk_pw_rows": [I, I, I],
     "ttdk_pw_conv": [P, P, P, P, P, P, P, P, P, I, I, P, L, I, I, I, E, P],

@@ -145,6 +145,31 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     return out
 
 
+def gemm_f32(a, b, *, trans_a=False, trans_b=False, out=None, bias=None, beta=0):
+    """Exact-fp32 C = op(a) @ op(b) (+bias[N]) (+C if beta) on the f32 MFMA (gemm_f32.hip).
+
+    a: [M, K] (or [K, M] with trans_a); b: [K, N] (or [N, K] with trans_b); fp32 2-D with unit
+    column stride. The fp32 MatMul of the reference MLP (distribute_training.py:54,61)."""
+    _check2d(a, torch.float32, "a")
+    _check2d(b, torch.float32, "b")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else a.shape
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else b.shape
+    if K != Kb:
+        raise ValueError("gemm inner dims differ: %d vs %d" % (K, Kb))
+    if out is None:
+        if beta:
+            raise ValueError("beta=1 needs an out tensor")
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    elif out.dtype != torch.float32 or tuple(out.shape) != (M, N) or out.stride(-1) != 1:
+        raise ValueError("gemm_f32 out must be fp32 [%d, %d] row-major" % (M, N))
+    if bias is not None:
+        _check(bias, torch.float32, "bias")
+    _log("gemm_f32_%s%s" % ("t" if trans_a else "n", "t" if trans_b else "n"), M, N, K, 1)
+    _lib.call("ttdk_gemm_f32", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(), b.stride(0), int(trans_b),
+              out.data_ptr(), out.stride(0), _lib.ptr(bias), int(bool(beta)), M, N, K, _lib.stream())
+    return out
+
+
 def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
     """Split-K factor for a weight-gradient GEMM (long K = tokens, small M x N). Mirrors the
     launcher's kernel choice: the 256x256 LDS-DMA kernel (M, N >= 256, M*N >= 2^20, one

@@ -334,3 +334,225 @@ def sumsq(x, out=None):
     partial = torch.empty(2048, dtype=torch.float32, device=x.device)  # per-block partials (fixed-order fold)
     _lib.call("ttdk_sumsq", x.data_ptr(), x.numel(), out.data_ptr(), partial.data_ptr(), _s())
     return out
+
+
+# ------------------------------------------------------------------ shape-general ttd.nn kernels (nn_generic.hip)
+_lib.register({
+    "ttdk_col_stats_parts": [_lib.L, _lib.I],
+    "ttdk_col_stats": [_lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.L, _lib.I, _lib.P, _lib.I, _lib.P],
+    "ttdk_col_reduce2": [_lib.P, _lib.I, _lib.I, _lib.P, _lib.P, _lib.I, _lib.P],
+    "ttdk_col_affine": [_lib.P, _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.L, _lib.I, _lib.P],
+    "ttdk_bn_infer_coef": [_lib.P, _lib.P, _lib.P, _lib.P, _lib.F, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P],
+    "ttdk_bn_infer_bwd": [_lib.P, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P],
+    "ttdk_maxpool_generic_fwd": [_lib.P, _lib.P, _lib.P, _lib.I] + [_lib.I] * 12 + [_lib.P],
+    "ttdk_maxpool_generic_bwd": [_lib.P, _lib.P, _lib.P, _lib.I] + [_lib.I] * 12 + [_lib.P],
+    "ttdk_gap_fwd": [_lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P],
+    "ttdk_gap_bwd": [_lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P],
+    "ttdk_ln_generic_fwd": [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.L, _lib.I, _lib.F, _lib.P],
+    "ttdk_ln_generic_bwd_dx": [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.L, _lib.I, _lib.P],
+    "ttdk_gather_generic": [_lib.P, _lib.P, _lib.I, _lib.P, _lib.I, _lib.L, _lib.I, _lib.L, _lib.P],
+    "ttdk_scatter_add_generic": [_lib.P, _lib.P, _lib.I, _lib.P, _lib.I, _lib.L, _lib.I, _lib.L, _lib.P],
+    "ttdk_in_top_k": [_lib.P, _lib.P, _lib.I, _lib.P, _lib.I, _lib.L, _lib.I, _lib.I, _lib.P],
+    "ttdk_unary": [_lib.P, _lib.P, _lib.I, _lib.L, _lib.I, _lib.P],
+    "ttdk_unary_bwd": [_lib.P, _lib.P, _lib.P, _lib.I, _lib.L, _lib.I, _lib.P],
+})
+
+
+def _dt(*ts):
+    d = ts[0].dtype
+    for t in ts:
+        if t is not None and (t.dtype != d or not t.is_contiguous()):
+            raise ValueError("generic nn kernels need contiguous tensors of one dtype (got %s)"
+                             % [(x.dtype, x.is_contiguous()) for x in ts if x is not None])
+    if d not in _DT:
+        raise ValueError("generic nn kernels support float32/bfloat16, got %s" % d)
+    return _DT[d]
+
+
+def col_stats(a2d, b2d=None, mode=0, mu=None, rs=None):
+    """Per-row-block column sums: mode 0 (sum a, sum a^2), 1 (sum a, sum a*b), 2 (sum a,
+    sum a*(b-mu[r])*rs[r]). Returns (partial [T, 2, C], T)."""
+    M, C = a2d.shape
+    T = _lib.query("ttdk_col_stats_parts", M, C)
+    part = torch.empty((T, 2, C), dtype=torch.float32, device=a2d.device)
+    _lib.call("ttdk_col_stats", a2d.data_ptr(), _p(b2d), _p(mu), _p(rs), _dt(a2d, b2d), int(mode), M, C,
+              part.data_ptr(), T, _s())
+    return part, T
+
+
+def col_reduce2(part, T, o0=None, o1=None, accumulate=False):
+    C = part.shape[-1]
+    _lib.call("ttdk_col_reduce2", part.data_ptr(), T, C, _p(o0), _p(o1), int(accumulate), _s())
+    return o0, o1
+
+
+def col_affine(a, c0, b=None, c1=None, c2=None, out=None):
+    """out = a*c0[c] + b*c1[c] + c2[c] over the last (channel) axis."""
+    if out is None:
+        out = torch.empty_like(a)
+    _lib.call("ttdk_col_affine", a.data_ptr(), _p(b), _dt(a, b, out), c0.data_ptr(), _p(c1), _p(c2), out.data_ptr(),
+              a.numel(), a.shape[-1], _s())
+    return out
+
+
+def bn_infer_coef(mm, mv, gamma, beta, eps):
+    C = mm.numel()
+    buf = torch.empty((3, C), dtype=torch.float32, device=mm.device)
+    _lib.call("ttdk_bn_infer_coef", mm.data_ptr(), mv.data_ptr(), _p(gamma), _p(beta), float(eps), C,
+              buf[0].data_ptr(), buf[1].data_ptr(), buf[2].data_ptr(), _s())
+    return buf[0], buf[1], buf[2]
+
+
+def bn_infer_bwd(part, T, mm, rstd, dgamma, dbeta):
+    _lib.call("ttdk_bn_infer_bwd", part.data_ptr(), T, part.shape[-1], mm.data_ptr(), rstd.data_ptr(), _p(dgamma),
+              _p(dbeta), _s())
+
+
+def maxpool_generic_fwd(x, R, S, sh, sw, ph, pw, P, Q):
+    N, H, W, C = x.shape
+    y = torch.empty((N, P, Q, C), dtype=x.dtype, device=x.device)
+    arg = torch.empty((N, P, Q, C), dtype=torch.uint8, device=x.device)
+    _lib.call("ttdk_maxpool_generic_fwd", x.data_ptr(), y.data_ptr(), arg.data_ptr(), _dt(x), N, H, W, C, P, Q, R, S,
+              sh, sw, ph, pw, _s())
+    return y, arg
+
+
+def maxpool_generic_bwd(dy, arg, x_shape, R, S, sh, sw, ph, pw):
+    N, H, W, C = x_shape
+    P, Q = dy.shape[1], dy.shape[2]
+    dx = torch.empty(tuple(x_shape), dtype=dy.dtype, device=dy.device)
+    _lib.call("ttdk_maxpool_generic_bwd", dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), _dt(dy), N, H, W, C, P, Q, R,
+              S, sh, sw, ph, pw, _s())
+    return dx
+
+
+def gap_fwd(x):
+    N, H, W, C = x.shape
+    y = torch.empty((N, C), dtype=x.dtype, device=x.device)
+    _lib.call("ttdk_gap_fwd", x.data_ptr(), y.data_ptr(), _dt(x), N, H * W, C, _s())
+    return y
+
+
+def gap_bwd(dy, x_shape):
+    N, H, W, C = x_shape
+    dx = torch.empty(tuple(x_shape), dtype=dy.dtype, device=dy.device)
+    _lib.call("ttdk_gap_bwd", dy.data_ptr(), dx.data_ptr(), _dt(dy), N, H * W, C, _s())
+    return dx
+
+
+def ln_generic_fwd(x2d, gamma, beta, eps):
+    rows, H = x2d.shape
+    y = torch.empty_like(x2d)
+    stats = torch.empty((2, rows), dtype=torch.float32, device=x2d.device)
+    _lib.call("ttdk_ln_generic_fwd", x2d.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+              stats[0].data_ptr(), stats[1].data_ptr(), _dt(x2d), rows, H, float(eps), _s())
+    return y, stats[0], stats[1]
+
+
+def ln_generic_bwd(dy2d, x2d, gamma, mean, rstd, dgamma, dbeta, want_dx=True):
+    rows, H = x2d.shape
+    dx = None
+    if want_dx:
+        dx = torch.empty_like(x2d)
+        _lib.call("ttdk_ln_generic_bwd_dx", dy2d.data_ptr(), x2d.data_ptr(), gamma.data_ptr(), mean.data_ptr(),
+                  rstd.data_ptr(), dx.data_ptr(), _dt(dy2d, x2d), rows, H, _s())
+    part, T = col_stats(dy2d, x2d, mode=2, mu=mean, rs=rstd)
+    col_reduce2(part, T, o0=dbeta, o1=dgamma)
+    return dx
+
+
+def _ids(ids):
+    if ids.dtype not in (torch.int32, torch.int64) or not ids.is_contiguous():
+        raise ValueError("ids must be a contiguous int32/int64 tensor")
+    return 1 if ids.dtype == torch.int64 else 0
+
+
+def gather_generic(table, ids):
+    V, H = table.shape
+    out = torch.empty(tuple(ids.shape) + (H,), dtype=table.dtype, device=table.device)
+    _lib.call("ttdk_gather_generic", table.data_ptr(), ids.data_ptr(), _ids(ids), out.data_ptr(), _dt(table),
+              ids.numel(), H, V, _s())
+    return out
+
+
+def scatter_add_generic(dy, ids, dtable):
+    V, H = dtable.shape
+    if dtable.dtype != torch.float32:
+        raise ValueError("scatter_add_generic accumulates into an fp32 table")
+    _lib.call("ttdk_scatter_add_generic", dy.data_ptr(), ids.data_ptr(), _ids(ids), dtable.data_ptr(), _dt(dy),
+              ids.numel(), H, V, _s())
+    return dtable
+
+
+def in_top_k(z, targets, k):
+    rows, V = z.shape
+    out = torch.empty(rows, dtype=torch.uint8, device=z.device)
+    _lib.call("ttdk_in_top_k", z.data_ptr(), targets.data_ptr(), _ids(targets), out.data_ptr(), _dt(z), rows, V, int(k),
+              _s())
+    return out
+
+
+UNARY_TANH, UNARY_SIGMOID = 0, 1
+
+
+def unary(x, op):
+    y = torch.empty_like(x)
+    _lib.call("ttdk_unary", x.data_ptr(), y.data_ptr(), _dt(x), x.numel(), int(op), _s())
+    return y
+
+
+def unary_bwd(dy, y, op):
+    dx = torch.empty_like(y)
+    _lib.call("ttdk_unary_bwd", dy.data_ptr(), y.data_ptr(), dx.data_ptr(), _dt(dy, y), y.numel(), int(op), _s())
+    return dx
+
+
+_lib.register({
+    "ttdk_sum_blocks": [_lib.L],
+    "ttdk_sum_all": [_lib.P, _lib.I, _lib.L, _lib.P, _lib.F, _lib.P, _lib.P],
+    "ttdk_fill_scaled": [_lib.P, _lib.I, _lib.L, _lib.P, _lib.F, _lib.P],
+    "ttdk_row_scale": [_lib.P, _lib.P, _lib.P, _lib.I, _lib.L, _lib.I, _lib.P],
+})
+
+
+def sum_all(x, scale=1.0):
+    """0-d tensor = scale * sum(x) (deterministic two-stage reduction), same dtype as x."""
+    n = x.numel()
+    ws = torch.empty(_lib.query("ttdk_sum_blocks", n), dtype=torch.float32, device=x.device)
+    out = torch.empty((), dtype=x.dtype, device=x.device)
+    _lib.call("ttdk_sum_all", x.data_ptr(), _dt(x), n, ws.data_ptr(), float(scale), out.data_ptr(), _s())
+    return out
+
+
+def fill_scaled(shape, g, scale, dtype):
+    dx = torch.empty(shape, dtype=dtype, device=g.device)
+    if g.dtype != dtype:
+        raise ValueError("fill_scaled: gradient dtype %s != %s" % (g.dtype, dtype))
+    _lib.call("ttdk_fill_scaled", dx.data_ptr(), _dt(dx), dx.numel(), g.data_ptr(), float(scale), _s())
+    return dx
+
+
+def row_scale(a2d, g):
+    rows, C = a2d.shape
+    out = torch.empty_like(a2d)
+    _lib.call("ttdk_row_scale", a2d.data_ptr(), g.data_ptr(), out.data_ptr(), _dt(a2d, out), rows, C, _s())
+    return out
+
+
+_lib.register({"ttdk_zero": [_lib.P, _lib.L, _lib.P], "ttdk_trace_marker": [_lib.I, _lib.P]})
+
+
+def zero_(t):
+    """t.zero_() through hipMemsetAsync on the current stream (contiguous CUDA tensors)."""
+    if not t.is_contiguous():
+        raise ValueError("zero_ needs a contiguous tensor")
+    _lib.call("ttdk_zero", t.data_ptr(), t.numel() * t.element_size(), _s())
+    return t
+
+
+def zeros(shape, dtype=torch.float32, device="cuda"):
+    return zero_(torch.empty(shape, dtype=dtype, device=device))
+
+
+def trace_marker(tag=0):
+    _lib.call("ttdk_trace_marker", int(tag), _s())

@@ -100,7 +100,11 @@ class FlatParams:
                     self.compute.copy_(self.master)
 
     def zero_grad(self):
-        self.grad.zero_()
+        if self.grad.is_cuda:
+            from ..ops import kernels as K
+            K.zero_(self.grad)  # hipMemsetAsync, no framework kernel
+        else:
+            self.grad.zero_()
 
     def valid_mask(self):
         """1.0 on trainable variable elements, 0.0 on alignment padding / non-trainables."""
@@ -225,8 +229,13 @@ class FlatOptimizer:
         return self.p.device.type == "cuda"
 
     def seg_wd(self):
-        _, _, mask = self.p.chunk_table()
-        return mask * self.weight_decay
+        """Per-segment weight decay (cached: computed once, not per step)."""
+        c = getattr(self, "_seg_wd", None)
+        if c is None or c[0] != self.weight_decay:
+            _, _, mask = self.p.chunk_table()
+            c = (self.weight_decay, mask * self.weight_decay)
+            self._seg_wd = c
+        return c[1]
 
     def set_step(self, step: int):
         self.step_t.fill_(int(step))

@@ -80,17 +80,43 @@ def _reducer_for(strategy, flat):
 
 
 def _arm_hooks(flat):
+    """Post-accumulate-grad hooks on every trainable flat variable (installed once).
+
+    While a tape runs the backward, the variables' .grad is None, so autograd's AccumulateGrad
+    hands over the freshly computed gradient without an accumulate kernel; the hook moves it
+    into the variable's slice of the flat gradient buffer (a same-dtype device copy) and then
+    advances the all-reduce watermark."""
     if getattr(flat, "_ttd_hooks", None):
         return
     handles = []
     for name, p in getattr(flat, "_ttd_vars", {}).items():
         if p.requires_grad:
             def hook(param, name=name, flat=flat):
+                if getattr(flat, "_ttd_steal", False) and param.grad is not None:
+                    dst = flat.g[name]
+                    if param.grad.data_ptr() != dst.data_ptr():
+                        dst.copy_(param.grad)
+                    param.grad = None
                 tr = getattr(flat, "_ttd_tracker", None)
                 if tr is not None:
                     tr.hit(name)
             handles.append(p.register_post_accumulate_grad_hook(hook))
     flat._ttd_hooks = handles
+
+
+_ONES = {}
+
+
+def _seed_grad(target):
+    """d(target)/d(target) = 1 for a scalar target, cached per (dtype, device) so a steady-state
+    step launches no fill kernel for it."""
+    if target.numel() != 1:
+        return None
+    key = (target.dtype, target.device, tuple(target.shape))
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones(target.shape, dtype=target.dtype, device=target.device)
+    return t
 
 
 class GradientTape:
@@ -140,19 +166,28 @@ class GradientTape:
         st = _replica_strategy()
         reducers = []
         for fp in flats.values():
-            fp.grad.zero_()
+            fp.zero_grad()
             fp._ttd_aggregated = False
+            _arm_hooks(fp)
+            fp._ttd_steal = True
+            for p in getattr(fp, "_ttd_vars", {}).values():
+                p.grad = None
             if st is not None:
                 red = _reducer_for(st, fp)
                 red.begin()
-                _arm_hooks(fp)
                 fp._ttd_tracker = _ReadyTracker(fp, red)
                 reducers.append((fp, red))
+        seed = output_gradients if output_gradients is not None else _seed_grad(target)
         try:
-            target.backward(gradient=output_gradients, retain_graph=self.persistent)
+            target.backward(gradient=seed, retain_graph=self.persistent)
         finally:
-            for fp, _ in reducers:
+            for fp in flats.values():
+                fp._ttd_steal = False
                 fp._ttd_tracker = None
+                for name, p in getattr(fp, "_ttd_vars", {}).items():
+                    if p.grad is not None and p.grad.data_ptr() != fp.g[name].data_ptr():
+                        fp.g[name].copy_(p.grad)  # a variable without the hook (not trainable)
+                    p.grad = fp.g[name]
         for fp, red in reducers:
             red.finish()  # buckets not yet launched (unused variables) go now; waits for all
             fp._ttd_aggregated = True
