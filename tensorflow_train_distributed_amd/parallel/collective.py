@@ -19,6 +19,16 @@ Design for MI355X:
 * `finish()` makes the compute stream wait for the collectives (no host sync).
 
 Gradients are pre-scaled by 1/world (the loss gradient scale), so SUM == mean.
+
+Reduction algorithms (tf.distribute cross-device ops, strategy.py):
+* "allreduce"      one RCCL all-reduce per bucket (RcclAllReduce / NcclAllReduce);
+* "hierarchical"   reduce-scatter then all-gather per bucket — each rank reduces 1/world of the
+                   bucket, the two phases run back to back on the communicator's stream
+                   (HierarchicalCopyAllReduce; on one xGMI node both phases are per-link bound like
+                   the ring, it exists for its different bandwidth / latency split);
+* "reduce_to_one"  reduce to rank 0, then broadcast from it (ReductionToOneDevice).
+`num_packs` (TF's RcclAllReduce(num_packs)) splits the gradient buffer into that many
+equal-size buckets instead of the bucket_mb sizing.
 """
 from __future__ import annotations
 
@@ -29,13 +39,22 @@ import torch
 import torch.distributed as dist
 
 
+ALGORITHMS = ("allreduce", "hierarchical", "reduce_to_one")
+
+
 class BucketedAllReducer:
     def __init__(self, flat, group=None, bucket_mb: float = 32.0, first_bucket_mb: float = 4.0,
-                 compress_bf16: bool = False):
+                 compress_bf16: bool = False, algorithm: str = "allreduce", num_packs: Optional[int] = None):
+        if algorithm not in ALGORITHMS:
+            raise ValueError("unknown all-reduce algorithm %r (one of %s)" % (algorithm, ALGORITHMS))
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.compress = compress_bf16
+        self.algorithm = algorithm
+        if num_packs is not None and num_packs > 0:
+            # TF num_packs: that many (roughly equal) buckets over the whole gradient buffer
+            bucket_mb = first_bucket_mb = max(flat.numel * 4 / num_packs, 4.0) / (1 << 20)
         ends = []  # end offset (exclusive) of each variable, in layout order
         for s in flat.specs:
             o = flat.offsets[s.name]
@@ -60,6 +79,7 @@ class BucketedAllReducer:
         self._bucket_ends = [b[1] for b in self.buckets]
         self._next = 0
         self._works = []
+        self._keep = []
         self.launch_log: List[int] = []
 
     def bytes_per_step(self) -> int:
@@ -69,6 +89,7 @@ class BucketedAllReducer:
     def begin(self):
         self._next = 0
         self._works = []
+        self._keep = []
         self.launch_log = []
 
     def _launch(self, i):
@@ -77,13 +98,39 @@ class BucketedAllReducer:
         self.launch_log.append(i)
         if self.world == 1:
             return
-        if self.compress:
-            c = t.to(torch.bfloat16)
+        c = t.to(torch.bfloat16) if self.compress else t
+        if self.algorithm == "allreduce":
             w = dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self._works.append((w, c, t))
-        else:
-            w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self._works.append((w, None, None))
+        elif self.algorithm == "reduce_to_one":
+            # ops on one communicator run in issue order (RCCL: one stream); gloo's worker
+            # threads need the reduce finished before the broadcast reads rank 0's result
+            w = dist.reduce(c, dst=0, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if not self._ordered():
+                w.wait()
+            w = dist.broadcast(c, src=0, group=self.group, async_op=True)
+        else:  # hierarchical: reduce-scatter + all-gather over a world-divisible staging buffer
+            n = c.numel()
+            per = -(-n // self.world)
+            if per * self.world == n:
+                buf = c
+            else:
+                buf = torch.zeros(per * self.world, dtype=c.dtype, device=c.device)
+                buf[:n].copy_(c)
+            part = torch.empty(per, dtype=c.dtype, device=c.device)
+            w = dist.reduce_scatter_tensor(part, buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if not self._ordered():
+                w.wait()
+            w = dist.all_gather_into_tensor(buf, part, group=self.group, async_op=True)
+            self._keep.append(part)  # alive until the collective completed (finish)
+            if buf is not c:
+                self._works.append((w, buf[:n], t))
+                return
+        self._works.append((w, c if c is not t else None, t if c is not t else None))
+
+    def _ordered(self) -> bool:
+        """Whether async collectives of this group complete in issue order (RCCL's single
+        communicator stream) — gloo runs them on a thread pool."""
+        return dist.get_backend(self.group) == "nccl"
 
     def mark_ready(self, name: str):
         """All gradients up to and including variable `name` are final."""
@@ -111,6 +158,7 @@ class BucketedAllReducer:
                 raise as_preemption_error(e) from e
             if c is not None:
                 t.copy_(c)
+        self._keep = []
 
 
 def allreduce_mean_(tensor: torch.Tensor, group=None):

@@ -46,26 +46,49 @@ class CommunicationOptions:
 
 
 class CrossDeviceOps:
-    """Gradient aggregation policy: bucket size (MB) and optional bf16 compression."""
+    """Gradient aggregation policy (tf.distribute cross-device ops): reduction algorithm, bucket
+    sizing (bucket_mb, or TF's num_packs = number of equal buckets) and optional bf16 compression
+    on the wire. The algorithms are parallel/collective.py's BucketedAllReducer ALGORITHMS."""
 
-    def __init__(self, bucket_mb: float = 32.0, first_bucket_mb: float = 4.0, compress_bf16: bool = False):
+    algorithm = "allreduce"
+
+    def __init__(self, bucket_mb: float = 32.0, first_bucket_mb: float = 4.0, compress_bf16: bool = False,
+                 num_packs: Optional[int] = None):
         self.bucket_mb = bucket_mb
         self.first_bucket_mb = first_bucket_mb
         self.compress_bf16 = compress_bf16
-
-
-class RcclAllReduce(CrossDeviceOps):
-    def __init__(self, num_packs: int = 1, bucket_mb: float = 32.0, **kw):
-        super().__init__(bucket_mb=bucket_mb, **kw)
         self.num_packs = num_packs
 
 
+class RcclAllReduce(CrossDeviceOps):
+    """One RCCL all-reduce per bucket. num_packs=None keeps the overlap-oriented bucket sizing
+    (first bucket small so communication starts early); num_packs=k packs the gradients into
+    k equal buckets (TF semantics)."""
+
+    def __init__(self, num_packs: Optional[int] = None, bucket_mb: float = 32.0, **kw):
+        super().__init__(bucket_mb=bucket_mb, num_packs=num_packs, **kw)
+
+
 NcclAllReduce = RcclAllReduce
-HierarchicalCopyAllReduce = RcclAllReduce
+
+
+class HierarchicalCopyAllReduce(CrossDeviceOps):
+    """Reduce-scatter + all-gather per bucket (each replica reduces its 1/N shard)."""
+
+    algorithm = "hierarchical"
+
+    def __init__(self, num_packs: Optional[int] = None, **kw):
+        super().__init__(num_packs=num_packs, **kw)
 
 
 class ReductionToOneDevice(CrossDeviceOps):
-    pass
+    """Reduce every bucket onto replica 0, then broadcast it back (TF's ReductionToOneDevice)."""
+
+    algorithm = "reduce_to_one"
+
+    def __init__(self, reduce_to_device=None, accumulation_fn=None, **kw):
+        super().__init__(**kw)
+        self.reduce_to_device = reduce_to_device
 
 
 _tls = threading.local()
@@ -180,7 +203,7 @@ class Strategy:
         broadcast_flat_(params, group=self.group)
         c = self.cross_device_ops
         return BucketedAllReducer(params, group=self.group, bucket_mb=c.bucket_mb, first_bucket_mb=c.first_bucket_mb,
-                                  compress_bf16=c.compress_bf16)
+                                  compress_bf16=c.compress_bf16, algorithm=c.algorithm, num_packs=c.num_packs)
 
     def grad_scale(self, feed) -> float:
         n = None
@@ -393,7 +416,14 @@ class ParameterServerStrategy(Strategy):
         from .ps import replica_device_setter
         cr = cluster_resolver or TFConfigClusterResolver()
         self.cluster = cr.cluster_spec()
-        dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        # one worker process per GPU: a launcher's LOCAL_RANK, else the task index over the
+        # node's GPUs (the same mapping as examples/distribute_training.py --device gpu)
+        if torch.cuda.is_available():
+            n = max(1, torch.cuda.device_count())
+            dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", cr.task_id % n)))
+            torch.cuda.set_device(dev)
+        else:
+            dev = torch.device("cpu")
         super().__init__(dev)
         self.cluster_resolver = cr
         self.device_setter = replica_device_setter(cluster=self.cluster,

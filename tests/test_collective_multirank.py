@@ -32,7 +32,7 @@ def _spawn(fn, world, tmp_path, *args):
     return sorted(res, key=lambda r: r["rank"])
 
 
-def _reducer_worker(rank, world, store, q, compress):
+def _reducer_worker(rank, world, store, q, compress, algorithm="allreduce", num_packs=None):
     torch.set_num_threads(1)
     import torch.distributed as dist
     from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer
@@ -41,7 +41,8 @@ def _reducer_worker(rank, world, store, q, compress):
     # variables in backward-completion order; sizes so that several buckets form
     specs = [ParamSpec("v%d" % i, (n,), None, True) for i, n in enumerate([20000, 3, 120000, 5000, 250000, 17])]
     p = FlatParams(specs, "cpu", compute_dtype=None)
-    red = BucketedAllReducer(p, bucket_mb=0.6, first_bucket_mb=0.2, compress_bf16=compress)
+    red = BucketedAllReducer(p, bucket_mb=0.6, first_bucket_mb=0.2, compress_bf16=compress, algorithm=algorithm,
+                             num_packs=num_packs)
     g = torch.Generator().manual_seed(100 + rank)
     # each rank's gradient, pre-scaled by 1/world (zero in the alignment padding between variables)
     local = torch.randn(p.numel, generator=g) / world * p.valid_mask()
@@ -79,6 +80,29 @@ def test_bucketed_allreduce_mean_and_order(tmp_path, compress):
         if not compress:  # every replica holds the same result (gloo's bf16 sums may round per rank)
             assert torch.equal(r["grad"], res[0]["grad"])
     assert res[0]["bytes"] == buckets[-1][1] * (2 if compress else 4)
+
+
+@pytest.mark.parametrize("algorithm,num_packs", [("hierarchical", None), ("reduce_to_one", None),
+                                                 ("allreduce", 2), ("hierarchical", 3)])
+def test_cross_device_ops_algorithms_give_the_mean(tmp_path, algorithm, num_packs):
+    """HierarchicalCopyAllReduce (reduce-scatter + all-gather, ragged buckets padded),
+    ReductionToOneDevice (reduce to rank 0 + broadcast) and RcclAllReduce(num_packs=k)."""
+    world = 3
+    res = _spawn(_reducer_worker, world, tmp_path, False, algorithm, num_packs)
+    buckets = res[0]["buckets"]
+    if num_packs:
+        assert len(buckets) == num_packs
+    mean = sum(r["local"] for r in res)
+    for r in res:
+        torch.testing.assert_close(r["grad"], mean, rtol=1e-6, atol=1e-7)
+        assert torch.equal(r["grad"], res[0]["grad"])
+
+
+def test_strategy_cross_device_ops_classes_select_algorithms():
+    from tensorflow_train_distributed_amd.parallel import strategy as S
+    assert S.HierarchicalCopyAllReduce(num_packs=2).algorithm == "hierarchical"
+    assert S.ReductionToOneDevice().algorithm == "reduce_to_one"
+    assert S.NcclAllReduce is S.RcclAllReduce and S.RcclAllReduce(num_packs=4).num_packs == 4
 
 
 def _mlp_worker(rank, world, store, q):
