@@ -96,6 +96,11 @@ class ResNet:
         self.fuse_pw = os.environ.get("TTD_FUSE_PW", "1") != "0" and precision == "bf16"
         # individual switches (A/B and debugging): plain pw forward, c2->c3, c3->next c1, dgrad
         self.pw_parts = {"plain": True, "c23": True, "c31": True, "dgrad": True}
+        # halo-tiled 3x3 kernel (ops.gemm.conv3_halo) for the shapes it is compiled for, with the
+        # producing BN apply / BN backward fused in as its operand prologue; TTD_FUSE_C3=0: off
+        self.fuse_c3 = os.environ.get("TTD_FUSE_C3", "1") != "0" and precision == "bf16"
+        # data gradient on the halo kernel: off until it beats bwd-apply + conv_dgrad (tools/conv3_bench.py)
+        self.c3_dgrad = os.environ.get("TTD_C3_DGRAD", "0") != "0"
         self._wgrad_stream = None
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -234,6 +239,12 @@ class ResNet:
         return (self.fuse_pw and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0
                 and (c.cout, c.cin_store) in self.PW_DGRAD_SHAPES and G.pw_ok(1 << 20, c.cin_store, c.cout))
 
+    def _c3_ok(self, c: ConvSpec, H: int, W: int) -> bool:
+        """3x3/s1 conv on the halo kernel (its input is H x W)."""
+        from ..ops import gemm as G
+        return (self.fuse_c3 and self.device.type == "cuda" and c.k == 3 and c.stride == 1 and c.pad == 1
+                and G.conv3_rows(H, W, c.cin_store, c.cout) > 0)
+
     def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False, pool=False, defer=False,
                     residual_bn=None, pro=None):
         """conv + BN (+residual) (+ReLU). x8 = (fp8 copy of x, its scale slot) selects the fp8
@@ -263,7 +274,15 @@ class ResNet:
             bm, bn = 256, big  # 256-row LDS-DMA kernel (BN stat rows per 256-pixel tile)
         T = -(-M // bm)
         partial = None
-        if pro is not None or (not use8 and self._pw_part("plain") and self._pw_fwd_ok(c, False)):
+        if not use8 and self._c3_ok(c, H, W):
+            w4 = P.c[c.name + "_conv/kernel"]
+            if pro is not None:
+                psc, psh, _, _, side, side_mask = pro
+                y, partial, T = G.conv3_halo(x, w4, prologue=("bn_fwd", psc, psh, side, side_mask), stat=True)
+                x = side  # the unit's input as the backward needs it
+            else:
+                y, partial, T = G.conv3_halo(x, w4, stat=True)
+        elif pro is not None or (not use8 and self._pw_part("plain") and self._pw_fwd_ok(c, False)):
             w2 = P.c[c.name + "_conv/kernel"].view(c.cout, c.cin_store)
             if pro is not None:
                 psc, psh, pres, pres_bn, side, side_mask = pro
@@ -350,6 +369,20 @@ class ResNet:
             bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
             out, partial, T = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, dz), bn_stat=(fy, fmask),
                                         out=dx, beta=dx_beta if dx is not None else 0, beta_s2=bs2)
+            self._wgrad(c, x, dz, wname)
+            return out, (partial, T)
+        if (need_dx and dstat is not None and feeds is not None and feeds2 is None and dx is None
+                and self.fuse_bn_bwd and self.c3_dgrad and self._c3_ok(c, x.shape[1], x.shape[2])):
+            # halo 3x3 data gradient with this unit's BN backward as its operand prologue (dz is
+            # written once there for the weight gradient) and the feeding unit's BN-backward
+            # statistics in its epilogue
+            coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
+                                      dstat[0], dstat[1])
+            dz = torch.empty_like(y)
+            wt = K.krsc_to_crsk(P.c[wname])
+            _, fy, fmask, _ = feeds
+            out, partial, T = G.conv3_halo(dout, wt, flip=True, prologue=("bn_bwd", y, None, coef, dz),
+                                           bn_stat=(fy, fmask))
             self._wgrad(c, x, dz, wname)
             return out, (partial, T)
         if dstat is not None:
@@ -456,13 +489,16 @@ class ResNet:
             nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
             side = self._wgrad_stream
             c1 = None
+            # c2 on the halo kernel: c1's BN apply + ReLU run inside c2's operand load
+            c3ok = not fp8 and self._c3_ok(blk["c2"], h.shape[1] if pend is None else pend[0].shape[1],
+                                           h.shape[2] if pend is None else pend[0].shape[2])
             if pend is not None:
                 # this block's input h = relu(bn3(y3) + shortcut) is produced by c1's operand load
                 y3p, stp, resp, resbnp, ctxp = pend
                 h = torch.empty_like(y3p)
                 hm = torch.empty(h.numel() // 8, dtype=torch.uint8, device=h.device)
                 ctxp[2] = hm  # the producing unit's ReLU bits (its backward reads them)
-                o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm))
+                o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm), defer=c3ok)
                 pend = None
             if blk["cd"] is not None and side is not None:
                 # projection shortcut on the side stream, concurrent with the c1 -> c2 chain
@@ -475,17 +511,25 @@ class ResNet:
                 # h / h8 stay referenced (c1's ctx) past the join below; cd's outputs were made on
                 # the side stream, whose next work is always ordered after this step's main stream
             if c1 is None:
-                o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]))
+                o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]), defer=c3ok)
+            pro2 = None
+            if c3ok:
+                # o1 was returned raw (deferred BN): the halo kernel writes the applied o1 + bits
+                y1 = o1
+                o1 = torch.empty_like(y1)
+                c1[2] = torch.empty(o1.numel() // 8, dtype=torch.uint8, device=o1.device)
+                pro2 = (c1[3].scale, c1[3].shift, None, None, o1, c1[2])
+                o1 = y1  # c2's operand is the raw c1 output; _convbn_fwd swaps in the applied one
             fuse23 = self._pw_part("c23") and self._pw_fwd_ok(blk["c3"], True)
             if fuse23:
                 # c2's BN + ReLU are applied inside c3's operand load; o2 and its ReLU bits are
                 # written there (c3's weight gradient and c2's backward read them)
-                y2, c2, _ = unit(blk["c2"], o1, True, inp8=o1_8, defer=True)
+                y2, c2, _ = unit(blk["c2"], o1, True, inp8=o1_8, defer=True, pro=pro2)
                 o2 = torch.empty_like(y2)
                 c2[2] = torch.empty(o2.numel() // 8, dtype=torch.uint8, device=o2.device)
                 o2_8 = None
             else:
-                o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]))
+                o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]), pro=pro2)
             if blk["cd"] is not None and side is not None:
                 main.wait_stream(side)
             elif blk["cd"] is not None:

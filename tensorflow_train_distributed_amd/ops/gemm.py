@@ -145,6 +145,66 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     return out
 
 
+_C3 = _os.environ.get("TTD_CONV3", "1") != "0"
+
+
+def conv3_rows(H, W, C, N):
+    """Output pixels per tile of the halo 3x3 kernel (conv3_halo.hip) for a [*, H, W, C] -> N
+    3x3/s1/p1 conv, or 0 when the shape is not compiled in (or TTD_CONV3=0)."""
+    return int(_lib.query("ttdk_conv3_rows", int(H), int(W), int(C), int(N))) if _C3 else 0
+
+
+def conv3_halo(x, w, *, prologue=None, flip=False, out=None, stat=False, bn_stat=None):
+    """3x3 stride-1 pad-1 conv on the persistent halo kernel (conv3_halo.hip):
+    out[N, H, W, Co] = conv(A'(x), w) with A' from the prologue
+
+      None                                   A' = x
+      ("bn_fwd", scale, shift, side, mask)   A' = relu(x*scale + shift), stored into side (+ ReLU bits)
+      ("bn_bwd", y, mask, coef, side)        A' = coef[0]*(x . mask) + coef[1]*y + coef[2], stored into side
+
+    w: [Co, 3, 3, C] bf16 — the forward filter, or with flip=True the transposed filter
+    (K.krsc_to_crsk of the forward filter) of the conv whose data gradient this is.
+    stat=True: per-tile BN partial sums of the output -> (out, partial, T); bn_stat=(y, mask):
+    ReLU-masked gradient + BN-backward sums of the consuming unit -> (out, partial, T)."""
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.bfloat16, "w")
+    Nimg, H, W, C = x.shape
+    Co = w.shape[0]
+    if tuple(w.shape) != (Co, 3, 3, C):
+        raise ValueError("conv3_halo: filter must be [%d, 3, 3, %d], got %s" % (Co, C, tuple(w.shape)))
+    bm = conv3_rows(H, W, C, Co)
+    if not bm:
+        raise ValueError("conv3_halo: shape %s -> %d not compiled in" % (tuple(x.shape), Co))
+    if out is None:
+        out = torch.empty((Nimg, H, W, Co), dtype=torch.bfloat16, device=x.device)
+    T = Nimg * H * W // bm
+    partial = None
+    by = bmask = None
+    if stat or bn_stat is not None:
+        partial = torch.empty((T, 2, Co), dtype=torch.float32, device=x.device)
+    if bn_stat is not None:
+        by, bmask = bn_stat
+        _check(by, torch.bfloat16, "bn_stat y")
+    e = _epi(out, ldo=Co, stat=partial, by=by, bmask=bmask)
+    P = _lib.ptr
+    pro, x2, mask_in, s, b, side, side_mask = 0, None, None, None, None, None, None
+    if prologue is not None:
+        if prologue[0] == "bn_fwd":
+            _, s, b, side, side_mask = prologue
+            pro = 1
+        elif prologue[0] == "bn_bwd":
+            _, x2, mask_in, s, side = prologue
+            pro = 2
+        else:
+            raise ValueError("unknown prologue %r" % (prologue[0],))
+    _log("c3_%s" % ("dgrad" if flip else "fwd"), Nimg * H * W, Co, 9 * C)
+    _lib.call("ttdk_conv3_halo", x.data_ptr(), P(x2), P(mask_in), P(s), P(b), P(side), P(side_mask), pro, int(flip),
+              w.data_ptr(), Nimg, H, W, C, Co, ctypes.byref(e), _lib.stream())
+    if partial is not None:
+        return out, partial, T
+    return out
+
+
 def gemm_f32(a, b, *, trans_a=False, trans_b=False, out=None, bias=None, beta=0):
     """Exact-fp32 C = op(a) @ op(b) (+bias[N]) (+C if beta) on the f32 MFMA (gemm_f32.hip).
 

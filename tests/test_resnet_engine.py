@@ -176,21 +176,24 @@ def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
 
 
 @pytest.mark.gpu
-def test_resnet_streaming_pointwise_fusions_match_unfused_engine():
+@pytest.mark.parametrize("flag,size,batch", [("fuse_pw", 64, 16), ("fuse_c3", 224, 4)])
+def test_resnet_streaming_pointwise_fusions_match_unfused_engine(flag, size, batch):
     """The BN-prologue fusions on the streaming pointwise kernel (c2 apply -> c3 conv, c3 apply ->
     next c1 conv, c3 BN backward -> c3 dgrad) evaluate the same per-element expressions as the
     unfused engine; only accumulation order and fma contraction differ. A deep random-init net
     amplifies such rounding chaotically (tools/debug_pw_ab.py: both engines sit at the same
     distance from the fp32 oracle), so this compares both engines with the oracle on the shallow
-    net of the test above (stage 2 with two blocks: every fusion site is exercised)."""
+    net of the test above (stage 2 with two blocks: every fusion site is exercised). fuse_c3: the
+    halo 3x3 kernel with c1's BN apply / c2's BN backward as prologue (224-pixel input, so
+    stage 2 runs at its 56x56 shape)."""
     torch.manual_seed(0)
     stages = ((64, 2, 1), (128, 1, 2), (256, 1, 2), (512, 1, 2))
-    x = torch.randn(16, 64, 64, 3, device="cuda").bfloat16()
-    y = torch.randint(0, 100, (16,), device="cuda")
+    x = torch.randn(batch, size, size, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 100, (batch,), device="cuda")
     res = {}
     for fuse in (True, False):
         m = ResNet(stages, num_classes=100, device="cuda", seed=3)
-        m.fuse_pw = fuse
+        setattr(m, flag, fuse)
         sums = m.forward_backward(x, y)
         torch.cuda.synchronize()
         g = m.params.grad.clone()
