@@ -261,24 +261,28 @@ def main():
         use_graph = 0  # collectives are issued eagerly (bucket order follows backward)
     graph = None
     out = None
-    if use_graph:
-        from tensorflow_train_distributed_amd.utils.graphs import capture
-        for _ in range(2):
-            step()
-        sync()
-        graph, out = capture(step)
-        run = graph.replay
-    else:
-        run = step
     # The step (its main chain; the weight gradients stay on the engine's normal-priority side
     # stream) on a high-priority HIP stream: the main chain's small BN/reduce kernels are
     # dispatched ahead of the side stream's GEMM workgroups as CUs free up. A/B on one box:
     # ResNet-50 b1024 82.1 -> 81.4 ms (3 pairs); BERT 190.9 -> 191.8 ms, so auto = ResNet only.
     main_prio = os.environ.get("TTD_MAIN_PRIO", "auto")
     main_prio = (args.model == "resnet50") if main_prio == "auto" else main_prio != "0"
-    if main_prio and graph is None and not on_cpu:
+    prio = None
+    if main_prio and not on_cpu:
         prio = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
         prio.wait_stream(torch.cuda.current_stream())
+    if use_graph:
+        # the whole step (both streams: the side-stream weight-gradient chain forks from and
+        # joins the captured stream, so replay keeps the two branches concurrent) in one hipGraph
+        from tensorflow_train_distributed_amd.utils.graphs import capture
+        for _ in range(2):
+            step()
+        sync()
+        graph, out = capture(step, stream=prio)
+        run = graph.replay
+    else:
+        run = step
+    if prio is not None:
         inner = run
 
         def run():
@@ -321,6 +325,30 @@ def main():
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         replicas_in_sync = bool(lo.item() == hi.item())
+    # collective evidence for the scaling run: RCCL bus bandwidth of the gradient all-reduce at
+    # the bucket sizes the reducer uses and at the whole gradient buffer (after the timed region,
+    # on scratch copies: it does not touch the weights)
+    probe = None
+    red = getattr(step, "reducer", None)
+    if world > 1 and red is not None and not on_cpu and backend == "nccl":
+        probe = []
+        nbytes_all = red.flat.numel * 4
+        sizes = sorted({min(nbytes_all, 4 << 20), min(nbytes_all, int(args.bucket_mb * (1 << 20))), nbytes_all})
+        for nb in sizes:
+            buf = torch.zeros(nb // 4, dtype=torch.float32, device=dev)
+            dist.all_reduce(buf)
+            sync()
+            reps = 5
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                dist.all_reduce(buf)
+            e1.record()
+            sync()
+            t_ms = e0.elapsed_time(e1) / reps
+            probe.append({"bytes": nb, "ms": round(t_ms, 4),
+                          "busbw_GBps": round(2.0 * (world - 1) / world * nb / (t_ms * 1e-3) / 1e9, 1)})
+            del buf
     ms = elapsed / args.steps * 1e3
     rate = B * world * args.steps / elapsed
     if rank == 0:
@@ -337,6 +365,8 @@ def main():
             dinfo["allreduce_bytes_per_step"] = red.bytes_per_step() if world > 1 else 0
             dinfo["buckets"] = len(red.buckets)
             dinfo["allreduce_dtype"] = "bf16" if red.compress else "fp32"
+        if probe is not None:
+            dinfo["allreduce_probe"] = probe
         if backend == "nccl" and world > 1:
             try:
                 dinfo["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())

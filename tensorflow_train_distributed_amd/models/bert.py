@@ -75,12 +75,15 @@ def _trunc(std, rows=None):
         torch.nn.init.trunc_normal_(t, 0.0, std, -2 * std, 2 * std, generator=gen)
         if rows is not None:
             t[rows:] = 0.0
+    init.dev = (1, 0.0, float(std))  # device init: truncated normal (init.hip)
+    init.dev_zero_rows = rows
     return init
 
 
 def _fill(v):
     def init(t, gen):
         t.fill_(v)
+    init.dev = (3, float(v), 0.0)
     return init
 
 
@@ -129,7 +132,8 @@ class BertPretraining:
         self.cfg = cfg
         self.device = torch.device(device)
         self.dropout = dropout
-        self.params = FlatParams(self.build_specs(cfg), self.device, seed=seed)
+        self.params = FlatParams(self.build_specs(cfg), self.device, seed=seed,
+                                 device_init=os.environ.get("TTD_DEVICE_INIT", "1") != "0")
         P = self.params
         H, I, L = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
         for name_a, n, width in [("query/kernel", 3, H * H), ("query/bias", 3, H)]:

@@ -35,23 +35,28 @@ STAGES_50 = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
 
 
 def _he_init(fan_in):
+    std = math.sqrt(2.0 / fan_in) / 0.87962566103423978  # truncated-normal (+-2 sigma) correction
+
     def init(t, gen):
-        std = math.sqrt(2.0 / fan_in) / 0.87962566103423978  # truncated-normal (+-2 sigma) correction
         t.normal_(0.0, std, generator=gen)
         t.clamp_(-2 * std, 2 * std)
+    init.dev = (1, 0.0, std)  # device init: truncated normal (init.hip)
     return init
 
 
 def _fill(v):
     def init(t, gen):
         t.fill_(v)
+    init.dev = (3, float(v), 0.0)
     return init
 
 
 def _glorot(fan_in, fan_out):
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+
     def init(t, gen):
-        lim = math.sqrt(6.0 / (fan_in + fan_out))
         t.uniform_(-lim, lim, generator=gen)
+    init.dev = (2, -lim, lim)
     return init
 
 
@@ -123,7 +128,8 @@ class ResNet:
                 self.blocks.append(blk)
                 cin = mid * 4
         self.feat = cin
-        self.params = FlatParams(self._specs(), self.device, seed=seed)
+        self.params = FlatParams(self._specs(), self.device, seed=seed,
+                                 device_init=os.environ.get("TTD_DEVICE_INIT", "1") != "0")
         self._fp8 = None
         if precision == "fp8" and self.device.type == "cuda":
             self._init_fp8()

@@ -556,3 +556,19 @@ def zeros(shape, dtype=torch.float32, device="cuda"):
 
 def trace_marker(tag=0):
     _lib.call("ttdk_trace_marker", int(tag), _s())
+
+
+# ------------------------------------------------------------------ device initialisation (init.hip)
+_lib.register({"ttdk_init_random": [_lib.P, _lib.L, _lib.I, _lib.F, _lib.F, _lib.U64, _lib.U64, _lib.P]})
+
+INIT_NORMAL, INIT_TRUNCATED, INIT_UNIFORM, INIT_CONSTANT = 0, 1, 2, 3
+
+
+def init_random_(t, dist, a, b=0.0, seed=0, offset=0):
+    """Fill contiguous fp32 CUDA tensor t on the device: normal(a, b), truncated normal(a, b)
+    (+-2 b, resampled), uniform[a, b) or constant a — a pure function of (seed, offset, index)."""
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise ValueError("init_random_ needs a contiguous fp32 tensor")
+    _lib.call("ttdk_init_random", t.data_ptr(), t.numel(), int(dist), float(a), float(b), int(seed) & (2**64 - 1),
+              int(offset) & (2**64 - 1), _s())
+    return t

@@ -43,7 +43,8 @@ class ParamSpec:
 
 
 class FlatParams:
-    def __init__(self, specs: List[ParamSpec], device, compute_dtype=torch.bfloat16, seed: int = 0):
+    def __init__(self, specs: List[ParamSpec], device, compute_dtype=torch.bfloat16, seed: int = 0,
+                 device_init: bool = False):
         self.device = torch.device(device)
         self.specs = list(specs)
         self.offsets: Dict[str, int] = {}
@@ -70,9 +71,20 @@ class FlatParams:
                 self.c[s.name] = self.compute[o:o + n].view(shape)
         gen = torch.Generator(device="cpu")
         gen.manual_seed(seed)
+        # device_init: initialisers that describe their distribution (`init.dev` = (dist, a, b),
+        # see models/resnet.py) run as the Philox init kernel on the GPU (init.hip), keyed by
+        # (seed, variable index) — no host RNG or host->device copy of the whole model
+        on_dev = device_init and self.device.type == "cuda"
         with torch.no_grad():
-            for s in self.specs:
-                if s.init is not None:
+            for i, s in enumerate(self.specs):
+                dev = getattr(s.init, "dev", None) if on_dev else None
+                if dev is not None:
+                    from ..ops import kernels as K
+                    K.init_random_(self.var[s.name], dev[0], dev[1], dev[2], seed=seed, offset=i)
+                    rows = getattr(s.init, "dev_zero_rows", None)
+                    if rows is not None:
+                        self.var[s.name][rows:].zero_()
+                elif s.init is not None:
                     t = torch.empty(tuple(s.shape), dtype=torch.float32)
                     s.init(t, gen)
                     self.var[s.name].copy_(t)
