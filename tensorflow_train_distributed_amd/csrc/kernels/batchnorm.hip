@@ -611,6 +611,15 @@ TTDK_EXPORT int ttdk_bn_reduce_finalize(const float* partial, int T, int C, floa
   FinalizeArgs a{count, gamma, beta, eps, momentum, running_mean, running_var, mean, rstd, scale, shift,
                  dgamma, dbeta, coef, accumulate};
   const int cgr = (C + 31) / 32;
+  if (T <= 256) {
+    // few partial rows (persistent producers, small layers): the finalize folds them directly,
+    // in the same fixed order, one launch instead of two
+    if (bwd)
+      hipLaunchKernelGGL(finalize_kernel<true>, dim3(cgr), dim3(kThreads), 0, st, partial, T, C, a);
+    else
+      hipLaunchKernelGGL(finalize_kernel<false>, dim3(cgr), dim3(kThreads), 0, st, partial, T, C, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(reduce_slices_kernel, dim3(cgr, S), dim3(kThreads), 0, st, partial, T, C, per, slab);
   if (bwd)
     hipLaunchKernelGGL(finalize_kernel<true>, dim3(cgr), dim3(kThreads), 0, st, slab, S, C, a);

@@ -65,14 +65,14 @@ __device__ __forceinline__ int slot_chunk(int q) { return (q >> 3) % CP; }
 template <int CP>
 __device__ __forceinline__ int slot_pix(int q) { return (q & 7) + 8 * (q / (8 * CP)); }
 
-template <int C, int BN, int TH, int W, int PRO, bool FLIP>
+template <int C, int BN, int TH, int W, int PRO, bool FLIP, int WM>
 __global__ __launch_bounds__(THR, 1) void conv3_kernel(Pro pa, const bf16_t* __restrict__ w, EpiParams E, int H,
                                                       int N, int tiles, int nslices) {
   constexpr int BM = TH * W;              // output pixels per tile
   constexpr int HR = TH + 2, HC = W + 2;  // halo rows / cols
   constexpr int CP = C / 8;               // 16-B chunks per pixel
   constexpr int KT = 9 * C;               // reduction length
-  constexpr int WM = 4, WN = 2;
+  constexpr int WN = NW / WM;
   constexpr int WR = BM / WM, WC = BN / WN;
   constexpr int TM = WR / 16, TN = WC / 16;
   constexpr int NPIX = HR * HC;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(THR, 1) void conv3_kernel(Pro pa, const bf16_t* __r
   }
 }
 
-template <int C, int BN, int TH, int W, int PRO, bool FLIP>
+template <int C, int BN, int TH, int W, int PRO, bool FLIP, int WM>
 hipError_t launch(const Pro& pa, const bf16_t* w, const EpiParams& E, int Nimg, int H, int N, hipStream_t st) {
   const int nsl = N / BN;
   const int tiles = Nimg * (H / TH);
@@ -271,21 +271,26 @@ hipError_t launch(const Pro& pa, const bf16_t* w, const EpiParams& E, int Nimg, 
   if (per_xcd < 1) per_xcd = 1;
   const int need = ceil_div(tiles, 8);
   if (per_xcd > need) per_xcd = need;
-  hipLaunchKernelGGL((conv3_kernel<C, BN, TH, W, PRO, FLIP>), dim3(8 * nsl * per_xcd), dim3(THR), 0, st, pa, w, E, H, N,
+  hipLaunchKernelGGL((conv3_kernel<C, BN, TH, W, PRO, FLIP, WM>), dim3(8 * nsl * per_xcd), dim3(THR), 0, st, pa, w, E, H, N,
                      tiles, nsl);
   return hipGetLastError();
 }
 
-// the shapes compiled in: (C, N, W) -> TH
-inline int pick_th(int C, int N, int W) {
-  if (C == 64 && N == 64 && W == 56) return 8;
+// the shapes compiled in: (C, N, W, prologue) -> TH. The BN-backward prologue holds two
+// prefetched halos (gradient + BN input) in registers, so it takes 4-row tiles (8 waves as
+// 2 x 4): the 8-row configuration spilled them to scratch.
+inline int pick_th(int C, int N, int W, int pro) {
+  if (C == 64 && N == 64 && W == 56) return pro == 2 ? 4 : 8;
   return 0;
 }
 
 template <int PRO, bool FLIP>
 hipError_t dispatch(const Pro& pa, const bf16_t* w, const EpiParams& E, int Nimg, int H, int W, int C, int N,
                     hipStream_t st) {
-  if (C == 64 && N == 64 && W == 56) return launch<64, 64, 8, 56, PRO, FLIP>(pa, w, E, Nimg, H, N, st);
+  if (C == 64 && N == 64 && W == 56) {
+    if constexpr (PRO == 2) return launch<64, 64, 4, 56, PRO, FLIP, 2>(pa, w, E, Nimg, H, N, st);
+    else return launch<64, 64, 8, 56, PRO, FLIP, 4>(pa, w, E, Nimg, H, N, st);
+  }
   return hipErrorInvalidValue;
 }
 
@@ -297,8 +302,8 @@ using namespace ttdk;
 
 // Output rows per tile (= BN partial-statistics row count divisor) of ttdk_conv3_halo for a
 // [*, H, W, C] -> N 3x3/s1/p1 conv, or 0 when the shape is not compiled in.
-TTDK_EXPORT int ttdk_conv3_rows(int H, int W, int C, int N) {
-  const int th = c3::pick_th(C, N, W);
+TTDK_EXPORT int ttdk_conv3_rows(int H, int W, int C, int N, int pro) {
+  const int th = c3::pick_th(C, N, W, pro);
   return (th && H % th == 0) ? th * W : 0;
 }
 
@@ -309,7 +314,7 @@ TTDK_EXPORT int ttdk_conv3_rows(int H, int W, int C, int N) {
 TTDK_EXPORT int ttdk_conv3_halo(const bf16_t* x, const bf16_t* x2, const uint8_t* mask_in, const float* s,
                                 const float* b, bf16_t* side, uint8_t* side_mask, int pro, int flip, const bf16_t* w,
                                 int Nimg, int H, int W, int C, int N, const TtdkEpilogue* epi, hipStream_t st) {
-  const int th = c3::pick_th(C, N, W);
+  const int th = c3::pick_th(C, N, W, pro);
   if (!th || H % th || (reinterpret_cast<uintptr_t>(x) & 15) || pro < 0 || pro > 2) return hipErrorInvalidValue;
   const EpiParams e = to_epi(epi);
   if (e.mode != 0 || e.remap || e.bH || e.ldo != N || e.residual || e.by2) return hipErrorInvalidValue;

@@ -60,7 +60,7 @@ _SIGS = {
     # gemm_f32.hip
     "ttdk_gemm_f32": [P, L, I, P, L, I, P, L, P, I, I, I, I, P],
     # conv3_halo.hip
-    "ttdk_conv3_rows": [I, I, I, I],
+    "ttdk_conv3_rows": [I, I, I, I, I],
     "ttdk_conv3_halo": [P, P, P, P, P, P, P, I, I, P, I, I, I, I, I, E, P],
     # pw_gemm.hip
     "ttdk_pw_rows": [I, I, I],

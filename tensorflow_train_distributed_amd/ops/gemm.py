@@ -148,10 +148,11 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
 _C3 = _os.environ.get("TTD_CONV3", "1") != "0"
 
 
-def conv3_rows(H, W, C, N):
+def conv3_rows(H, W, C, N, pro=0):
     """Output pixels per tile of the halo 3x3 kernel (conv3_halo.hip) for a [*, H, W, C] -> N
-    3x3/s1/p1 conv, or 0 when the shape is not compiled in (or TTD_CONV3=0)."""
-    return int(_lib.query("ttdk_conv3_rows", int(H), int(W), int(C), int(N))) if _C3 else 0
+    3x3/s1/p1 conv with prologue `pro` (0 none, 1 BN forward, 2 BN backward), or 0 when the
+    shape is not compiled in (or TTD_CONV3=0)."""
+    return int(_lib.query("ttdk_conv3_rows", int(H), int(W), int(C), int(N), int(pro))) if _C3 else 0
 
 
 def conv3_halo(x, w, *, prologue=None, flip=False, out=None, stat=False, bn_stat=None):
@@ -172,7 +173,8 @@ def conv3_halo(x, w, *, prologue=None, flip=False, out=None, stat=False, bn_stat
     Co = w.shape[0]
     if tuple(w.shape) != (Co, 3, 3, C):
         raise ValueError("conv3_halo: filter must be [%d, 3, 3, %d], got %s" % (Co, C, tuple(w.shape)))
-    bm = conv3_rows(H, W, C, Co)
+    pro_code = 0 if prologue is None else {"bn_fwd": 1, "bn_bwd": 2}.get(prologue[0], -1)
+    bm = conv3_rows(H, W, C, Co, max(pro_code, 0))
     if not bm:
         raise ValueError("conv3_halo: shape %s -> %d not compiled in" % (tuple(x.shape), Co))
     if out is None:
