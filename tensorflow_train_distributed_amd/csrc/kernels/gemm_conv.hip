@@ -38,3 +38,18 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
 TTDK_EXPORT int ttdk_splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {
   return splitk_reduce(ws, splits, n, out, beta, st);
 }
+
+// Runtime switch of the split-K tail for wave-quantised 256-row GEMM launches (gemm_conv.h
+// big::launch); returns the previous setting.
+namespace ttdk_rt {
+int& tail_split_flag() {
+  static int on = getenv_int("TTD_TAIL_SPLIT", 0);
+  return on;
+}
+}  // namespace ttdk_rt
+
+TTDK_EXPORT int ttdk_set_tail_split(int on) {
+  const int old = ttdk_rt::tail_split_flag();
+  ttdk_rt::tail_split_flag() = on;
+  return old;
+}
