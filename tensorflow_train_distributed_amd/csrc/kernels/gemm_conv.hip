@@ -16,11 +16,14 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
   DenseParams pb{B, ldb, N, K};
   // 256-row LDS-DMA path for big GEMMs (explicit tile 256 forces it; 128/64 force the 4-wave kernel)
   const int bbn = big_bn(M, N, K);
-  const bool big_ok = vec && bbn && pe.remap == 0 && pe.stat == nullptr && (a_kmajor || M % 8 == 0);
+  // per-tile statistics rows follow the kernel's tile height: with `stat` the 256-row kernel runs
+  // only on an explicit bm == 256 request (the caller sized `stat` for 256-row tiles)
+  const bool big_ok = vec && bbn && pe.remap == 0 && (pe.stat == nullptr || bm == 256) && (a_kmajor || M % 8 == 0);
   if (big_ok && (bm == 256 || bm == 0)) {
     if (bbn == 256) return big::dense<256>(A, lda, a_kmajor, B, ldb, b_kmajor, pe, M, N, K, splits, st);
     return big::dense<128>(A, lda, a_kmajor, B, ldb, b_kmajor, pe, M, N, K, splits, st);
   }
+  if (bm == 256 && pe.stat) return hipErrorInvalidValue;  // asked for 256-row statistics rows, kernel not eligible
   if (bm == 256) bm = 0;
   if (bm == 0 || bn == 0) pick_tile(M, N, &bm, &bn);
   if (vec) {

@@ -1,0 +1,196 @@
+// Weight gradient of the ResNet stem (7x7 stride-2 pad-3 conv over the RGB image stored with 8
+// channels) with the stem BatchNorm's backward applied on the fly:
+//     dW[k][r][s][c] = sum_{n,p,q} dz[n,p,q,k] * x[n, 2p-3+r, 2q-3+s, c],
+//     dz = coef[0][k]*g + coef[1][k]*y + coef[2][k]           (c < 3; the padded channels get 0)
+//
+// Why (tools/op_timing.py): the generic im2col-gather GEMM ran this at 2.4 ms/step at batch
+// 1024 — it computes all 8 stored channels (5 of them zero padding, 62 % of its MFMA work),
+// its 392-wide column space leaves a 128-wide tile almost empty, and it is the last kernel of
+// the backward pass with nothing to overlap.
+//
+// Design (MI355X-first): persistent workgroups (4 waves, 3 per CU) walk bands of 8 half output
+// rows (56 pixels) of the 112x112 stem output. The 7 input rows a half row touches live in an
+// LDS ring, so each further output row of the band loads only its 2 new input rows (prefetched
+// into registers with the row's g / y one row ahead); the 56x64 dz block is formed from g and y in registers and stored
+// channel-major (the MFMA A operand, k = pixel), and the 147 real im2col columns (r, s, c<3)
+// are built channel-major from the staged rows (the B operand); 2 k-steps x 10 column blocks
+// of v_mfma_f32_16x16x32_bf16 per wave accumulate a 64 x 160 partial in registers across all
+// of the workgroup's rows. Partials go to a [workgroups][64][160] slab that a deterministic
+// split-K fold reduces, and a scatter writes dW in the [K][7][7][8] filter layout.
+#include "gemm_conv.h"
+
+namespace ttdk {
+namespace {
+namespace stem {
+
+constexpr int THR = 256;
+constexpr int QB = 56;            // output pixels per work item (half of a 112-pixel row)
+constexpr int KP = 64;            // k (pixels) padded to the MFMA step
+constexpr int XW = 2 * QB + 5;    // staged input columns per row
+constexpr int NC = 160;           // im2col columns: 7*7*3 = 147, padded to 10 MFMA blocks
+constexpr int KO = 64;            // output channels
+
+constexpr int BAND = 8;          // output rows per work unit (a ring of input rows is kept across them)
+constexpr int RING = 8;          // input-row slots (7 in use)
+
+__global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
+                                                            const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                                            float* __restrict__ ws, int N, int H, int W, int P, int Q,
+                                                            int units) {
+  __shared__ __attribute__((aligned(16))) char xs[RING * XW * 16];  // input rows h % RING: [col][8 ch] bf16
+  __shared__ __attribute__((aligned(16))) char sA[KO * 128];        // dz^T: [k_out][64 pixels] (kmaj)
+  __shared__ __attribute__((aligned(16))) char sB[NC * 128];        // im2col^T: [col][64 pixels] (kmaj)
+  __shared__ float cf[3 * KO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int halves = (Q + QB - 1) / QB;
+  const int bands = (P + BAND - 1) / BAND;
+  for (int i = tid; i < 3 * KO; i += THR) cf[i] = coef[i];
+  for (int c = tid; c < KO; c += THR)  // the padded pixel chunk (k = 56..63) of every dz^T row stays zero
+    *reinterpret_cast<uint4*>(sA + kmaj_off(c, QB / 8)) = make_uint4(0, 0, 0, 0);
+  f32x4_t acc[NC / 16];
+#pragma unroll
+  for (int b = 0; b < NC / 16; ++b) acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // one input row (XW 16-B pixels starting at column 2*q0-3, zero outside the image)
+  auto load_xpix = [&](int n, int h, int q0, int t) -> uint4 {
+    const int w = 2 * q0 - 3 + t;
+    return (h >= 0 && h < H && w >= 0 && w < W) ? ldg16(x + ((static_cast<long long>(n) * H + h) * W + w) * 8)
+                                                : make_uint4(0, 0, 0, 0);
+  };
+  // per output row: g / y chunks and the two input rows that row adds to the ring, prefetched
+  // into registers one row ahead
+  constexpr int NG = (QB * (KO / 8) + THR - 1) / THR;
+  constexpr int NX2 = (2 * XW + THR - 1) / THR;
+  uint4 pg[NG], py[NG], px[NX2];
+  auto prefetch = [&](int n, int p, int q0) {
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int c = tid + THR * i;
+      const int j = c / (KO / 8), cc = c % (KO / 8);
+      const bool ok = c < QB * (KO / 8) && q0 + j < Q;
+      const long long off = ((static_cast<long long>(n) * P + p) * Q + q0 + j) * KO + cc * 8;
+      pg[i] = ok ? ldg16(g + off) : make_uint4(0, 0, 0, 0);
+      py[i] = ok ? ldg16(y + off) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NX2; ++i) {
+      const int c = tid + THR * i;
+      const int rr = c / XW, t = c % XW;
+      px[i] = c < 2 * XW ? load_xpix(n, 2 * p + 2 + rr, q0, t) : make_uint4(0, 0, 0, 0);  // rows 2p+2, 2p+3
+    }
+  };
+
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const int half = u % halves, band = (u / halves) % bands, n = u / (halves * bands);
+    const int q0 = half * QB, p0 = band * BAND, p1 = min(P, p0 + BAND);
+    // first output row of the band: input rows 2p0-3 .. 2p0+1 directly (the last two come with
+    // the row's prefetch like every later row's two new rows)
+    for (int c = tid; c < 5 * XW; c += THR) {
+      const int rr = c / XW, t = c % XW;
+      const int h = 2 * p0 - 3 + rr;
+      *reinterpret_cast<uint4*>(xs + (((h + 8 * RING) % RING) * XW + t) * 16) = load_xpix(n, h, q0, t);
+    }
+    prefetch(n, p0, q0);
+    for (int p = p0; p < p1; ++p) {
+      // 1. stage: the row's two new input rows, dz^T (BN backward applied on the way)
+#pragma unroll
+      for (int i = 0; i < NX2; ++i) {
+        const int c = tid + THR * i;
+        if (c < 2 * XW) {
+          const int rr = c / XW, t = c % XW;
+          *reinterpret_cast<uint4*>(xs + (((2 * p + 2 + rr) % RING) * XW + t) * 16) = px[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const int c = tid + THR * i;
+        if (c >= QB * (KO / 8)) break;
+        const int j = c / (KO / 8), cc = c % (KO / 8);
+        float gf[8], yf[8];
+        unpack8(pg[i], gf);
+        unpack8(py[i], yf);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int k = cc * 8 + t;
+          const float f = cf[k] * gf[t] + cf[KO + k] * yf[t] + cf[2 * KO + k];
+          *reinterpret_cast<bf16_t*>(sA + kmaj_off(k, j >> 3) + (j & 7) * 2) = f2bf(f);
+        }
+      }
+      __syncthreads();
+      if (p + 1 < p1) prefetch(n, p + 1, q0);  // in flight under this row's im2col build and MFMAs
+      // 2. im2col^T: column (r, s, c<3) -> B[col][j] = input row 2p-3+r, column 2j+s (relative), channel c
+      for (int c = tid; c < NC * (KP / 8); c += THR) {
+        const int col = c / (KP / 8), kc = c % (KP / 8);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (col < 147) {
+          const int r = col / 21, rem = col % 21, s = rem / 3, ch = rem % 3;
+          const char* row = xs + (((2 * p - 3 + r + 8 * RING) % RING) * XW) * 16;
+          uint32_t w4[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int j0 = kc * 8 + 2 * t, j1 = j0 + 1;
+            const uint32_t lo = j0 < QB ? *reinterpret_cast<const bf16_t*>(row + ((2 * j0 + s) * 8 + ch) * 2) : 0u;
+            const uint32_t hi = j1 < QB ? *reinterpret_cast<const bf16_t*>(row + ((2 * j1 + s) * 8 + ch) * 2) : 0u;
+            w4[t] = lo | (hi << 16);
+          }
+          v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        *reinterpret_cast<uint4*>(sB + kmaj_off(col, kc)) = v;
+      }
+      __syncthreads();
+      // 3. wave w: output channels 16w..16w+15 x all 160 columns, K = 64 pixels
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t a = lds_read_b128(sA + kmaj_off(wave * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+#pragma unroll
+        for (int b = 0; b < NC / 16; ++b) {
+          const bf16x8_t bb = lds_read_b128(sB + kmaj_off(b * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[b], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // D[i][j]: i = output channel (A rows), j = column; lane holds rows 4*(lane>>4)+v, column lane&15
+  float* o = ws + static_cast<long long>(blockIdx.x) * KO * NC;
+#pragma unroll
+  for (int b = 0; b < NC / 16; ++b)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) o[(wave * 16 + 4 * (lane >> 4) + v) * NC + b * 16 + (lane & 15)] = acc[b][v];
+}
+
+// dW[k][r][s][c] (fp32, filter layout [64][7][7][8]) from the folded [64][160] sums
+__global__ void stem_scatter_kernel(const float* __restrict__ sums, float* __restrict__ dw, int beta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= KO * 49 * 8) return;
+  const int c = i % 8, rs = (i / 8) % 49, k = i / (8 * 49);
+  const float v = c < 3 ? sums[k * NC + (rs / 7) * 21 + (rs % 7) * 3 + c] : 0.f;
+  dw[i] = v + (beta ? dw[i] : 0.f);
+}
+
+}  // namespace stem
+}  // namespace
+}  // namespace ttdk
+
+using namespace ttdk;
+
+// Workgroups of ttdk_stem_wgrad (the caller's workspace holds workgroups*64*160 + 64*160 floats).
+TTDK_EXPORT int ttdk_stem_wgrad_blocks(int N, int P, int Q) {
+  const long long units = static_cast<long long>(N) * ((P + stem::BAND - 1) / stem::BAND) * ((Q + stem::QB - 1) / stem::QB);
+  const int want = 3 * 256;
+  return static_cast<int>(units < want ? units : want);
+}
+
+// x [N][H][W][8] (3 real channels), g / y [N][P][Q][64], coef [3][64] -> dw [64][7][7][8] fp32.
+TTDK_EXPORT int ttdk_stem_wgrad(const bf16_t* x, const bf16_t* g, const bf16_t* y, const float* coef, float* dw,
+                                float* ws, int N, int H, int W, int P, int Q, int beta, hipStream_t st) {
+  if (P != (H + 6 - 7) / 2 + 1 || Q != (W + 6 - 7) / 2 + 1 || N <= 0) return hipErrorInvalidValue;
+  const int units = N * ((P + stem::BAND - 1) / stem::BAND) * ((Q + stem::QB - 1) / stem::QB);
+  const int G = ttdk_stem_wgrad_blocks(N, P, Q);
+  hipLaunchKernelGGL(stem::stem_wgrad_kernel, dim3(G), dim3(stem::THR), 0, st, x, g, y, coef, ws, N, H, W, P, Q, units);
+  float* sums = ws + static_cast<long long>(G) * stem::KO * stem::NC;
+  hipError_t e = splitk_reduce(ws, G, static_cast<long long>(stem::KO) * stem::NC, sums, 0, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(stem::stem_scatter_kernel, dim3((stem::KO * 49 * 8 + 255) / 256), dim3(256), 0, st, sums, dw, beta);
+  return hipGetLastError();
+}

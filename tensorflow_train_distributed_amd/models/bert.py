@@ -150,6 +150,9 @@ class BertPretraining:
         # than the MN-major [out][in] read); refreshed each step on the side stream during the
         # forward pass (TTD_BERT_WT=0: off)
         self.transposed_dgrad = os.environ.get("TTD_BERT_WT", "1") != "0" and self.device.type == "cuda"
+        # FFN1 bias gradient from the dGELU dgrad epilogue column statistics instead of a colsum pass
+        # on the side stream (TTD_BERT_BIAS_STAT=1; measured neutral-to-slower: 190.4 vs 188.5 ms)
+        self.fuse_bias_grad = os.environ.get("TTD_BERT_BIAS_STAT", "0") != "0" and self.device.type == "cuda"
         self._wt = None
         if self.device.type == "cuda":
             from ..ops.transformer import RngState
@@ -296,16 +299,20 @@ class BertPretraining:
             side = self._side
 
         def wgrad_bias(dy, x, wout, bout):
+            """weight gradient (+ bias column sum unless bout is None: the producer's epilogue
+            already emitted it) on the side stream"""
             if side is None:
                 wgrad(dy, x, wout)
-                K.colsum(dy, out=bout)
+                if bout is not None:
+                    K.colsum(dy, out=bout)
                 return
             ev = torch.cuda.Event()
             ev.record()
             side.wait_event(ev)
             with torch.cuda.stream(side):
                 wgrad(dy, x, wout)
-                K.colsum(dy, out=bout)
+                if bout is not None:
+                    K.colsum(dy, out=bout)
             keep.extend((dy, x))  # alive until the streams join (no deferred record_stream frees)
 
         wt_ready = None
@@ -422,6 +429,10 @@ class BertPretraining:
 
         # ---------------------------------------------------------------- backward: encoder
         ln_work = T.ln_bwd_workspace(Tk, H, dev)
+        # FFN1 bias gradient from the FFN2-dgrad epilogue statistics (256-row GEMM tiles)
+        fuse_bias = self.fuse_bias_grad and G.big_fits(Tk, c.intermediate_size, H)
+        bias_part = (torch.empty((-(-Tk // 256), 2, c.intermediate_size), dtype=torch.float32, device=dev)
+                     if fuse_bias else None)
         delta = torch.empty((B * NH, S), dtype=torch.float32, device=dev)
         if wt_ready is not None:
             torch.cuda.current_stream().wait_event(wt_ready)
@@ -434,10 +445,18 @@ class BertPretraining:
                                        site_in=site(l, 2), rng=rng, work=ln_work)
             del dy
             wgrad_bias(dout2, inter, g[self._ln(l, "output/dense/kernel")], g[self._ln(l, "output/dense/bias")])
-            dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre)
+            b_inter = g[self._ln(l, "intermediate/dense/bias")]
+            if fuse_bias:
+                # the intermediate bias gradient = column sums of dpre, taken from the per-tile
+                # statistics of the dGELU dgrad epilogue that produces dpre (no separate column-sum
+                # pass over the [tokens, 4096] gradient)
+                dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre, stat=bias_part, tile=(256, 0))
+                K.col_reduce2(bias_part, bias_part.shape[0], o0=b_inter)
+                b_inter = None
+            else:
+                dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre)
             del dout2, inter, pre
-            wgrad_bias(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")],
-                       g[self._ln(l, "intermediate/dense/bias")])
+            wgrad_bias(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")], b_inter)
             self._dgrad(dpre, l, 2, out=G1, beta=1)
             del dpre
             layer_hook(self._ln(l, "intermediate/dense/bias"))

@@ -106,6 +106,8 @@ class ResNet:
         self.fuse_c3 = os.environ.get("TTD_FUSE_C3", "1") != "0" and precision == "bf16"
         # data gradient on the halo kernel: off until it beats bwd-apply + conv_dgrad (tools/conv3_bench.py)
         self.c3_dgrad = os.environ.get("TTD_C3_DGRAD", "0") != "0"
+        # stem weight gradient on its dedicated kernel (3 real input channels, BN backward on the fly)
+        self.stem_kernel = os.environ.get("TTD_STEM_WGRAD", "1") != "0"
         self._wgrad_stream = None
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -356,7 +358,11 @@ class ResNet:
             # of the backward, where nothing else runs)
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
-            G.conv_wgrad_bn(x, dout, y, coef, wshape, (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+            if self.stem_kernel and G.stem_wgrad_ok(tuple(x.shape), wshape, (c.stride, c.stride), (c.pad, c.pad),
+                                                    self.in_channels):
+                G.stem_wgrad(x, dout, y, coef, out=P.g[wname])  # dedicated kernel (stem_wgrad.hip)
+            else:
+                G.conv_wgrad_bn(x, dout, y, coef, wshape, (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
             if self._wgrad_stream is not None:
                 # the bucket this completes may hold side-stream gradients: collectives issued
                 # from here must order after that stream too

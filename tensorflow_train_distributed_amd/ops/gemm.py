@@ -116,6 +116,12 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     Kb, N = (b.shape[1], b.shape[0]) if trans_b else b.shape
     if K != Kb:
         raise ValueError("gemm inner dims differ: %d vs %d" % (K, Kb))
+    if stat is not None:
+        # statistics rows = M tiles of the kernel: the caller names the tile height
+        if (tile[0] not in (64, 128, 256) or (tile[0] != 256 and not tile[1]) or stat.shape[0] < -(-M // tile[0])
+                or stat.shape[-1] != N):
+            raise ValueError("gemm stat needs tile=(BM, ..) with BM in 64/128/256 and >= ceil(M/BM) rows of N "
+                             "(got tile %s, stat %s)" % (tile, tuple(stat.shape)))
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     elif tuple(out.shape) != (M, N) or out.stride(-1) != 1:
@@ -566,6 +572,31 @@ def conv_wgrad_bn(x, g_out, y, coef, w_shape, stride=(1, 1), padding=(0, 0), *, 
         ws = torch.empty((splits,) + tuple(w_shape), dtype=torch.float32, device=x.device)
     _lib.call("ttdk_conv_wgrad_bn", x.data_ptr(), g_out.data_ptr(), y.data_ptr(), coef.data_ptr(), ctypes.byref(g),
               out.data_ptr(), ws.data_ptr() if ws is not None else None, splits, beta, 0, 0, _lib.stream())
+    return out
+
+
+def stem_wgrad_ok(x_shape, w_shape, stride, padding, cin_real):
+    """The ResNet stem shape the dedicated weight-gradient kernel (stem_wgrad.hip) handles."""
+    return (len(x_shape) == 4 and x_shape[-1] == 8 and tuple(w_shape) == (64, 7, 7, 8) and tuple(stride) == (2, 2)
+            and tuple(padding) == (3, 3) and cin_real <= 3)
+
+
+def stem_wgrad(x, g_out, y, coef, *, out=None, beta=0):
+    """Stem weight gradient with the stem BN backward on the fly: dz = coef[0]*g + coef[1]*y +
+    coef[2], dW[64][7][7][8] = sum over pixels of dz x im2col(x) for the 3 real input channels
+    (the padded channels get 0). x [N,H,W,8]; g_out / y [N,P,Q,64]."""
+    _check(x, torch.bfloat16, "x")
+    _check(g_out, torch.bfloat16, "g_out")
+    _check(y, torch.bfloat16, "y")
+    N, H, W, _ = x.shape
+    P, Q = y.shape[1], y.shape[2]
+    if out is None:
+        out = torch.empty((64, 7, 7, 8), dtype=torch.float32, device=x.device)
+    nb = int(_lib.query("ttdk_stem_wgrad_blocks", N, P, Q))
+    ws = torch.empty(nb * 64 * 160 + 64 * 160, dtype=torch.float32, device=x.device)
+    _log("stem_wgrad", 64, 147, N * P * Q)
+    _lib.call("ttdk_stem_wgrad", x.data_ptr(), g_out.data_ptr(), y.data_ptr(), coef.data_ptr(), out.data_ptr(),
+              ws.data_ptr(), N, H, W, P, Q, int(beta), _lib.stream())
     return out
 
 

@@ -370,3 +370,27 @@ def _tail_case(G, C, K, R):
     gs = got.float().view(-1, C)
     torch.testing.assert_close(partial.sum(0)[0], gs.sum(0), rtol=1e-3, atol=1e-1)
     torch.testing.assert_close(partial.sum(0)[1], (gs * yb.float().view(-1, C)).sum(0), rtol=1e-3, atol=1e-1)
+
+
+def test_stem_weight_gradient_kernel_matches_oracle():
+    """stem_wgrad.hip: 7x7/s2/p3 weight gradient over the 3 real channels of an 8-channel
+    image with dz = coef0*g + coef1*y + coef2 formed on the fly, vs fp32 torch."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(9)
+    N, H = 3, 224
+    x = torch.zeros(N, H, H, 8, device="cuda")
+    x[..., :3] = torch.randn(N, H, H, 3, device="cuda")
+    x = x.bfloat16()
+    P = 112
+    g = torch.randn(N, P, P, 64, device="cuda").bfloat16()
+    y = torch.randn(N, P, P, 64, device="cuda").bfloat16()
+    coef = torch.randn(3, 64, device="cuda") * torch.tensor([[1.0], [0.1], [0.05]], device="cuda")
+    out = G.stem_wgrad(x, g, y, coef)
+    dz = (coef[0] * g.float() + coef[1] * y.float() + coef[2]).bfloat16().float()
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 8, 7, 7), dz.permute(0, 3, 1, 2),
+                                      stride=2, padding=3).permute(0, 2, 3, 1)
+    assert _rel(out, ref) < 1e-2
+    assert bool((out[..., 3:] == 0).all())
+    old = torch.randn_like(out)
+    out2 = G.stem_wgrad(x, g, y, coef, out=old.clone(), beta=1)
+    assert _rel(out2, ref + old) < 1e-2
