@@ -119,8 +119,10 @@ __global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __rest
       __syncthreads();
       if (p + 1 < p1) prefetch(n, p + 1, q0);  // in flight under this row's im2col build and MFMAs
       // 2. im2col^T: column (r, s, c<3) -> B[col][j] = input row 2p-3+r, column 2j+s (relative), channel c
+      // consecutive lanes take consecutive columns of one pixel chunk: their scalar LDS reads
+      // fall on neighbouring bytes (the chunk-fastest order put 8 lanes 256 B apart on one bank)
       for (int c = tid; c < NC * (KP / 8); c += THR) {
-        const int col = c / (KP / 8), kc = c % (KP / 8);
+        const int kc = c / NC, col = c % NC;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (col < 147) {
           const int r = col / 21, rem = col % 21, s = rem / 3, ch = rem % 3;
