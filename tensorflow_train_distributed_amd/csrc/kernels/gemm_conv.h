@@ -36,6 +36,7 @@
 // gemm_conv.hip; everything below lives in an anonymous namespace, i.e. per TU)
 namespace ttdk_rt {
 int& tail_split_flag();
+int& pers_flag();
 }
 
 namespace ttdk {
@@ -1586,6 +1587,229 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   }
 }
 
+
+// Epilogue kinds of the persistent kernel (compile-time: the run-time flags of EpiParams made
+// every element a branch; BERT needs these five)
+constexpr int kEkBias = 1, kEkDGelu = 2, kEkBeta = 4, kEkAux = 8, kEkGelu = 16;
+
+// Register epilogue of gemm256p_kernel: acc[ha][hb][a][b][v] = C[m0 + ha*128 + wm*64 + a*16 +
+// (lane & 15)][n0 + hb*BNH + wn*WC + b*16 + 4*(lane >> 4) + v]. Lane pairs (g even, g + 1)
+// swap halves so each lane stores 16 B (8 columns): 16 rows x 64 contiguous bytes per store.
+// CHECK: the tile overhangs M or N (row / column guards per lane).
+template <int EK, bool CHECK, int BNH, int WC>
+__device__ __forceinline__ void pers_epi(const f32x4_t (&acc)[2][2][4][2], const EpiParams& E, int m0, int n0, int M,
+                                         int N, float alpha, int lane, int wm, int wn) {
+  const int g = lane >> 4, i16 = lane & 15;
+  const bool odd = g & 1;
+  bf16_t* const out = static_cast<bf16_t*>(E.out);
+#pragma unroll
+  for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int m = m0 + ha * 128 + wm * 64 + a * 16 + i16;
+      if (CHECK && m >= M) continue;
+      const long long row = static_cast<long long>(m) * E.ldo;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        const int nb = n0 + hb * BNH + wn * WC + 4 * g;  // block b: nb + 16 b
+        uint2 rv[2], ov[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if constexpr ((EK & kEkDGelu) != 0)
+            if (!CHECK || nb + 16 * b < N) rv[b] = *reinterpret_cast<const uint2*>(E.residual + static_cast<long long>(m) * E.ldr + nb + 16 * b);
+          if constexpr ((EK & kEkBeta) != 0)
+            if (!CHECK || nb + 16 * b < N) ov[b] = *reinterpret_cast<const uint2*>(out + row + nb + 16 * b);
+        }
+        uint2 po[2], pa[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          f32x4_t v = acc[ha][hb][a][b] * alpha;
+          if constexpr ((EK & kEkBias) != 0)
+            if (!CHECK || nb + 16 * b < N) v += *reinterpret_cast<const f32x4_t*>(E.bias + nb + 16 * b);
+          if constexpr ((EK & kEkDGelu) != 0) {
+            v[0] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].x & 0xffff)));
+            v[1] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].x >> 16)));
+            v[2] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].y & 0xffff)));
+            v[3] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].y >> 16)));
+          }
+          if constexpr ((EK & kEkBeta) != 0) {
+            v[0] += bf2f(static_cast<bf16_t>(ov[b].x & 0xffff));
+            v[1] += bf2f(static_cast<bf16_t>(ov[b].x >> 16));
+            v[2] += bf2f(static_cast<bf16_t>(ov[b].y & 0xffff));
+            v[3] += bf2f(static_cast<bf16_t>(ov[b].y >> 16));
+          }
+          if constexpr ((EK & kEkAux) != 0) pa[b] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          if constexpr ((EK & kEkGelu) != 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
+          }
+          po[b] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+        const int nst = odd ? nb + 12 : nb;  // odd lane: columns 4(g-1).. of block 1
+        {
+          const uint2 snd = odd ? po[0] : po[1];
+          const uint2 rcv = make_uint2(__shfl_xor(snd.x, 16, 64), __shfl_xor(snd.y, 16, 64));
+          const uint4 w = odd ? make_uint4(rcv.x, rcv.y, po[1].x, po[1].y) : make_uint4(po[0].x, po[0].y, rcv.x, rcv.y);
+          if (!CHECK || nst < N) *reinterpret_cast<uint4*>(out + row + nst) = w;
+        }
+        if constexpr ((EK & kEkAux) != 0) {
+          const uint2 snd = odd ? pa[0] : pa[1];
+          const uint2 rcv = make_uint2(__shfl_xor(snd.x, 16, 64), __shfl_xor(snd.y, 16, 64));
+          const uint4 w = odd ? make_uint4(rcv.x, rcv.y, pa[1].x, pa[1].y) : make_uint4(pa[0].x, pa[0].y, rcv.x, rcv.y);
+          if (!CHECK || nst < N) *reinterpret_cast<uint4*>(E.aux + row + nst) = w;
+        }
+      }
+    }
+}
+
+// Persistent 256 x BN GEMM for elementwise epilogues (bias, residual / dGELU, beta, aux copy,
+// ReLU / GELU / tanh; no BN statistics, no row remap, no split-K): one workgroup per CU walks
+// tiles vt = blockIdx.x, + gridDim.x, ... (the same XCD-aware order as the one-tile kernel).
+// When a tile's last K-tile has been consumed, the DMA of the next tile's first two K-tiles is
+// issued into the now idle stage buffers and only then does the epilogue run, straight from
+// the accumulator registers (8-B stores of 4 consecutive columns per lane; no LDS staging, so
+// the stage buffers stay free): the next tile's operand latency hides under this tile's
+// epilogue instead of both sitting exposed between two one-tile workgroups (the per-tile
+// prologue + epilogue were ~15 % of a K = 1024 BERT GEMM on one workgroup per CU).
+// Main loop: the ping-pong schedule of gemm256_kernel (PP = 1), bf16 operands.
+template <int BN, class OA, class OB, int EK>
+__global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::Params pa, typename OB::Params pb,
+                                                                EpiParams E, int M, int N, int K, int tiles_m,
+                                                                int tiles_n, int ovl) {
+  using Gm = Geo<BN>;
+  constexpr int T = OA::THREADS, NW = T / 64, WN = NW / 2;
+  static_assert(OB::THREADS == T && NW == 8, "8-wave operand policies");
+  constexpr int BNH = Gm::BNH, WC = BNH / WN, NB = WC / 16, GA = OA::G, GB = OB::G;
+  constexpr bool AK = Traits<OA>::kmaj, BKM = Traits<OB>::kmaj;
+  static_assert(NB == 2, "the 16-B store exchange pairs the two 16-column blocks of a wave");
+  __shared__ __attribute__((aligned(16))) char smem[2 * Gm::STAGE];
+  const int nblk = tiles_m * tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const bool lag = __builtin_amdgcn_readfirstlane(wm) == 1;
+  const int ktiles = K / 64;
+  constexpr int A0 = 0, A1 = Gm::AH, B0 = 2 * Gm::AH, B1 = 2 * Gm::AH + Gm::BH;
+  auto buf = [&](int kt) { return smem + (kt & 1) * Gm::STAGE; };
+
+  OA la;
+  OB lb;
+  bf16x8_t fa[2][2][4], fb[2][2][NB];
+  auto read_a = [&](const char* sA, bf16x8_t (&f)[2][4]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        if constexpr (AK) f[ks][a] = frag_k(sA, wm * 64 + a * 16, ks, lane);
+        else f[ks][a] = frag_mn<128>(sA, wm * 64 + a * 16, ks, lane);
+      }
+  };
+  auto read_b = [&](const char* sB, bf16x8_t (&f)[2][NB]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        if constexpr (BKM) f[ks][b] = frag_k(sB, wn * WC + b * 16, ks, lane);
+        else f[ks][b] = frag_mn<BNH>(sB, wn * WC + b * 16, ks, lane);
+      }
+  };
+  auto mma = [&](const bf16x8_t (&x)[2][4], const bf16x8_t (&y)[2][NB], f32x4_t (&c)[4][NB]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y[ks][b], x[ks][a], c[a][b], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // first two K-tiles of a tile: all four halves of K-tile 0, then A0 / B0 / B1 of K-tile 1
+  // (its A1 is issued in the first phase of the main loop, as in gemm256_kernel)
+  auto prologue = [&](int m0, int n0) {
+    la.init(pa, m0, tid);
+    lb.init(pb, n0, tid);
+    char* b0 = buf(0);
+    la.template issue<0>(b0 + A0, 0, wave);
+    lb.template issue<0>(b0 + B0, 0, wave);
+    lb.template issue<1>(b0 + B1, 0, wave);
+    la.template issue<1>(b0 + A1, 0, wave);
+    if (ktiles > 1) {
+      char* b1 = buf(1);
+      la.template issue<0>(b1 + A0, 1, wave);
+      lb.template issue<0>(b1 + B0, 1, wave);
+      lb.template issue<1>(b1 + B1, 1, wave);
+    }
+  };
+
+  int vt = blockIdx.x;
+  if (vt >= nblk) return;
+  int t = xcd_remap(vt, nblk);
+  prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
+  const float alpha_e = epi_alpha(E);
+
+  for (;;) {
+    const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+    f32x4_t acc[2][2][4][NB];
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) acc[ha][hb][a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // K-tile 0 landed (every store of the previous epilogue retired too: vmcnt counts both,
+    // in issue order, and the epilogue's count is not a compile-time constant)
+    if (ktiles > 1 && vt == static_cast<int>(blockIdx.x)) wait_vm<GA + 2 * GB>();
+    else wait_vm<0>();
+    barrier();
+    if (lag) barrier();
+    for (int kt = 0; kt < ktiles; ++kt) {
+      const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
+      char* cb = buf(kt);
+      read_a(cb + A0, fa[0]);
+      read_b(cb + B0, fb[0]);
+      if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
+      barrier();
+      mma(fa[0], fb[0], acc[0][0]);
+      barrier();
+      read_b(cb + B1, fb[1]);
+      barrier();
+      mma(fa[0], fb[1], acc[0][1]);
+      barrier();
+      read_a(cb + A1, fa[1]);
+      if (has2) {
+        la.template issue<0>(cb + A0, kt + 2, wave);
+        lb.template issue<0>(cb + B0, kt + 2, wave);
+      }
+      barrier();
+      mma(fa[1], fb[1], acc[1][1]);
+      barrier();
+      if (has1) {
+        if (has2) wait_vm<GA + GB>(); else wait_vm<0>();
+      }
+      if (has2) lb.template issue<1>(cb + B1, kt + 2, wave);
+      barrier();
+      mma(fa[1], fb[0], acc[1][0]);
+      barrier();
+    }
+    if (!lag) barrier();  // both wave halves past their last LDS read: the stage buffers are free
+    const int nvt = vt + gridDim.x;
+    if (ovl && nvt < nblk) {
+      t = xcd_remap(nvt, nblk);
+      prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
+    }
+    // ------------------------------------------------------------ register epilogue
+    if (m0 + BM <= M && n0 + BN <= N) pers_epi<EK, false, BNH, WC>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
+    else pers_epi<EK, true, BNH, WC>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
+    if (nvt >= nblk) break;
+    if (!ovl) {
+      t = xcd_remap(nvt, nblk);
+      prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
+    }
+    vt = nvt;
+  }
+}
+
 // Split-K tail epilogue: rows [m_base, M) of the GEMM were computed as S fp32 slabs
 // ws[S][M - m_base][N] (alpha applied); sum them, stage the tile as bf16 and run the same
 // fused epilogue (epi_rows + BN statistics) the 256-row kernel runs, for tile rows
@@ -1761,6 +1985,38 @@ hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, 
   if (splits > ktiles) splits = ktiles;
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);
+  if constexpr (F8 == 0 && PP == 1 && OA::THREADS == THR && BN == 256) {
+    // elementwise-only epilogue on more than one round of tiles: persistent kernel, the next
+    // tile's operand DMA in flight under this tile's register epilogue
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    int ek = -1;
+    if (pe.act == kActNone && !pe.residual) ek = 0;
+    else if (pe.act == kActGelu && !pe.residual) ek = kEkGelu;
+    else if (pe.act == kActDGelu && pe.residual) ek = kEkDGelu;
+    if (ek >= 0) {
+      if (pe.bias) ek |= kEkBias;
+      if (pe.beta) ek |= kEkBeta;
+      if (pe.aux) ek |= kEkAux;
+    }
+    if (::ttdk_rt::pers_flag() && splits == 1 && pe.mode == 0 && !pe.remap && !pe.stat && !pe.by && !pe.bH && tiles > cus &&
+        N % 8 == 0 && pe.ldo % 8 == 0 && (!pe.residual || pe.ldr % 4 == 0) && (!pe.bias || al16(pe.bias)) &&
+        al16(pe.out) && (!pe.aux || al16(pe.aux)) && (!pe.residual || (reinterpret_cast<uintptr_t>(pe.residual) & 7) == 0)) {
+      const int ovl = ::ttdk_rt::pers_flag() == 1;
+#define TTDK_PERS(EKV)                                                                                                \
+  case EKV:                                                                                                           \
+    hipLaunchKernelGGL((gemm256p_kernel<BN, OA, OB, EKV>), dim3(cus), dim3(THR), 0, st, pa, pb, pe, M, N, K, tm, tn, ovl); \
+    return hipGetLastError();
+      switch (ek) {
+        TTDK_PERS(0)
+        TTDK_PERS(kEkBias)
+        TTDK_PERS(kEkBias | kEkAux | kEkGelu)
+        TTDK_PERS(kEkDGelu)
+        TTDK_PERS(kEkBeta)
+        default: break;
+      }
+#undef TTDK_PERS
+    }
+  }
   hipLaunchKernelGGL((gemm256_kernel<BN, OA, OB, F8, PP>), dim3(tm * tn, splits), dim3(OA::THREADS), 0, st, pa, pb, pe, M, N,
                      K, tm, tn, per, 0);
   return hipGetLastError();

@@ -49,10 +49,22 @@ int& tail_split_flag() {
   static int on = getenv_int("TTD_TAIL_SPLIT", 0);
   return on;
 }
+int& pers_flag() {
+  static int on = getenv_int("TTD_BIG_PERS", 1);
+  return on;
+}
 }  // namespace ttdk_rt
 
 TTDK_EXPORT int ttdk_set_tail_split(int on) {
   const int old = ttdk_rt::tail_split_flag();
   ttdk_rt::tail_split_flag() = on;
+  return old;
+}
+
+// Runtime switch of the persistent register-epilogue 256-row GEMM (gemm256p_kernel); returns
+// the previous setting.
+TTDK_EXPORT int ttdk_set_big_pers(int on) {
+  const int old = ttdk_rt::pers_flag();
+  ttdk_rt::pers_flag() = on;
   return old;
 }

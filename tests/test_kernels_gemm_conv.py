@@ -394,3 +394,65 @@ def test_stem_weight_gradient_kernel_matches_oracle():
     old = torch.randn_like(out)
     out2 = G.stem_wgrad(x, g, y, coef, out=old.clone(), beta=1)
     assert _rel(out2, ref + old) < 1e-2
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+@pytest.mark.parametrize("epi", ["bias_gelu_aux", "dgelu", "bias_residual", "beta"])
+def test_persistent_register_epilogue_gemm_matches_one_tile_kernel(ta, tb, epi):
+    """More than one round of 256 x 256 tiles with K >= 1024 and an elementwise epilogue runs on
+    the persistent kernel (gemm256p_kernel: next tile's operand DMA under this tile's register
+    epilogue). Compared with the one-tile-per-workgroup kernel (switched off at run time) and an
+    fp32 oracle; ragged M exercises the row guard."""
+    from tensorflow_train_distributed_amd.ops import _lib
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(3)
+    M, N, K = 8192 + 72, 2048, 1024  # 33 x 8 = 264 tiles > 256 CUs
+    a = (torch.randn((K, M) if ta else (M, K), device="cuda") / K ** 0.25).bfloat16()
+    b = (torch.randn((N, K) if tb else (K, N), device="cuda") / K ** 0.25).bfloat16()
+    af = a.float().t() if ta else a.float()
+    bf = b.float().t() if tb else b.float()
+    ref = af @ bf
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda").bfloat16()
+    old = torch.randn(M, N, device="cuda").bfloat16()
+
+    def run():
+        kw = dict(trans_a=ta, trans_b=tb)
+        if epi == "bias_gelu_aux":
+            aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            y = G.gemm(a, b, bias=bias, act=G.ACT_GELU, aux=aux, **kw)
+            return y, aux
+        if epi == "dgelu":
+            return G.gemm(a, b, act=G.ACT_DGELU, residual=res, **kw), None
+        if epi == "bias_residual":
+            return G.gemm(a, b, bias=bias, residual=res, **kw), None
+        out = old.clone()
+        return G.gemm(a, b, out=out, beta=1, **kw), None
+
+    prev = _lib.query("ttdk_set_big_pers", 1)
+    try:
+        y1, x1 = run()
+        _lib.query("ttdk_set_big_pers", 0)
+        y0, x0 = run()
+    finally:
+        _lib.query("ttdk_set_big_pers", prev)
+    torch.cuda.synchronize()
+    if epi == "bias_gelu_aux":
+        pre = ref + bias
+        want = F.gelu(pre, approximate="tanh")
+        assert _rel(x1, pre) < 1e-2
+        assert _rel(x1, x0) < 1e-2
+    elif epi == "dgelu":
+        xr = res.float()
+        t = torch.tanh(0.7978845608028654 * (xr + 0.044715 * xr ** 3))
+        gg = 0.5 * (1 + t) + 0.5 * xr * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * xr * xr)
+        want = ref * gg
+    elif epi == "bias_residual":
+        want = ref + bias + res.float()
+    else:
+        want = ref + old.float()
+    assert _rel(y1, want) < 1e-2
+    # the one-tile kernel rounds the accumulator to bf16 before the epilogue: same result to
+    # within bf16 rounding
+    assert _rel(y1, y0) < 1e-2
+    assert torch.isfinite(y1.float()).all()

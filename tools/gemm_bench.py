@@ -66,6 +66,16 @@ def main():
                 f = lambda: G.gemm(a, b, trans_a=ta, trans_b=tb, out=out, tile=tile)  # noqa: E731
             ms = timeit(f)
             res.append("%s %.3f ms %.0f TF/s" % (tile[0], ms, fl / ms / 1e9))
+            if tile[0] == 256 and not wgrad:  # one-tile-per-workgroup kernel (persistent path off)
+                from tensorflow_train_distributed_amd.ops import _lib
+                prev = _lib.query("ttdk_set_big_pers", 0)
+                ms = timeit(f)
+                _lib.query("ttdk_set_big_pers", prev)
+                res.append("256np %.3f ms %.0f TF/s" % (ms, fl / ms / 1e9))
+                prev = _lib.query("ttdk_set_big_pers", 2)
+                ms = timeit(f)
+                _lib.query("ttdk_set_big_pers", prev)
+                res.append("256p-noovl %.3f ms %.0f TF/s" % (ms, fl / ms / 1e9))
         at = a.t() if ta else a
         bt = b.t() if tb else b
         ms = timeit(lambda: torch.matmul(at, bt))
