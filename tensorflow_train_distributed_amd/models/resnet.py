@@ -108,6 +108,8 @@ class ResNet:
         self.c3_dgrad = os.environ.get("TTD_C3_DGRAD", "0") != "0"
         # stem weight gradient on its dedicated kernel (3 real input channels, BN backward on the fly)
         self.stem_kernel = os.environ.get("TTD_STEM_WGRAD", "1") != "0"
+        # dedicated stem forward kernel (stem_fwd.hip: K = 7 x 32 over the 3 real channels)
+        self.stem_fwd_kernel = os.environ.get("TTD_STEM_FWD", "1") != "0"
         self._wgrad_stream = None
         self.num_classes = num_classes
         self.in_channels = in_channels
@@ -282,7 +284,11 @@ class ResNet:
             bm, bn = 256, big  # 256-row LDS-DMA kernel (BN stat rows per 256-pixel tile)
         T = -(-M // bm)
         partial = None
-        if not use8 and self._c3_ok(c, H, W):
+        if (c is self.stem and not use8 and self.stem_fwd_kernel and self.device.type == "cuda"
+                and G.stem_fwd_ok(tuple(x.shape), tuple(P.var[c.name + "_conv/kernel"].shape), (c.stride, c.stride),
+                                  (c.pad, c.pad), self.in_channels)):
+            y, partial, T = G.stem_fwd(x, P.c[c.name + "_conv/kernel"])
+        elif not use8 and self._c3_ok(c, H, W):
             w4 = P.c[c.name + "_conv/kernel"]
             if pro is not None:
                 psc, psh, _, _, side, side_mask = pro

@@ -61,7 +61,9 @@ _SIGS = {
     "ttdk_set_big_pers": [I],
     # gemm_f32.hip
     "ttdk_gemm_f32": [P, L, I, P, L, I, P, L, P, I, I, I, I, P],
-    # stem_wgrad.hip
+    # stem_fwd.hip / stem_wgrad.hip
+    "ttdk_stem_fwd_blocks": [I],
+    "ttdk_stem_fwd": [P, P, P, P, I, I, I, P],
     "ttdk_stem_wgrad_blocks": [I, I, I],
     "ttdk_stem_wgrad": [P, P, P, P, P, P, I, I, I, I, I, I, P],
     # conv3_halo.hip

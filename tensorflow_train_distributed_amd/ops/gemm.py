@@ -575,6 +575,27 @@ def conv_wgrad_bn(x, g_out, y, coef, w_shape, stride=(1, 1), padding=(0, 0), *, 
     return out
 
 
+def stem_fwd_ok(x_shape, w_shape, stride, padding, cin_real):
+    """The ResNet stem shape the dedicated forward kernel (stem_fwd.hip) handles: 224 x 224 RGB
+    stored with 8 channels, 64 7x7/2 filters."""
+    return (len(x_shape) == 4 and tuple(x_shape[1:]) == (224, 224, 8) and tuple(w_shape) == (64, 7, 7, 8)
+            and tuple(stride) == (2, 2) and tuple(padding) == (3, 3) and cin_real <= 3)
+
+
+def stem_fwd(x, w):
+    """Stem convolution (7x7/2, pad 3) over the 3 real input channels -> (y [N,112,112,64] bf16,
+    partial [T,2,64] per-workgroup BN (sum, sum of squares) of the stored y, T)."""
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.bfloat16, "w")
+    N, H, W, _ = x.shape
+    y = torch.empty((N, 112, 112, 64), dtype=torch.bfloat16, device=x.device)
+    T = int(_lib.query("ttdk_stem_fwd_blocks", N))
+    partial = torch.empty((T, 2, 64), dtype=torch.float32, device=x.device)
+    _log("stem_fwd", N * 112 * 112, 64, 147)
+    _lib.call("ttdk_stem_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(), partial.data_ptr(), N, H, W, _lib.stream())
+    return y, partial, T
+
+
 def stem_wgrad_ok(x_shape, w_shape, stride, padding, cin_real):
     """The ResNet stem shape the dedicated weight-gradient kernel (stem_wgrad.hip) handles."""
     return (len(x_shape) == 4 and x_shape[-1] == 8 and tuple(w_shape) == (64, 7, 7, 8) and tuple(stride) == (2, 2)

@@ -456,3 +456,30 @@ def test_persistent_register_epilogue_gemm_matches_one_tile_kernel(ta, tb, epi):
     # within bf16 rounding
     assert _rel(y1, y0) < 1e-2
     assert torch.isfinite(y1.float()).all()
+
+
+@pytest.mark.parametrize("N", [3, 257])
+def test_stem_forward_kernel_matches_conv_oracle(N):
+    """Dedicated stem forward (stem_fwd.hip: K = 7 taps x (s, c4) over the 3 real channels, no
+    im2col) vs the fp32 convolution, and its per-workgroup BN sums vs the stored output."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(21)
+    x = torch.zeros(N, 224, 224, 8, device="cuda", dtype=torch.bfloat16)
+    x[..., :3] = torch.randn(N, 224, 224, 3, device="cuda").bfloat16()
+    w = (torch.randn(64, 7, 7, 8, device="cuda") * 0.1).bfloat16()
+    w[..., 3:] = 0
+    assert G.stem_fwd_ok(x.shape, w.shape, (2, 2), (3, 3), 3)
+    y, part, T = G.stem_fwd(x, w)
+    torch.cuda.synchronize()
+    n_chk = min(N, 4)
+    xs = torch.cat([x[:2], x[-2:]]) if N > 4 else x
+    ys = torch.cat([y[:2], y[-2:]]) if N > 4 else y
+    ref = F.conv2d(xs.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=2, padding=3).permute(0, 2, 3, 1)
+    assert ys.shape[0] == n_chk
+    assert _rel(ys, ref) < 8e-3
+    yf = y.float().view(-1, 64)
+    torch.testing.assert_close(part[:T, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1.0)
+    torch.testing.assert_close(part[:T, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1.0)
+    # same values as the generic implicit-GEMM conv (both round the fp32 sum once)
+    y2 = G.conv_fwd(xs, w, (2, 2), (3, 3))
+    assert _rel(ys, y2) < 8e-3

@@ -35,3 +35,4 @@ t_old = timeit(lambda: G.conv_wgrad_bn(x, g, y, coef, (64, 7, 7, 8), (2, 2), (3,
 gb = (g.numel() * 2 * 2 + x.numel() * 2) / 1e9
 print("stem wgrad b%d: kernel %.1f us (%.2f TB/s of g+y+x)  generic %.1f us" % (B, t_new, gb / t_new * 1e3, t_old),
       flush=True)
+
