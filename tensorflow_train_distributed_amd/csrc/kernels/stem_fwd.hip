@@ -1,5 +1,5 @@
 // Forward of the ResNet stem convolution (7x7, stride 2, pad 3, 64 filters) over the RGB image
-// stored with 8 channels [N][H][W][8] (channels 3..7 zero), with the per-workgroup BatchNorm
+// (packed [N][H][W][3], or stored with 8 channels, 3..7 zero), with the per-workgroup BatchNorm
 // statistics of the stored bf16 output:
 //     y[n][p][q][k] = sum_{r,s,c<3} x[n][2p-3+r][2q-3+s][c] * w[k][r][s][c]
 //
@@ -35,10 +35,15 @@ constexpr int XC = W + 6;              // staged columns: input columns -3 .. W+
 constexpr int XP = XC * 8;             // bytes per staged row (4 bf16 channels per column)
 constexpr int KO = 64;
 constexpr int WP = 7 * 64 + 16;        // bytes per staged filter row k: 7 taps x 32 bf16 (+16: odd slot pitch)
-constexpr int NLD = (NEWR * W + THR - 1) / THR;  // prefetched 16-B pixels per thread per band
+constexpr int NLD = (NEWR * W + THR - 1) / THR;  // prefetched pixels per thread per band (8-channel input)
+constexpr int RC3 = W * 3 * 2 / 16;              // 16-B chunks per input row (3-channel input)
+constexpr int NLD3 = (NEWR * RC3 + THR - 1) / THR;
 
 __device__ __forceinline__ int ring_slot(int h) { return (h + 4 * RING) % RING; }
 
+// CIN: channel stride of x — 8 (RGB padded with zeros, one 16-B load per pixel) or 3 (packed
+// RGB, 16-B loads over the row, scattered into the ring as 2-B writes; no padding pass)
+template <int CIN>
 __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                           bf16_t* __restrict__ y, float* __restrict__ part, int N,
                                                           int H, int P, int imgs_per_wg) {
@@ -55,18 +60,30 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
     const bf16_t v = (s < 7 && c < 3) ? w[((k * 7 + r) * 7 + s) * 8 + c] : static_cast<bf16_t>(0);
     *reinterpret_cast<bf16_t*>(ws + k * WP + (r * 32 + s * 4 + c) * 2) = v;
   }
-  // the 3 pad columns on each side of every ring row stay zero
-  for (int i = tid; i < RING * 6; i += THR) {
-    const int row = i / 6, j = i % 6, col = j < 3 ? j : W + j;
-    *reinterpret_cast<uint2*>(xs + row * XP + col * 8) = make_uint2(0, 0);
-  }
+  // the ring starts zero: the pad columns and (3-channel input) channel 3 are never written
+  for (int i = tid; i < RING * XP / 16; i += THR) reinterpret_cast<uint4*>(xs)[i] = make_uint4(0, 0, 0, 0);
 
-  auto xpix = [&](int n, int h, int col) -> uint2 {  // channels 0..3 of input pixel (h, col)
+  // 8-channel input: pixel loads (channels 0..3 kept)
+  auto xpix = [&](int n, int h, int col) -> uint2 {
     if (h < 0 || h >= H) return make_uint2(0, 0);
     const uint4 v = ldg16(x + ((static_cast<long long>(n) * H + h) * W + col) * 8);
     return make_uint2(v.x, v.y);
   };
   auto put = [&](int h, int col, uint2 v) { *reinterpret_cast<uint2*>(xs + ring_slot(h) * XP + (col + 3) * 8) = v; };
+  // 3-channel input: 16-B chunk j of row h (elements 8j .. 8j+7 of its packed [W][3] values)
+  auto xchunk = [&](int n, int h, int j) -> uint4 {
+    if (h < 0 || h >= H) return make_uint4(0, 0, 0, 0);
+    return ldg16(x + (static_cast<long long>(n) * H + h) * W * 3 + j * 8);
+  };
+  auto put3 = [&](int h, int j, uint4 v) {
+    char* row = xs + ring_slot(h) * XP;
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int el = 8 * j + e, px = el / 3, ch = el - 3 * px;
+      *reinterpret_cast<bf16_t*>(row + (px + 3) * 8 + ch * 2) = static_cast<bf16_t>((wd[e >> 1] >> (16 * (e & 1))) & 0xffff);
+    }
+  };
 
   float st[4][4], sq[4][4];  // BN partial sums of this lane's channels cb*16 + 4g + v
 #pragma unroll
@@ -78,21 +95,35 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
   for (int n = n_begin; n < n_end; ++n) {
     // first band of the image: all of its input rows 2p0-3 .. 2p0+2*BAND+1 (p0 = 0)
     __syncthreads();
-    for (int i = tid; i < RING * W; i += THR) {
-      const int rr = i / W, col = i % W, h = rr - 3;
-      put(h, col, xpix(n, h, col));
+    if constexpr (CIN == 8) {
+      for (int i = tid; i < RING * W; i += THR) {
+        const int rr = i / W, col = i % W, h = rr - 3;
+        put(h, col, xpix(n, h, col));
+      }
+    } else {
+      for (int i = tid; i < RING * RC3; i += THR) {
+        const int rr = i / RC3, j = i % RC3, h = rr - 3;
+        put3(h, j, xchunk(n, h, j));
+      }
     }
     __syncthreads();
     for (int band = 0; band < bands; ++band) {
       const int p0 = band * BAND;
       const bool pre = band + 1 < bands;
       // next band's new input rows 2p0+2*BAND+2 .. +NEWR-1 into registers (in flight under the MFMAs)
-      uint2 nx[NLD];
+      constexpr int NPF = CIN == 8 ? NLD : NLD3;
+      uint2 nx[CIN == 8 ? NLD : 1];
+      uint4 nx3[CIN == 8 ? 1 : NLD3];
 #pragma unroll
-      for (int i = 0; i < NLD; ++i) {
+      for (int i = 0; i < NPF; ++i) {
         const int idx = tid + THR * i;
-        const int rr = idx / W, col = idx % W;
-        nx[i] = (pre && idx < NEWR * W) ? xpix(n, 2 * p0 + 2 * BAND + 2 + rr, col) : make_uint2(0, 0);
+        if constexpr (CIN == 8) {
+          const int rr = idx / W, col = idx % W;
+          nx[i] = (pre && idx < NEWR * W) ? xpix(n, 2 * p0 + 2 * BAND + 2 + rr, col) : make_uint2(0, 0);
+        } else {
+          const int rr = idx / RC3, j = idx % RC3;
+          nx3[i] = (pre && idx < NEWR * RC3) ? xchunk(n, 2 * p0 + 2 * BAND + 2 + rr, j) : make_uint4(0, 0, 0, 0);
+        }
       }
       // wave: output row p = p0 + wave
       const int p = p0 + wave;
@@ -148,9 +179,13 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
       __syncthreads();  // every wave done with the ring rows the prefetched ones replace
       if (pre) {
 #pragma unroll
-        for (int i = 0; i < NLD; ++i) {
+        for (int i = 0; i < NPF; ++i) {
           const int idx = tid + THR * i;
-          if (idx < NEWR * W) put(2 * p0 + 2 * BAND + 2 + idx / W, idx % W, nx[i]);
+          if constexpr (CIN == 8) {
+            if (idx < NEWR * W) put(2 * p0 + 2 * BAND + 2 + idx / W, idx % W, nx[i]);
+          } else {
+            if (idx < NEWR * RC3) put3(2 * p0 + 2 * BAND + 2 + idx / RC3, idx % RC3, nx3[i]);
+          }
         }
       }
       __syncthreads();
@@ -198,15 +233,19 @@ TTDK_EXPORT int ttdk_stem_fwd_blocks(int N) {
   return (N + per - 1) / per;
 }
 
-// x [N][224][224][8] bf16 (channels 3..7 zero), w [64][7][7][8] bf16 -> y [N][112][112][64]
-// bf16, part [blocks][2][64] fp32 (per-workgroup sum / sum of squares of the stored y).
-TTDK_EXPORT int ttdk_stem_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int N, int H, int Wd,
+// x [N][224][224][cin] bf16 (cin = 3, or 8 with channels 3..7 zero), w [64][7][7][8] bf16 ->
+// y [N][112][112][64] bf16, part [blocks][2][64] fp32 (per-workgroup sum / sum of squares of y).
+TTDK_EXPORT int ttdk_stem_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int N, int H, int Wd, int cin,
                               hipStream_t st) {
+  if (cin != 3 && cin != 8) return hipErrorInvalidValue;
   if (N <= 0 || H != stemf::W || Wd != stemf::W) return hipErrorInvalidValue;
   const int P = (H + 6 - 7) / 2 + 1;
   if (P % stemf::BAND != 0) return hipErrorInvalidValue;
   const int G = ttdk_stem_fwd_blocks(N);
   const int per = (N + G - 1) / G;
-  hipLaunchKernelGGL(stemf::stem_fwd_kernel, dim3(G), dim3(stemf::THR), 0, st, x, w, y, part, N, H, P, per);
+  if (cin == 3)
+    hipLaunchKernelGGL(stemf::stem_fwd_kernel<3>, dim3(G), dim3(stemf::THR), 0, st, x, w, y, part, N, H, P, per);
+  else
+    hipLaunchKernelGGL(stemf::stem_fwd_kernel<8>, dim3(G), dim3(stemf::THR), 0, st, x, w, y, part, N, H, P, per);
   return hipGetLastError();
 }

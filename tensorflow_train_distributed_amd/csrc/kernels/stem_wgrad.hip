@@ -33,6 +33,9 @@ constexpr int KO = 64;            // output channels
 constexpr int BAND = 8;          // output rows per work unit (a ring of input rows is kept across them)
 constexpr int RING = 8;          // input-row slots (7 in use)
 
+// CIN: channel stride of x (8: RGB padded with zeros, one 16-B load per pixel; 3: packed RGB,
+// three 2-B loads per pixel, no padding pass)
+template <int CIN>
 __global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
                                                             const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                             float* __restrict__ ws, int N, int H, int W, int P, int Q,
@@ -54,8 +57,10 @@ __global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __rest
   // one input row (XW 16-B pixels starting at column 2*q0-3, zero outside the image)
   auto load_xpix = [&](int n, int h, int q0, int t) -> uint4 {
     const int w = 2 * q0 - 3 + t;
-    return (h >= 0 && h < H && w >= 0 && w < W) ? ldg16(x + ((static_cast<long long>(n) * H + h) * W + w) * 8)
-                                                : make_uint4(0, 0, 0, 0);
+    if (!(h >= 0 && h < H && w >= 0 && w < W)) return make_uint4(0, 0, 0, 0);
+    const bf16_t* px = x + ((static_cast<long long>(n) * H + h) * W + w) * CIN;
+    if constexpr (CIN == 8) return ldg16(px);
+    return make_uint4(static_cast<uint32_t>(px[0]) | (static_cast<uint32_t>(px[1]) << 16), px[2], 0, 0);
   };
   // per output row: g / y chunks and the two input rows that row adds to the ring, prefetched
   // into registers one row ahead
@@ -183,13 +188,17 @@ TTDK_EXPORT int ttdk_stem_wgrad_blocks(int N, int P, int Q) {
   return static_cast<int>(units < want ? units : want);
 }
 
-// x [N][H][W][8] (3 real channels), g / y [N][P][Q][64], coef [3][64] -> dw [64][7][7][8] fp32.
+// x [N][H][W][cin] (cin = 3, or 8 with 3 real channels), g / y [N][P][Q][64], coef [3][64] -> dw [64][7][7][8] fp32.
 TTDK_EXPORT int ttdk_stem_wgrad(const bf16_t* x, const bf16_t* g, const bf16_t* y, const float* coef, float* dw,
-                                float* ws, int N, int H, int W, int P, int Q, int beta, hipStream_t st) {
+                                float* ws, int N, int H, int W, int P, int Q, int beta, int cin, hipStream_t st) {
+  if (cin != 3 && cin != 8) return hipErrorInvalidValue;
   if (P != (H + 6 - 7) / 2 + 1 || Q != (W + 6 - 7) / 2 + 1 || N <= 0) return hipErrorInvalidValue;
   const int units = N * ((P + stem::BAND - 1) / stem::BAND) * ((Q + stem::QB - 1) / stem::QB);
   const int G = ttdk_stem_wgrad_blocks(N, P, Q);
-  hipLaunchKernelGGL(stem::stem_wgrad_kernel, dim3(G), dim3(stem::THR), 0, st, x, g, y, coef, ws, N, H, W, P, Q, units);
+  if (cin == 3)
+    hipLaunchKernelGGL(stem::stem_wgrad_kernel<3>, dim3(G), dim3(stem::THR), 0, st, x, g, y, coef, ws, N, H, W, P, Q, units);
+  else
+    hipLaunchKernelGGL(stem::stem_wgrad_kernel<8>, dim3(G), dim3(stem::THR), 0, st, x, g, y, coef, ws, N, H, W, P, Q, units);
   float* sums = ws + static_cast<long long>(G) * stem::KO * stem::NC;
   hipError_t e = splitk_reduce(ws, G, static_cast<long long>(stem::KO) * stem::NC, sums, 0, st);
   if (e != hipSuccess) return e;

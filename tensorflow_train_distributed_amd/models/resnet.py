@@ -249,6 +249,17 @@ class ResNet:
         return (self.fuse_pw and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0
                 and (c.cout, c.cin_store) in self.PW_DGRAD_SHAPES and G.pw_ok(1 << 20, c.cin_store, c.cout))
 
+    def _stem_packed_ok(self, shape) -> bool:
+        """Both stem kernels (stem_fwd.hip, stem_wgrad.hip) take the unpadded [N,H,W,3] images."""
+        from ..ops import gemm as G
+        c = self.stem
+        w = (c.cout, c.k, c.k, c.cin_store)
+        from ..ops import kernels as K
+        return (self.device.type == "cuda" and self.stem_fwd_kernel and self.stem_kernel and self.fuse_bn_bwd
+                and shape[-1] == self.in_channels and K.stem_pool_fusable((shape[0], 112, 112, c.cout))
+                and G.stem_fwd_ok(shape, w, (c.stride, c.stride), (c.pad, c.pad), self.in_channels)
+                and G.stem_wgrad_ok(shape, w, (c.stride, c.stride), (c.pad, c.pad), self.in_channels))
+
     def _c3_ok(self, c: ConvSpec, H: int, W: int) -> bool:
         """3x3/s1 conv on the halo kernel (its input is H x W)."""
         from ..ops import gemm as G
@@ -357,15 +368,16 @@ class ResNet:
         pre = c.name + "_bn/"
         wname = c.name + "_conv/kernel"
         wshape = tuple(P.var[wname].shape)
+        stem_k = (self.stem_kernel and c is self.stem
+                  and G.stem_wgrad_ok(tuple(x.shape), wshape, (c.stride, c.stride), (c.pad, c.pad), self.in_channels))
         if (not need_dx and dstat is not None and self.fuse_bn_bwd
-                and G.conv_wgrad_bn_fusable(tuple(x.shape), wshape, (c.stride, c.stride), (c.pad, c.pad))):
+                and (stem_k or G.conv_wgrad_bn_fusable(tuple(x.shape), wshape, (c.stride, c.stride), (c.pad, c.pad)))):
             # weight gradient only (the stem): the BN backward is applied inside the weight
             # gradient's operand load, its output never stored (one HBM pass less at the very end
             # of the backward, where nothing else runs)
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
-            if self.stem_kernel and G.stem_wgrad_ok(tuple(x.shape), wshape, (c.stride, c.stride), (c.pad, c.pad),
-                                                    self.in_channels):
+            if stem_k:
                 G.stem_wgrad(x, dout, y, coef, out=P.g[wname])  # dedicated kernel (stem_wgrad.hip)
             else:
                 G.conv_wgrad_bn(x, dout, y, coef, wshape, (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
@@ -476,8 +488,11 @@ class ResNet:
             self._wgrad_stream = self._side
         if grad_scale is None:
             grad_scale = 1.0 / N
-        x = images if images.shape[-1] == self.in_store else K.pad_channels(images.contiguous(), self.in_store)
         fp8 = self._fp8 is not None
+        if images.shape[-1] == self.in_store or (self._stem_packed_ok(tuple(images.shape)) and not fp8):
+            x = images  # the dedicated stem kernels read the packed RGB (no channel-padding pass)
+        else:
+            x = K.pad_channels(images.contiguous(), self.in_store)
         if fp8:
             self._fp8_step_begin()
 

@@ -63,9 +63,9 @@ _SIGS = {
     "ttdk_gemm_f32": [P, L, I, P, L, I, P, L, P, I, I, I, I, P],
     # stem_fwd.hip / stem_wgrad.hip
     "ttdk_stem_fwd_blocks": [I],
-    "ttdk_stem_fwd": [P, P, P, P, I, I, I, P],
+    "ttdk_stem_fwd": [P, P, P, P, I, I, I, I, P],
     "ttdk_stem_wgrad_blocks": [I, I, I],
-    "ttdk_stem_wgrad": [P, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ttdk_stem_wgrad": [P, P, P, P, P, P, I, I, I, I, I, I, I, P],
     # conv3_halo.hip
     "ttdk_conv3_rows": [I, I, I, I, I],
     "ttdk_conv3_halo": [P, P, P, P, P, P, P, I, I, P, I, I, I, I, I, E, P],

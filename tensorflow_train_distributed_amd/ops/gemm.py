@@ -578,13 +578,14 @@ def conv_wgrad_bn(x, g_out, y, coef, w_shape, stride=(1, 1), padding=(0, 0), *, 
 def stem_fwd_ok(x_shape, w_shape, stride, padding, cin_real):
     """The ResNet stem shape the dedicated forward kernel (stem_fwd.hip) handles: 224 x 224 RGB
     stored with 8 channels, 64 7x7/2 filters."""
-    return (len(x_shape) == 4 and tuple(x_shape[1:]) == (224, 224, 8) and tuple(w_shape) == (64, 7, 7, 8)
+    return (len(x_shape) == 4 and tuple(x_shape[1:3]) == (224, 224) and x_shape[3] in (3, 8)
+            and tuple(w_shape) == (64, 7, 7, 8)
             and tuple(stride) == (2, 2) and tuple(padding) == (3, 3) and cin_real <= 3)
 
 
 def stem_fwd(x, w):
-    """Stem convolution (7x7/2, pad 3) over the 3 real input channels -> (y [N,112,112,64] bf16,
-    partial [T,2,64] per-workgroup BN (sum, sum of squares) of the stored y, T)."""
+    """Stem convolution (7x7/2, pad 3) over the 3 real input channels of x [N,224,224,3 or 8] ->
+    (y [N,112,112,64] bf16, partial [T,2,64] per-workgroup BN (sum, sum of squares) of y, T)."""
     _check(x, torch.bfloat16, "x")
     _check(w, torch.bfloat16, "w")
     N, H, W, _ = x.shape
@@ -592,20 +593,21 @@ def stem_fwd(x, w):
     T = int(_lib.query("ttdk_stem_fwd_blocks", N))
     partial = torch.empty((T, 2, 64), dtype=torch.float32, device=x.device)
     _log("stem_fwd", N * 112 * 112, 64, 147)
-    _lib.call("ttdk_stem_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(), partial.data_ptr(), N, H, W, _lib.stream())
+    _lib.call("ttdk_stem_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(), partial.data_ptr(), N, H, W, x.shape[3],
+              _lib.stream())
     return y, partial, T
 
 
 def stem_wgrad_ok(x_shape, w_shape, stride, padding, cin_real):
     """The ResNet stem shape the dedicated weight-gradient kernel (stem_wgrad.hip) handles."""
-    return (len(x_shape) == 4 and x_shape[-1] == 8 and tuple(w_shape) == (64, 7, 7, 8) and tuple(stride) == (2, 2)
+    return (len(x_shape) == 4 and x_shape[-1] in (3, 8) and tuple(w_shape) == (64, 7, 7, 8) and tuple(stride) == (2, 2)
             and tuple(padding) == (3, 3) and cin_real <= 3)
 
 
 def stem_wgrad(x, g_out, y, coef, *, out=None, beta=0):
     """Stem weight gradient with the stem BN backward on the fly: dz = coef[0]*g + coef[1]*y +
     coef[2], dW[64][7][7][8] = sum over pixels of dz x im2col(x) for the 3 real input channels
-    (the padded channels get 0). x [N,H,W,8]; g_out / y [N,P,Q,64]."""
+    (the padded channels get 0). x [N,H,W,3] or [N,H,W,8]; g_out / y [N,P,Q,64]."""
     _check(x, torch.bfloat16, "x")
     _check(g_out, torch.bfloat16, "g_out")
     _check(y, torch.bfloat16, "y")
@@ -617,7 +619,7 @@ def stem_wgrad(x, g_out, y, coef, *, out=None, beta=0):
     ws = torch.empty(nb * 64 * 160 + 64 * 160, dtype=torch.float32, device=x.device)
     _log("stem_wgrad", 64, 147, N * P * Q)
     _lib.call("ttdk_stem_wgrad", x.data_ptr(), g_out.data_ptr(), y.data_ptr(), coef.data_ptr(), out.data_ptr(),
-              ws.data_ptr(), N, H, W, P, Q, int(beta), _lib.stream())
+              ws.data_ptr(), N, H, W, P, Q, int(beta), x.shape[3], _lib.stream())
     return out
 
 

@@ -394,6 +394,9 @@ def test_stem_weight_gradient_kernel_matches_oracle():
     old = torch.randn_like(out)
     out2 = G.stem_wgrad(x, g, y, coef, out=old.clone(), beta=1)
     assert _rel(out2, ref + old) < 1e-2
+    # packed [N, H, W, 3] input: same sums (same LDS contents, same order)
+    out3 = G.stem_wgrad(x[..., :3].contiguous(), g, y, coef)
+    assert torch.equal(out3, out)
 
 
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
@@ -458,8 +461,8 @@ def test_persistent_register_epilogue_gemm_matches_one_tile_kernel(ta, tb, epi):
     assert torch.isfinite(y1.float()).all()
 
 
-@pytest.mark.parametrize("N", [3, 257])
-def test_stem_forward_kernel_matches_conv_oracle(N):
+@pytest.mark.parametrize("N,cin", [(3, 8), (257, 8), (3, 3)])
+def test_stem_forward_kernel_matches_conv_oracle(N, cin):
     """Dedicated stem forward (stem_fwd.hip: K = 7 taps x (s, c4) over the 3 real channels, no
     im2col) vs the fp32 convolution, and its per-workgroup BN sums vs the stored output."""
     from tensorflow_train_distributed_amd.ops import gemm as G
@@ -469,7 +472,7 @@ def test_stem_forward_kernel_matches_conv_oracle(N):
     w = (torch.randn(64, 7, 7, 8, device="cuda") * 0.1).bfloat16()
     w[..., 3:] = 0
     assert G.stem_fwd_ok(x.shape, w.shape, (2, 2), (3, 3), 3)
-    y, part, T = G.stem_fwd(x, w)
+    y, part, T = G.stem_fwd(x if cin == 8 else x[..., :3].contiguous(), w)
     torch.cuda.synchronize()
     n_chk = min(N, 4)
     xs = torch.cat([x[:2], x[-2:]]) if N > 4 else x

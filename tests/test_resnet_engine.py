@@ -211,3 +211,22 @@ def test_resnet_streaming_pointwise_fusions_match_unfused_engine(flag, size, bat
     # engine-vs-engine agreement is bounded by the same bf16 chaos (both are checked against the
     # fp32 oracle above, which is the correctness criterion)
     assert float(torch.dot(gf, gu) / (gf.norm() * gu.norm())) > 0.96
+
+
+@pytest.mark.gpu
+def test_packed_rgb_input_skips_padding_and_matches_padded():
+    """At 224 x 224 the dedicated stem kernels read the packed [N,224,224,3] images (no
+    channel-padding pass): the step must equal, bitwise, the one fed the 8-channel padded copy."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(0)
+    m = ResNet(((64, 1, 1), (128, 1, 2)), num_classes=10, device="cuda", seed=5)
+    x = torch.randn(2, 224, 224, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (2,), device="cuda")
+    assert m._stem_packed_ok(tuple(x.shape))
+    s8 = m.forward_backward(K.pad_channels(x.contiguous(), m.in_store), y).clone()
+    g8 = m.params.grad.clone()
+    s3 = m.forward_backward(x, y).clone()
+    g3 = m.params.grad.clone()
+    assert torch.equal(s3, s8)
+    assert torch.equal(g3, g8)
+    assert float(m.params.g["conv1_conv/kernel"][..., 3:].abs().sum()) == 0.0
