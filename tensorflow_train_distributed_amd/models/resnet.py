@@ -104,8 +104,10 @@ class ResNet:
         # halo-tiled 3x3 kernel (ops.gemm.conv3_halo) for the shapes it is compiled for, with the
         # producing BN apply / BN backward fused in as its operand prologue; TTD_FUSE_C3=0: off
         self.fuse_c3 = os.environ.get("TTD_FUSE_C3", "1") != "0" and precision == "bf16"
-        # data gradient on the halo kernel: off until it beats bwd-apply + conv_dgrad (tools/conv3_bench.py)
-        self.c3_dgrad = os.environ.get("TTD_C3_DGRAD", "0") != "0"
+        # halo-kernel data gradient of those convs: 2 = after the BN-backward pass, with the feeding
+        # unit's BN-backward sums in its epilogue (tools/conv3_bench.py: 648 -> 529 us at b1024);
+        # 1 = with the BN backward as its operand prologue (slower: 920 vs 863 us incl. the pass)
+        self.c3_dgrad = int(os.environ.get("TTD_C3_DGRAD", "2"))
         # stem weight gradient on its dedicated kernel (3 real input channels, BN backward on the fly)
         self.stem_kernel = os.environ.get("TTD_STEM_WGRAD", "1") != "0"
         # dedicated stem forward kernel (stem_fwd.hip: K = 7 x 32 over the 3 real channels)
@@ -402,7 +404,7 @@ class ResNet:
             self._wgrad(c, x, dz, wname)
             return out, (partial, T)
         if (need_dx and dstat is not None and feeds is not None and feeds2 is None and dx is None
-                and self.fuse_bn_bwd and self.c3_dgrad and self._c3_ok(c, x.shape[1], x.shape[2])):
+                and self.fuse_bn_bwd and self.c3_dgrad == 1 and self._c3_ok(c, x.shape[1], x.shape[2])):
             # halo 3x3 data gradient with this unit's BN backward as its operand prologue (dz is
             # written once there for the weight gradient) and the feeding unit's BN-backward
             # statistics in its epilogue
@@ -428,6 +430,12 @@ class ResNet:
         wt = K.krsc_to_crsk(P.c[wname])
         stride, pad = (c.stride, c.stride), (c.pad, c.pad)
         bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
+        if (feeds is not None and feeds2 is None and dx is None and self.fuse_bn_bwd and self.c3_dgrad == 2
+                and self._c3_ok(c, x.shape[1], x.shape[2])):
+            # halo 3x3 kernel (flipped filter) with the feeding unit's BN-backward sums in its epilogue
+            _, fy, fmask, _ = feeds
+            out, partial, T = G.conv3_halo(dz, wt, flip=True, bn_stat=(fy, fmask))
+            return out, (partial, T)
         if (feeds is not None and self.fuse_bn_bwd
                 and G.dgrad_stat_rows(tuple(x.shape), tuple(wt.shape), stride, pad) is not None):
             _, fy, fmask, _ = feeds

@@ -67,6 +67,11 @@ def main():
                                         dz.data_ptr(), M * N, N, _lib.stream()),
                               G.conv_dgrad(dz, wt, (B, H, W, C), (1, 1), (1, 1), bn_stat=(fy, fm))),
         "dgrad_c3": lambda: G.conv3_halo(g, wt, flip=True, prologue=("bn_bwd", y, None, coef, dz), bn_stat=(fy, fm)),
+        "dgrad_c3p0": lambda: (_lib.call("ttdk_bn_bwd_apply", g.data_ptr(), None, None, y.data_ptr(), coef.data_ptr(),
+                                         dz.data_ptr(), M * N, N, _lib.stream()),
+                               G.conv3_halo(dz, wt, flip=True, bn_stat=(fy, fm))),
+        "dg_gemm": lambda: G.conv_dgrad(dz, wt, (B, H, W, C), (1, 1), (1, 1), bn_stat=(fy, fm)),
+        "dg_c3": lambda: G.conv3_halo(dz, wt, flip=True, bn_stat=(fy, fm)),
     }
     res = {k: [] for k in variants}
     for _ in range(args.rounds):
