@@ -15,9 +15,11 @@
 // The 21 input rows a band reads live in an LDS ring (input row h in slot h % 21, 4 channels,
 // 3 zero columns each side), so each further band of the image adds 16 rows, prefetched into
 // registers under the previous band's MFMAs. The filter is staged once per workgroup as
-// [k][r][s][c4] rows. Results go from the accumulators to 16-B stores (lane pairs swap halves:
-// 16 pixels x 64 contiguous bytes per store); BN sum / sum of squares of the rounded values
-// accumulate per lane and are reduced once per workgroup into part[block][2][64].
+// [k][r][s][c4] rows and held as MFMA B fragments in registers (112 VGPRs) for the whole launch.
+// A wave computes its row one 16-pixel block at a time (28 MFMAs) and stores that block right
+// away (lane pairs swap halves: 16 pixels x 64 contiguous bytes per store), so the stores drain
+// under the next block's MFMAs; BN sum / sum of squares accumulate per lane (packed fp32
+// pairs) and are reduced once per workgroup into part[block][2][64].
 #include "gemm_conv.h"
 
 namespace ttdk {
@@ -63,6 +65,14 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
   // the ring starts zero: the pad columns and (3-channel input) channel 3 are never written
   for (int i = tid; i < RING * XP / 16; i += THR) reinterpret_cast<uint4*>(xs)[i] = make_uint4(0, 0, 0, 0);
 
+  __syncthreads();
+  // the filter as MFMA B fragments, resident in registers for the whole launch (28 x 16 B)
+  bf16x8_t bw[7][4];
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) bw[r][cb] = lds_read_b128(ws + (cb * 16 + i16) * WP + (r * 4 + g) * 16);
+
   // 8-channel input: pixel loads (channels 0..3 kept)
   auto xpix = [&](int n, int h, int col) -> uint2 {
     if (h < 0 || h >= H) return make_uint2(0, 0);
@@ -85,11 +95,14 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
     }
   };
 
-  float st[4][4], sq[4][4];  // BN partial sums of this lane's channels cb*16 + 4g + v
+  // BN partial sums of this lane's channels cb*16 + 4g + 2h + {0,1}, as packed fp32 pairs
+  // (v_pk_add_f32 / v_pk_fma_f32)
+  typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+  f32x2_t st[4][2], sq[4][2];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) st[cb][v] = sq[cb][v] = 0.f;
+    for (int h = 0; h < 2; ++h) st[cb][h] = sq[cb][h] = f32x2_t{0.f, 0.f};
 
   const int bands = P / BAND;
   for (int n = n_begin; n < n_end; ++n) {
@@ -125,49 +138,44 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
           nx3[i] = (pre && idx < NEWR * RC3) ? xchunk(n, 2 * p0 + 2 * BAND + 2 + rr, j) : make_uint4(0, 0, 0, 0);
         }
       }
-      // wave: output row p = p0 + wave
+      // wave: output row p = p0 + wave, one 16-pixel block at a time (7 taps x 4 channel blocks
+      // of MFMAs, then that block's stores, which drain under the next block's MFMAs)
       const int p = p0 + wave;
-      f32x4_t acc[QB][4];
+      int roff[7];
 #pragma unroll
-      for (int pb = 0; pb < QB; ++pb)
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) acc[pb][cb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-      for (int r = 0; r < 7; ++r) {
-        const char* row = xs + ring_slot(2 * p - 3 + r) * XP;
-        bf16x8_t bfr[4];
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) bfr[cb] = lds_read_b128(ws + (cb * 16 + i16) * WP + (r * 4 + g) * 16);
-#pragma unroll
-        for (int pb = 0; pb < QB; ++pb) {
-          // columns 2q-3+2g, 2q-2+2g (q = 16 pb + i16) = staged columns 2q+2g, 2q+2g+1
-          const bf16x8_t afr = lds_read_b128(row + (2 * (pb * 16 + i16) + 2 * g) * 8);
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) acc[pb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[cb], afr, acc[pb][cb], 0, 0, 0);
-        }
-      }
-      // store: lane holds pixel 16 pb + i16, channels cb*16 + 4g + v. Lane pairs (g, g^1) swap
-      // so the even lane stores channels cb0*16 + 4g .. +7 and the odd lane those of cb0 + 1.
+      for (int r = 0; r < 7; ++r) roff[r] = ring_slot(2 * p - 3 + r) * XP + 2 * g * 8;
       bf16_t* yrow = y + (static_cast<long long>(n) * P + p) * Q * KO;
       const bool odd = g & 1;
-#pragma unroll
+#pragma unroll 1
       for (int pb = 0; pb < QB; ++pb) {
         const int q = pb * 16 + i16;
+        f32x4_t acc[4];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 7; ++r) {
+          // columns 2q-3+2g, 2q-2+2g = staged columns 2q+2g, 2q+2g+1
+          const bf16x8_t afr = lds_read_b128(xs + roff[r] + 2 * q * 8);
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[r][cb], afr, acc[cb], 0, 0, 0);
+        }
+        // lane holds pixel q, channels cb*16 + 4g + v. Lane pairs (g, g^1) swap so the even lane
+        // stores channels cb0*16 + 4g .. +7 and the odd lane those of cb0 + 1.
 #pragma unroll
         for (int cp = 0; cp < 2; ++cp) {
           uint2 pk[2];
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2) {
             const int cb = 2 * cp + h2;
-            const f32x4_t v = acc[pb][cb];
+            const f32x4_t v = acc[cb];
             pk[h2] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-            const float rv[4] = {bf2f(static_cast<bf16_t>(pk[h2].x & 0xffff)), bf2f(static_cast<bf16_t>(pk[h2].x >> 16)),
-                                 bf2f(static_cast<bf16_t>(pk[h2].y & 0xffff)), bf2f(static_cast<bf16_t>(pk[h2].y >> 16))};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              st[cb][j] += rv[j];
-              sq[cb][j] += rv[j] * rv[j];
-            }
+            // statistics of the values actually stored (bf16-rounded)
+            const f32x2_t v01 = {bf2f(static_cast<bf16_t>(pk[h2].x & 0xffff)), bf2f(static_cast<bf16_t>(pk[h2].x >> 16))};
+            const f32x2_t v23 = {bf2f(static_cast<bf16_t>(pk[h2].y & 0xffff)), bf2f(static_cast<bf16_t>(pk[h2].y >> 16))};
+            st[cb][0] += v01;
+            st[cb][1] += v23;
+            sq[cb][0] += v01 * v01;
+            sq[cb][1] += v23 * v23;
           }
           const uint2 snd = odd ? pk[0] : pk[1];
           const uint2 rcv = make_uint2(__shfl_xor(snd.x, 16, 64), __shfl_xor(snd.y, 16, 64));
@@ -192,14 +200,17 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
     }
   }
   // BN partial sums: over the 16 pixel lanes of each channel group, then over the waves
+  float fs[4][4], fq[4][4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      fs[cb][j] = st[cb][j >> 1][j & 1];
+      fq[cb][j] = sq[cb][j >> 1][j & 1];
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
-        st[cb][j] += __shfl_xor(st[cb][j], o, 64);
-        sq[cb][j] += __shfl_xor(sq[cb][j], o, 64);
+        fs[cb][j] += __shfl_xor(fs[cb][j], o, 64);
+        fq[cb][j] += __shfl_xor(fq[cb][j], o, 64);
       }
     }
   if (i16 == 0) {
@@ -207,8 +218,8 @@ __global__ __launch_bounds__(THR, 1) void stem_fwd_kernel(const bf16_t* __restri
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        red[wave][0][cb * 16 + 4 * g + j] = st[cb][j];
-        red[wave][1][cb * 16 + 4 * g + j] = sq[cb][j];
+        red[wave][0][cb * 16 + 4 * g + j] = fs[cb][j];
+        red[wave][1][cb * 16 + 4 * g + j] = fq[cb][j];
       }
   }
   __syncthreads();
