@@ -91,6 +91,9 @@ class ResNet:
         self.device = torch.device(device)
         # weight gradients on a second HIP stream (TTD_WGRAD_STREAM=0: single stream)
         self.wgrad_stream = os.environ.get("TTD_WGRAD_STREAM", "1") != "0" and self.device.type == "cuda"
+        # projection-shortcut backward (BN backward + strided dgrad) on the side stream, concurrent
+        # with the block's c3 -> c2 data-gradient chain (joins before c1's dgrad accumulates into it)
+        self.cd_side = os.environ.get("TTD_CD_SIDE", "1") != "0"
         # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
         # never stored: two HBM passes of the stage's largest tensor saved; TTD_FUSE_PROJ=0: off)
         self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
@@ -351,7 +354,7 @@ class ResNet:
         return out, [x, y, mask, st]
 
     def _convbn_bwd(self, c: ConvSpec, dout, ctx, need_dx=True, g_out=None, dx=None, dx_beta=0, dstat=None,
-                    feeds=None, feeds2=None, sampled_only=False, dx_sampled=False):
+                    feeds=None, feeds2=None, sampled_only=False, dx_sampled=False, wgrad_last=False):
         """Backward of one conv+BN(+ReLU) unit. dout: gradient of the unit's output; with
         dstat = (partial, T) it is already ReLU-masked and its BN-backward sums came from the
         producing dgrad's epilogue. feeds: ctx of the conv+BN unit whose output is this conv's
@@ -424,7 +427,8 @@ class ResNet:
             dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
                                P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
                                mask=mask).view(N, Pp, Q, Kc)
-        self._wgrad(c, x, dz, wname)
+        if not wgrad_last:
+            self._wgrad(c, x, dz, wname)
         if not need_dx:
             return None, None
         wt = K.krsc_to_crsk(P.c[wname])
@@ -446,10 +450,17 @@ class ResNet:
             out, partial, T = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, bn_stat=(fy, fmask),
                                            beta_s2=bs2)
             return out, (partial, T)
-        return G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, sampled_only=sampled_only,
-                            beta_s2=bs2), None
+        out = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, sampled_only=sampled_only, beta_s2=bs2)
+        if wgrad_last:
+            # data gradient first (its consumer waits on this event), then the weight gradient
+            self._cd_done = torch.cuda.Event()
+            self._cd_done.record()
+            # its gradient-ready hook waits for the caller: the variables before it in the flat
+            # layout (the block's c3 and c2) are not final yet
+            self._wgrad(c, x, dz, wname, ready=False)
+        return out, None
 
-    def _wgrad(self, c: ConvSpec, x, dz, wname):
+    def _wgrad(self, c: ConvSpec, x, dz, wname, ready=True):
         """Weight gradient of conv c into its flat gradient slice; on the side stream when enabled,
         concurrent with the data-gradient chain (fills the tail waves of the 1-workgroup-per-CU
         GEMMs), then the gradient-ready hook (collectives order after the side stream)."""
@@ -457,19 +468,22 @@ class ResNet:
         P = self.params
         side = self._wgrad_stream
         if side is not None:
-            ev = torch.cuda.Event()
-            ev.record()
-            side.wait_event(ev)
+            if torch.cuda.current_stream() != side:  # (a stream waiting on its own event breaks hipGraph capture)
+                ev = torch.cuda.Event()
+                ev.record()
+                side.wait_event(ev)
             with torch.cuda.stream(side):
                 G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
-                self._ready(c.name + "_bn/moving_variance")
+                if ready:
+                    self._ready(c.name + "_bn/moving_variance")
             # keep the operands alive until the streams join at the end of the backward (no
             # record_stream: its deferred frees made the allocator re-malloc when the host ran
             # several steps ahead)
             self._side_keep += [x, dz]
         else:
             G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
-            self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
+            if ready:
+                self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
 
     def _ready(self, name):
         if self._grad_hook is not None:
@@ -609,6 +623,27 @@ class ResNet:
             c1, c2, c3, cd = ctxs[i]
             prev_c3 = ctxs[i - 1][2] if i > 0 else None  # the unit that produced this block's input
             prev_cd = ctxs[i - 1][3] if i > 0 else None  # its projection shortcut (fed by the same gradient)
+            side = self._wgrad_stream
+            cd_side = blk["cd"] is not None and dh_stat is not None and side is not None and self.cd_side
+            sampled = False
+            if blk["cd"] is not None:
+                cd_stat = (dh_stat[2], dh_stat[1]) if dh_stat is not None and len(dh_stat) == 3 else None
+                # a stride-2 projection writes only the pixels it samples; c1's accumulate reads it there
+                sampled = self.sampled_dgrad and blk["cd"].stride != 1 and blk["cd"].pad == 0
+            cd_done = None
+            if cd_side:
+                # projection branch (BN backward + strided dgrad, then its weight gradient) on the side
+                # stream, concurrent with the c3 -> c2 chain; c1's dgrad below accumulates into dx
+                ev = torch.cuda.Event()
+                ev.record()
+                side.wait_event(ev)
+                self._cd_done = None
+                with torch.cuda.stream(side):
+                    dx, _ = self._convbn_bwd(blk["cd"], dh, cd, dstat=cd_stat, sampled_only=sampled, wgrad_last=True)
+                    cd_done = self._cd_done
+                assert cd_done is not None, "projection backward took a path without the wgrad_last event"
+                # dx was made on the side stream and dh is read there: both alive until the streams join
+                self._side_keep += [dx, dh]
             if dh_stat is not None:
                 g_sc = dh  # already ReLU-masked by the producing dgrad epilogue
                 d2, st2 = self._convbn_bwd(blk["c3"], dh, c3, dstat=dh_stat[:2], feeds=c2)
@@ -616,13 +651,16 @@ class ResNet:
                 g_sc = torch.empty_like(dh)
                 d2, st2 = self._convbn_bwd(blk["c3"], dh, c3, g_out=g_sc, feeds=c2)
             d1, st1 = self._convbn_bwd(blk["c2"], d2, c2, dstat=st2, feeds=c1)
-            if blk["cd"] is not None:
-                cd_stat = (dh_stat[2], dh_stat[1]) if dh_stat is not None and len(dh_stat) == 3 else None
-                # a stride-2 projection writes only the pixels it samples; c1's accumulate reads it there
-                sampled = self.sampled_dgrad and blk["cd"].stride != 1 and blk["cd"].pad == 0
+            if cd_done is not None:
+                # c3 / c2 weight gradients are now queued on the side stream behind the projection's:
+                # the bucket hook for the projection variables can fire (in flat-layout order)
+                with torch.cuda.stream(side):
+                    self._ready(blk["cd"].name + "_bn/moving_variance")
+                torch.cuda.current_stream().wait_event(cd_done)
+            elif blk["cd"] is not None:
                 dx, _ = self._convbn_bwd(blk["cd"], g_sc, cd, dstat=cd_stat, sampled_only=sampled)
             else:
-                dx, sampled = g_sc, False
+                dx = g_sc
             dh, dh_stat = self._convbn_bwd(blk["c1"], d1, c1, dx=dx, dx_beta=1, dstat=st1, feeds=prev_c3,
                                            feeds2=prev_cd, dx_sampled=sampled)
         if pool_fused:

@@ -230,3 +230,21 @@ def test_packed_rgb_input_skips_padding_and_matches_padded():
     assert torch.equal(s3, s8)
     assert torch.equal(g3, g8)
     assert float(m.params.g["conv1_conv/kernel"][..., 3:].abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
+def test_gradient_ready_hooks_fire_in_flat_layout_order():
+    """The bucketed all-reduce launches every bucket up to the variable a hook names, so the
+    engine's hooks must come in flat-layout order even with branches on the side stream (the
+    projection backward runs there, concurrent with c3 -> c2)."""
+    torch.manual_seed(0)
+    m = ResNet(((64, 2, 1), (128, 1, 2)), num_classes=10, device="cuda", seed=5)
+    x = torch.randn(4, 32, 32, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (4,), device="cuda")
+    names = []
+    m.forward_backward(x, y, grad_hook=names.append)
+    torch.cuda.synchronize()
+    off = [m.params.offsets[n] for n in names]
+    assert off == sorted(off), names
+    convs = [c.name for c in m.conv_list()]
+    assert sorted(n.split("_bn/")[0] for n in names if n.endswith("_bn/moving_variance")) == sorted(convs)
