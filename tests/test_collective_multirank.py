@@ -18,6 +18,17 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _by_value(d):
+    """Tensors -> numpy for the result queue: a tensor is shared by file descriptor, which races
+    with the worker's exit (EOFError in the parent); numpy arrays are pickled by value."""
+    return {k: (v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in d.items()}
+
+
+def _as_tensors(d):
+    import numpy as np
+    return {k: (torch.from_numpy(v) if isinstance(v, np.ndarray) else v) for k, v in d.items()}
+
+
 def _spawn(fn, world, tmp_path, *args):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -29,7 +40,7 @@ def _spawn(fn, world, tmp_path, *args):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    return sorted(res, key=lambda r: r["rank"])
+    return sorted((_as_tensors(r) for r in res), key=lambda r: r["rank"])
 
 
 def _reducer_worker(rank, world, store, q, compress, algorithm="allreduce", num_packs=None):
@@ -54,8 +65,8 @@ def _reducer_worker(rank, world, store, q, compress, algorithm="allreduce", num_
         red.mark_ready(s.name)
         order.append(list(red.launch_log))
     red.finish()
-    q.put({"rank": rank, "grad": p.grad.clone(), "local": local, "buckets": red.buckets,
-           "log": red.launch_log, "order": order, "bytes": red.bytes_per_step()})
+    q.put(_by_value({"rank": rank, "grad": p.grad.clone(), "local": local, "buckets": red.buckets,
+           "log": red.launch_log, "order": order, "bytes": red.bytes_per_step()}))
     dist.destroy_process_group()
 
 
@@ -125,7 +136,7 @@ def _mlp_worker(rank, world, store, q):
     dp = model.params.grad.clone()
     # the same step on one replica holding the whole global batch
     model.forward_backward({"x-input": x, "y-input": y})
-    q.put({"rank": rank, "dp": dp, "big": model.params.grad.clone(), "w": model.params.master.clone()})
+    q.put(_by_value({"rank": rank, "dp": dp, "big": model.params.grad.clone(), "w": model.params.master.clone()}))
     dist.destroy_process_group()
 
 
@@ -186,8 +197,8 @@ def _tape_worker(rank, world, store, q):
     for i in range(4):
         xs, ys = X[i, rank * B:(rank + 1) * B], Y[i, rank * B:(rank + 1) * B]
         losses.append(float(strategy.reduce(S.ReduceOp.SUM, strategy.run(step_fn, args=(xs, ys)))))
-    q.put({"rank": rank, "w": model.params.master.clone(), "names": model.params.names(), "losses": losses,
-           "X": X, "Y": Y, "init": getattr(model, "_ttd_init", None)})
+    q.put(_by_value({"rank": rank, "w": model.params.master.clone(), "names": model.params.names(), "losses": losses,
+           "X": X, "Y": Y, "init": getattr(model, "_ttd_init", None)}))
     dist.destroy_process_group()
 
 
