@@ -257,8 +257,11 @@ def main():
     # hipGraph capture of the whole step pays only when the host cannot keep ahead of the GPU;
     # measured neutral for ResNet-50 at batch 256 (GPU-bound), so auto = off.
     use_graph = args.graph if args.graph >= 0 else 0
-    if on_cpu or world > 1:
-        use_graph = 0  # collectives are issued eagerly (bucket order follows backward)
+    red0 = getattr(step, "reducer", None)
+    if on_cpu or (world > 1 and getattr(red0, "comm", None) is None):
+        # torch process-group collectives are issued eagerly; the native RCCL engine's bucket
+        # launches are stream-ordered and capture into the step's hipGraph
+        use_graph = 0
     graph = None
     out = None
     # The step (its main chain; the weight gradients stay on the engine's normal-priority side
@@ -335,6 +338,9 @@ def main():
         nbytes_all = red.flat.numel * 4
         sizes = sorted({min(nbytes_all, 4 << 20), min(nbytes_all, int(args.bucket_mb * (1 << 20))), nbytes_all})
         for nb in sizes:
+            if red.comm is not None:  # the native engine's own communicator and stream
+                probe.append(red.comm.probe(nb, iters=5))
+                continue
             buf = torch.zeros(nb // 4, dtype=torch.float32, device=dev)
             dist.all_reduce(buf)
             sync()
@@ -365,6 +371,10 @@ def main():
             dinfo["allreduce_bytes_per_step"] = red.bytes_per_step() if world > 1 else 0
             dinfo["buckets"] = len(red.buckets)
             dinfo["allreduce_dtype"] = "bf16" if red.compress else "fp32"
+            dinfo["collective_engine"] = red.engine
+            if world > 1 and red.comm is None and backend == "nccl":
+                from tensorflow_train_distributed_amd.parallel import rccl
+                dinfo["native_engine_unavailable"] = rccl.failure_reason() or os.environ.get("TTD_COLLECTIVE")
         if probe is not None:
             dinfo["allreduce_probe"] = probe
         if backend == "nccl" and world > 1:

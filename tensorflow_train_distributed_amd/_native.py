@@ -113,7 +113,10 @@ def build_hip(force: bool = False) -> str:
     objs, changed = _build_objects(
         srcs, hdrs, lambda s, o: [hipcc, *flags, "-c", s, "-o", o], ".hip.o")
     if changed or not os.path.exists(HIP_LIB) or os.path.getmtime(HIP_LIB) < _newest_mtime(objs):
-        _run([hipcc, "--offload-arch=" + HIP_ARCH, "-shared", "-fPIC", "-o", HIP_LIB, *objs])
+        # librccl.so.1: the native collective engine (collective.hip). At run time the soname
+        # resolves to the RCCL torch already loaded, so the process holds one RCCL.
+        _run([hipcc, "--offload-arch=" + HIP_ARCH, "-shared", "-fPIC", "-o", HIP_LIB, *objs,
+              "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
     return HIP_LIB
 
 

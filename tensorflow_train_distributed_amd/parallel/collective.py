@@ -18,6 +18,11 @@ Design for MI355X:
   keeps ResNet-50 (~100 MB of fp32 gradients) at four collectives;
 * `finish()` makes the compute stream wait for the collectives (no host sync).
 
+On GPU process groups the buckets go through the native RCCL engine (`rccl.py`,
+`csrc/kernels/collective.hip`): its own communicator and HIP stream, an event fork per bucket,
+bf16 compression cast on the communicator stream, capture-safe. `TTD_COLLECTIVE=torch` (or a
+failed start-up self-check on any rank) routes them through torch.distributed instead.
+
 Gradients are pre-scaled by 1/world (the loss gradient scale), so SUM == mean.
 
 Reduction algorithms (tf.distribute cross-device ops, strategy.py):
@@ -44,7 +49,10 @@ ALGORITHMS = ("allreduce", "hierarchical", "reduce_to_one")
 
 class BucketedAllReducer:
     def __init__(self, flat, group=None, bucket_mb: float = 32.0, first_bucket_mb: float = 4.0,
-                 compress_bf16: bool = False, algorithm: str = "allreduce", num_packs: Optional[int] = None):
+                 compress_bf16: bool = False, algorithm: str = "allreduce", num_packs: Optional[int] = None,
+                 engine: str = "auto"):
+        """engine: "auto" (native RCCL engine on GPU process groups of > 1 rank), "native"
+        (required; also on a one-rank group — tests), "torch" (torch.distributed calls)."""
         if algorithm not in ALGORITHMS:
             raise ValueError("unknown all-reduce algorithm %r (one of %s)" % (algorithm, ALGORITHMS))
         self.flat = flat
@@ -77,6 +85,14 @@ class BucketedAllReducer:
         if start < flat.numel:
             self.buckets.append((start, flat.numel))
         self._bucket_ends = [b[1] for b in self.buckets]
+        # GPU process groups: the native RCCL engine (rccl.py / collective.hip) unless
+        # TTD_COLLECTIVE=torch or its self-check failed on some rank
+        self.comm = None
+        if engine == "native" or (engine == "auto" and self.world > 1 and flat.grad.is_cuda):
+            from . import rccl
+            self.comm = rccl.for_group(group, required=engine == "native")
+        self.engine = "native-rccl" if self.comm is not None else ("torch-" + dist.get_backend(group)
+                                                                   if self.world > 1 else "none")
         self._next = 0
         self._works = []
         self._keep = []
@@ -96,7 +112,11 @@ class BucketedAllReducer:
         s, e = self.buckets[i]
         t = self.flat.grad[s:e]
         self.launch_log.append(i)
-        if self.world == 1:
+        if self.world == 1 and self.comm is None:
+            return
+        if self.comm is not None:
+            # in place on the communicator stream, ordered after the current (producing) stream
+            self.comm.bucket(t, algorithm=self.algorithm, compress=self.compress)
             return
         c = t.to(torch.bfloat16) if self.compress else t
         if self.algorithm == "allreduce":
@@ -149,6 +169,9 @@ class BucketedAllReducer:
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
+        if self.comm is not None:
+            self.comm.join()  # the current stream waits for the buckets (no host sync)
+            return
         works, self._works = self._works, []
         for w, c, t in works:
             try:

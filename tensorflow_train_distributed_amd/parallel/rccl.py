@@ -1,0 +1,251 @@
+"""Native RCCL communicator (csrc/kernels/collective.hip) for the gradient all-reduce.
+
+`BucketedAllReducer` (collective.py) launches its buckets through this engine on GPU process
+groups: one RCCL communicator per replica group, created from rank 0's unique id (handed out
+over the existing torch process group), with its own HIP stream. A bucket launch is an event
+fork from the stream that produced the bucket's last gradient onto the communicator stream,
+then the in-place RCCL call(s); `join()` makes the consumer stream wait. No host
+synchronisation anywhere on the step path, and the calls are capture-safe (hipGraph).
+
+Tuning knobs (environment, read at communicator creation):
+  TTD_RCCL_MAX_CTAS / TTD_RCCL_MIN_CTAS  RCCL's CTA (workgroup) budget per collective: how many
+                                         CUs a bucket all-reduce may occupy while it overlaps
+                                         the backward GEMMs (default: RCCL's own choice)
+  TTD_RCCL_PRIO                          communicator stream priority (default 0 = normal, below
+                                         the main chain's high-priority stream)
+  TTD_RCCL_TIMEOUT                       seconds before a collective that makes no progress (a
+                                         dead peer) is reported as an error (default 300)
+  TTD_RCCL_NONBLOCKING=1                 non-blocking communicator: creation polled against the
+                                         deadline too (not capture-safe: RCCL may issue from its
+                                         own thread)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_char_p, c_double, c_float, c_int, c_longlong, c_void_p
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..utils import errors
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float64: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5}
+_OP = {"sum": 0, "avg": 1, "min": 2, "max": 3}
+_ALGO = {"allreduce": 0, "hierarchical": 1, "reduce_to_one": 2}
+
+_bound = False
+
+
+def _lib():
+    global _bound
+    lib = _native.hip()
+    if not _bound:
+        lib.ttdc_error.restype = c_char_p
+        lib.ttdc_error.argtypes = [c_void_p]
+        lib.ttdc_version.restype = c_int
+        lib.ttdc_unique_id.restype = c_int
+        lib.ttdc_unique_id.argtypes = [c_char_p]
+        lib.ttdc_create.restype = c_void_p
+        lib.ttdc_create.argtypes = [c_char_p, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_int]
+        lib.ttdc_stream.restype = c_void_p
+        lib.ttdc_stream.argtypes = [c_void_p]
+        lib.ttdc_bucket.restype = c_int
+        lib.ttdc_bucket.argtypes = [c_void_p, c_void_p, c_longlong, c_int, c_int, c_int, c_int, c_void_p]
+        lib.ttdc_join.restype = c_int
+        lib.ttdc_join.argtypes = [c_void_p, c_void_p]
+        lib.ttdc_collective.restype = c_int
+        lib.ttdc_collective.argtypes = [c_void_p, c_int, c_void_p, c_longlong, c_int, c_int, c_int, c_void_p]
+        lib.ttdc_synchronize.restype = c_int
+        lib.ttdc_synchronize.argtypes = [c_void_p]
+        lib.ttdc_probe.restype = c_int
+        lib.ttdc_probe.argtypes = [c_void_p, c_void_p, c_longlong, c_int, ctypes.POINTER(c_float)]
+        lib.ttdc_destroy.restype = None
+        lib.ttdc_destroy.argtypes = [c_void_p, c_int]
+        _bound = True
+    return lib
+
+
+def rccl_version() -> int:
+    """Version code of the RCCL the process actually loaded (torch's bundled one when torch
+    came first: both export the soname librccl.so.1)."""
+    return int(_lib().ttdc_version())
+
+
+def unique_id() -> bytes:
+    lib = _lib()
+    buf = ctypes.create_string_buffer(128)
+    if lib.ttdc_unique_id(buf) != 128:
+        raise errors.InternalError("ncclGetUniqueId failed: %s" % lib.ttdc_error(None).decode())
+    return buf.raw
+
+
+def _stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+class RcclCommunicator:
+    """One RCCL communicator + its HIP stream. Create it on every rank of the group with the
+    same `uid` (rank 0's `unique_id()`), or through `for_group` which distributes the id."""
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: torch.device, priority: Optional[int] = None,
+                 min_ctas: Optional[int] = None, max_ctas: Optional[int] = None, timeout: Optional[float] = None,
+                 nonblocking: Optional[bool] = None):
+        lib = _lib()
+        env = os.environ.get
+        prio = int(env("TTD_RCCL_PRIO", "0")) if priority is None else int(priority)
+        min_ctas = int(env("TTD_RCCL_MIN_CTAS", "0")) if min_ctas is None else int(min_ctas)
+        max_ctas = int(env("TTD_RCCL_MAX_CTAS", "0")) if max_ctas is None else int(max_ctas)
+        timeout = float(env("TTD_RCCL_TIMEOUT", "300")) if timeout is None else float(timeout)
+        nonblocking = env("TTD_RCCL_NONBLOCKING", "0") == "1" if nonblocking is None else bool(nonblocking)
+        self.device = torch.device(device)
+        self.rank, self.nranks = int(rank), int(nranks)
+        self.max_ctas = max_ctas
+        with torch.cuda.device(self.device):
+            h = lib.ttdc_create(uid, self.nranks, self.rank, self.device.index, prio, min_ctas, max_ctas, timeout,
+                                1 if nonblocking else 0)
+        if not h:
+            raise errors.UnavailableError("RCCL communicator creation failed: %s"
+                                          % lib.ttdc_error(None).decode())
+        self._h = h
+        self.stream = torch.cuda.ExternalStream(lib.ttdc_stream(h), device=self.device)
+
+    @classmethod
+    def for_group(cls, group=None, device=None, **kw) -> "RcclCommunicator":
+        """Collective over `group`: rank 0 draws the unique id, the torch process group carries
+        it to the others."""
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        ids = torch.zeros(128, dtype=torch.uint8, device=dev if dist.get_backend(group) == "nccl" else "cpu")
+        if rank == 0:
+            ids.copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
+        dist.broadcast(ids, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        return cls(bytes(ids.cpu().tolist()), world, rank, dev, **kw)
+
+    # ------------------------------------------------------------------ step path
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise errors.UnavailableError("%s: %s" % (what, self.error))
+
+    @property
+    def error(self) -> str:
+        return _lib().ttdc_error(self._h).decode("utf-8", "replace") if self._h else "destroyed"
+
+    def bucket(self, t: torch.Tensor, op: str = "sum", algorithm: str = "allreduce", compress: bool = False,
+               producer=None):
+        """In-place reduction of contiguous `t` on the communicator stream, ordered after the
+        work already queued on `producer` (default: the current stream)."""
+        assert t.is_contiguous() and t.device == self.device
+        self._check(_lib().ttdc_bucket(self._h, t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], _ALGO[algorithm],
+                                       1 if compress else 0, _stream_ptr(producer)), "bucket all-reduce")
+
+    def join(self, consumer=None):
+        """`consumer` (default: current stream) waits for every collective queued so far."""
+        self._check(_lib().ttdc_join(self._h, _stream_ptr(consumer)), "collective join")
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum", stream=None) -> torch.Tensor:
+        """Stream-ordered in-place all-reduce on `stream` (default: current)."""
+        assert t.is_contiguous()
+        self._check(_lib().ttdc_collective(self._h, 0, t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], 0,
+                                           _stream_ptr(stream)), "all-reduce")
+        return t
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0, stream=None) -> torch.Tensor:
+        assert t.is_contiguous()
+        self._check(_lib().ttdc_collective(self._h, 1, t.data_ptr(), t.numel(), _DT[t.dtype], 0, int(root),
+                                           _stream_ptr(stream)), "broadcast")
+        return t
+
+    def synchronize(self):
+        """Host wait for the communicator stream with a deadline (a dead peer raises)."""
+        self._check(_lib().ttdc_synchronize(self._h), "collective synchronize")
+
+    def probe(self, nbytes: int, iters: int = 5) -> Dict[str, float]:
+        """RCCL bus bandwidth of an fp32 all-reduce of `nbytes` on the communicator stream."""
+        buf = torch.zeros(max(1, nbytes // 4), dtype=torch.float32, device=self.device)
+        ms = c_float(0.0)
+        self._check(_lib().ttdc_probe(self._h, buf.data_ptr(), buf.numel(), int(iters), ctypes.byref(ms)), "probe")
+        t = float(ms.value)
+        bw = 2.0 * (self.nranks - 1) / self.nranks * nbytes / (t * 1e-3) / 1e9 if t > 0 else 0.0
+        return {"bytes": int(nbytes), "ms": round(t, 4), "busbw_GBps": round(bw, 1)}
+
+    def destroy(self, abort: bool = False):
+        if self._h:
+            _lib().ttdc_destroy(self._h, 1 if abort else 0)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy(abort=True)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+# one communicator per (process-group generation, group); recovery aborts them (strategy.py)
+_COMMS: Dict[tuple, RcclCommunicator] = {}
+_FAILED: Dict[tuple, str] = {}
+
+
+def _key(group):
+    from .strategy import _PG
+    return (_PG["generation"], id(group) if group is not None else None)
+
+
+def for_group(group=None, required: bool = False) -> Optional[RcclCommunicator]:
+    """The native communicator of `group` (created and self-checked on first use), or None when
+    the native engine does not apply: a non-RCCL group (gloo), a one-rank group, TTD_COLLECTIVE=
+    torch, or a failed self-check on ANY rank (every rank then agrees to use the torch process
+    group; the reason is kept in `failure_reason`). Collective: all ranks of `group` call it.
+    required=True: also on a one-rank group, and raise instead of returning None."""
+    if not dist.is_initialized() or dist.get_backend(group) != "nccl":
+        if required:
+            raise errors.FailedPreconditionError("the native RCCL engine needs an initialised nccl process group")
+        return None
+    if not required and (dist.get_world_size(group) == 1 or os.environ.get("TTD_COLLECTIVE", "native") == "torch"):
+        return None
+    k = _key(group)
+    if k in _COMMS:
+        return _COMMS[k]
+    if k in _FAILED:
+        return None
+    comm, reason = None, ""
+    try:
+        comm = RcclCommunicator.for_group(group)
+        # self-check: sum of (rank + 1) over the group, stream-ordered on the current stream
+        t = torch.full((1024,), float(dist.get_rank(group) + 1), dtype=torch.float32, device=comm.device)
+        comm.all_reduce_(t)
+        w = dist.get_world_size(group)
+        ok = bool(torch.all(t == w * (w + 1) / 2).item())
+        if not ok:
+            reason = "self-check all-reduce returned a wrong sum"
+    except Exception as e:  # noqa: BLE001 - reported, then every rank falls back together
+        ok, reason = False, "%s: %s" % (type(e).__name__, e)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if int(flag.item()) == 1:
+        _COMMS[k] = comm
+        return comm
+    if comm is not None:
+        comm.destroy(abort=True)
+    _FAILED[k] = reason or "self-check failed on another rank"
+    if required:
+        raise errors.UnavailableError("native RCCL engine unavailable: %s" % _FAILED[k])
+    import warnings
+    warnings.warn("native RCCL engine unavailable (%s); gradients all-reduce through the torch process group"
+                  % _FAILED[k])
+    return None
+
+
+def failure_reason(group=None) -> Optional[str]:
+    return _FAILED.get(_key(group))
+
+
+def abort_all():
+    """Abort every native communicator (process-group recovery: the peers may be gone)."""
+    for c in list(_COMMS.values()):
+        c.destroy(abort=True)
+    _COMMS.clear()
+    _FAILED.clear()

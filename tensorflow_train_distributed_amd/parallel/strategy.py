@@ -315,6 +315,8 @@ def reinit_process_group():
     ranks — the collective-side half of MonitoredTrainingSession's recovery."""
     if _PG["args"] is None:
         return False
+    from . import rccl
+    rccl.abort_all()  # the native communicators of the failed generation (peers may be gone)
     try:
         if dist.is_initialized():
             dist.destroy_process_group()
