@@ -313,6 +313,14 @@ def main():
         dist.all_gather(parts, t)
         per_rank = [float(p.item()) for p in parts]
     elapsed = max(per_rank)
+    red = getattr(step, "reducer", None)
+    comm_stats = None
+    if graph is None and red is not None and world > 1 and red.time_next_step():
+        # one extra (untimed) step with the collectives instrumented: busy time on the
+        # communicator stream and the part of it the backward did not hide
+        run()
+        sync()
+        comm_stats = red.comm_stats()
     sums = step() if graph is None else out
     loss = float(sums[0])
     # replicas must hold identical weights after synchronous data-parallel steps
@@ -377,6 +385,8 @@ def main():
                 dinfo["native_engine_unavailable"] = rccl.failure_reason() or os.environ.get("TTD_COLLECTIVE")
         if probe is not None:
             dinfo["allreduce_probe"] = probe
+        if comm_stats is not None:
+            dinfo["comm_per_step"] = comm_stats
         if backend == "nccl" and world > 1:
             try:
                 dinfo["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())

@@ -34,6 +34,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "common.h"
 
@@ -118,6 +119,11 @@ struct Engine {
   size_t stage_bytes = 0;
   bool failed = false;
   std::string err;
+  // per-bucket timing (ttdc_set_timing): events around each bucket's reduction on the
+  // communicator stream, recorded after its fork wait is satisfied
+  bool timing = false;
+  std::vector<hipEvent_t> t_begin, t_end;
+  int n_timed = 0;
 };
 
 bool set_err(Engine* e, const std::string& m) {
@@ -260,15 +266,10 @@ TTDK_EXPORT void* ttdc_create(const char* id_bytes, int nranks, int rank, int de
 
 TTDK_EXPORT void* ttdc_stream(void* h) { return static_cast<Engine*>(h)->cs; }
 
-// Bucket launch: the communicator stream waits for the work already queued on `producer`,
-// then reduces buf[0:count) in place. compress (fp32 buffers only): cast to bf16 on the
-// communicator stream, reduce in bf16, cast back.
-TTDK_EXPORT int ttdc_bucket(void* h, void* buf, long long count, int dtype, int op, int algo, int compress,
-                            hipStream_t producer) {
-  Engine* e = static_cast<Engine*>(h);
-  if (e->failed) return -1;
-  if (count < 0 || algo < 0 || algo > 2) return set_err(e, "ttdc_bucket: bad argument"), -1;
-  if (!fork_from(e, producer)) return -1;
+namespace ttdk {
+namespace {
+// The reduction part of a bucket launch (after the fork).
+int bucket_body(Engine* e, void* buf, long long count, int dtype, int op, int algo, int compress) {
   if (compress && dtype == 0) {
     const size_t need = static_cast<size_t>(count) * 2;
     if (need > e->stage_bytes) {
@@ -288,6 +289,53 @@ TTDK_EXPORT int ttdc_bucket(void* h, void* buf, long long count, int dtype, int 
   }
   return reduce_on(e, buf, count, to_nccl(dtype), dt_size(dtype), to_op(op), algo, e->cs) ? 0 : -1;
 }
+}  // namespace
+}  // namespace ttdk
+
+// Bucket launch: the communicator stream waits for the work already queued on `producer`,
+// then reduces buf[0:count) in place. compress (fp32 buffers only): cast to bf16 on the
+// communicator stream, reduce in bf16, cast back.
+TTDK_EXPORT int ttdc_bucket(void* h, void* buf, long long count, int dtype, int op, int algo, int compress,
+                            hipStream_t producer) {
+  Engine* e = static_cast<Engine*>(h);
+  if (e->failed) return -1;
+  if (count < 0 || algo < 0 || algo > 2) return set_err(e, "ttdc_bucket: bad argument"), -1;
+  if (!fork_from(e, producer)) return -1;
+  if (e->timing) {
+    if (e->n_timed == static_cast<int>(e->t_begin.size())) {
+      hipEvent_t a, b;
+      if (!hip_ok(e, hipEventCreate(&a), "hipEventCreate") || !hip_ok(e, hipEventCreate(&b), "hipEventCreate")) return -1;
+      e->t_begin.push_back(a);
+      e->t_end.push_back(b);
+    }
+    hipEventRecord(e->t_begin[e->n_timed], e->cs);
+  }
+  const int rc = bucket_body(e, buf, count, dtype, op, algo, compress);
+  if (e->timing && rc == 0) hipEventRecord(e->t_end[e->n_timed++], e->cs);
+  return rc;
+}
+
+// Timing mode on (resets the bucket count) or off.
+TTDK_EXPORT void ttdc_set_timing(void* h, int on) {
+  Engine* e = static_cast<Engine*>(h);
+  e->timing = on != 0;
+  e->n_timed = 0;
+}
+
+// After ttdc_synchronize: *busy_ms = sum over the timed buckets of their reduction time,
+// *span_ms = first bucket start -> last bucket end; returns the number of timed buckets.
+TTDK_EXPORT int ttdc_timing(void* h, float* busy_ms, float* span_ms) {
+  Engine* e = static_cast<Engine*>(h);
+  *busy_ms = *span_ms = 0.f;
+  for (int i = 0; i < e->n_timed; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e->t_begin[i], e->t_end[i]) != hipSuccess) return -1;
+    *busy_ms += ms;
+  }
+  if (e->n_timed > 0 && hipEventElapsedTime(span_ms, e->t_begin[0], e->t_end[e->n_timed - 1]) != hipSuccess) return -1;
+  return e->n_timed;
+}
+
 
 // `consumer` waits for every collective queued so far (no host synchronisation). Also reports
 // an asynchronous communicator failure (a peer died / aborted) as an error.
@@ -376,6 +424,8 @@ TTDK_EXPORT void ttdc_destroy(void* h, int abort) {
   if (!abort) hipStreamSynchronize(e->cs);
   for (int i = 0; i < 64; ++i) hipEventDestroy(e->fork[i]);
   hipEventDestroy(e->join);
+  for (hipEvent_t ev : e->t_begin) hipEventDestroy(ev);
+  for (hipEvent_t ev : e->t_end) hipEventDestroy(ev);
   if (e->stage) hipFree(e->stage);
   hipStreamDestroy(e->cs);
   delete e;

@@ -96,11 +96,36 @@ class BucketedAllReducer:
         self._next = 0
         self._works = []
         self._keep = []
+        self._timed = None
         self.launch_log: List[int] = []
 
     def bytes_per_step(self) -> int:
         """Bytes each rank hands to the collectives per step (all buckets)."""
         return sum(e - s for s, e in self.buckets) * (2 if self.compress else 4)
+
+    def time_next_step(self):
+        """Instrument the next step's collectives (native engine only): `comm_stats()` then
+        reports their busy time and how much of it the backward did not hide."""
+        if self.comm is None:
+            return False
+        self.comm.set_timing(True)
+        self._timed = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        return True
+
+    def comm_stats(self):
+        """After a step run with time_next_step(): {buckets, busy_ms, span_ms, exposed_ms,
+        overlap_pct}. exposed_ms = time the consumer stream waited for the collectives after the
+        backward's last kernel was queued; overlap_pct = share of the busy time hidden."""
+        if self.comm is None or self._timed is None:
+            return None
+        st = self.comm.timing()
+        self.comm.set_timing(False)
+        self._timed[1].synchronize()
+        exposed = float(self._timed[0].elapsed_time(self._timed[1]))
+        self._timed = None
+        st["exposed_ms"] = round(exposed, 4)
+        st["overlap_pct"] = round(100.0 * max(0.0, 1.0 - exposed / st["busy_ms"]), 1) if st["busy_ms"] > 0 else None
+        return st
 
     def begin(self):
         self._next = 0
@@ -170,7 +195,11 @@ class BucketedAllReducer:
             self._launch(self._next)
             self._next += 1
         if self.comm is not None:
+            if self._timed is not None:
+                self._timed[0].record()  # the backward's last queued work
             self.comm.join()  # the current stream waits for the buckets (no host sync)
+            if self._timed is not None:
+                self._timed[1].record()
             return
         works, self._works = self._works, []
         for w, c, t in works:

@@ -62,6 +62,10 @@ def _lib():
         lib.ttdc_synchronize.argtypes = [c_void_p]
         lib.ttdc_probe.restype = c_int
         lib.ttdc_probe.argtypes = [c_void_p, c_void_p, c_longlong, c_int, ctypes.POINTER(c_float)]
+        lib.ttdc_set_timing.restype = None
+        lib.ttdc_set_timing.argtypes = [c_void_p, c_int]
+        lib.ttdc_timing.restype = c_int
+        lib.ttdc_timing.argtypes = [c_void_p, ctypes.POINTER(c_float), ctypes.POINTER(c_float)]
         lib.ttdc_destroy.restype = None
         lib.ttdc_destroy.argtypes = [c_void_p, c_int]
         _bound = True
@@ -162,6 +166,20 @@ class RcclCommunicator:
     def synchronize(self):
         """Host wait for the communicator stream with a deadline (a dead peer raises)."""
         self._check(_lib().ttdc_synchronize(self._h), "collective synchronize")
+
+    def set_timing(self, on: bool):
+        """Time each following bucket's reduction on the communicator stream (events recorded
+        after its fork wait is satisfied); `timing()` reads them after a synchronize."""
+        _lib().ttdc_set_timing(self._h, 1 if on else 0)
+
+    def timing(self) -> Dict[str, float]:
+        """{buckets, busy_ms (sum of bucket reduction times), span_ms (first start -> last end)}."""
+        self.synchronize()
+        busy, span = c_float(0.0), c_float(0.0)
+        n = _lib().ttdc_timing(self._h, ctypes.byref(busy), ctypes.byref(span))
+        if n < 0:
+            raise errors.InternalError("hipEventElapsedTime failed")
+        return {"buckets": int(n), "busy_ms": round(float(busy.value), 4), "span_ms": round(float(span.value), 4)}
 
     def probe(self, nbytes: int, iters: int = 5) -> Dict[str, float]:
         """RCCL bus bandwidth of an fp32 all-reduce of `nbytes` on the communicator stream."""

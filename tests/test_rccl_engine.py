@@ -130,6 +130,15 @@ def test_bucketed_allreducer_drives_the_engine():
         torch.cuda.synchronize()
         assert red.launch_log == list(range(len(red.buckets)))
         torch.testing.assert_close(after, local.bfloat16().float(), rtol=0, atol=0)
+        # instrumented step: per-bucket busy time on the communicator stream + exposed time
+        assert red.time_next_step()
+        red.begin()
+        for s in specs:
+            red.mark_ready(s.name)
+        red.finish()
+        st = red.comm_stats()
+        assert st["buckets"] == len(red.buckets) and st["busy_ms"] > 0 and st["span_ms"] >= 0
+        assert st["exposed_ms"] >= 0 and 0 <= st["overlap_pct"] <= 100
     finally:
         from tensorflow_train_distributed_amd.parallel import rccl
         rccl.abort_all()
