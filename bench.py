@@ -220,7 +220,20 @@ def main():
     ap.add_argument("--compress-bf16", action="store_true", help="all-reduce gradients in bf16")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"], help="ResNet conv forward precision")
     ap.add_argument("--optimizer", default="momentum", choices=["momentum", "lamb"], help="ResNet optimizer")
+    ap.add_argument("--run-config", default=None,
+                    help="JSON/YAML RunConfig file (utils/run_config.py); its fields override the flags above")
     args = ap.parse_args()
+    if args.run_config:
+        from tensorflow_train_distributed_amd.utils.run_config import RunConfig
+        rc = RunConfig.from_file(args.run_config).with_env()
+        args.model, args.steps, args.warmup = rc.model, rc.train_steps, rc.warmup_steps
+        args.batch, args.image_size, args.seq_len = rc.per_replica_batch, rc.image_size, rc.seq_len
+        args.precision, args.bucket_mb, args.compress_bf16 = rc.precision, rc.bucket_mb, rc.compress_bf16
+        args.graph = 1 if rc.hipgraph else 0
+        if rc.optimizer in ("momentum", "lamb"):
+            args.optimizer = rc.optimizer
+        if rc.collective_engine != "auto":
+            os.environ["TTD_COLLECTIVE"] = "native" if rc.collective_engine == "native" else "torch"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))

@@ -16,6 +16,7 @@ __version__ = "0.1.0"
 from . import data, distribute, initializers, layers, models, nn, parallel, regularizers, summary, train  # noqa: E402
 from .parallel.ps import device  # noqa: E402
 from .utils import app, errors, flags, tracing  # noqa: E402
+from .utils.run_config import RunConfig  # noqa: E402
 from .utils import tracing as debugging  # noqa: E402  (tf.debugging.check_numerics)
 from .utils import tracing as profiler  # noqa: E402  (roctx ranges)
 from .train.graph import placeholder  # noqa: E402

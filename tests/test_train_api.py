@@ -144,3 +144,31 @@ def test_object_checkpoint_of_model_and_optimizer(tmp_path):
     keys = dict(ttd.train.list_variables(path))
     assert "model/output/kernel/.ATTRIBUTES/VARIABLE_VALUE" in keys
     assert "model/output/kernel/.OPTIMIZER_SLOT/optimizer/v/.ATTRIBUTES/VARIABLE_VALUE" in keys
+
+
+def test_run_config_layers_file_env_and_flags(tmp_path):
+    """Typed RunConfig: defaults <- file <- TTD_RUN_* env <- flags; the
+    reference's constants (distribute_training.py:10-36) as a preset; invalid values raise."""
+    import argparse
+    import json
+    from tensorflow_train_distributed_amd.utils.run_config import RunConfig
+    ref = RunConfig.reference_mnist()
+    assert (ref.per_replica_batch, ref.learning_rate, ref.decay_steps, ref.decay_rate, ref.train_steps,
+            ref.save_checkpoints_secs, ref.save_summary_steps) == (128, 0.01, 500, 0.96, 10000, 60.0, 100)
+    f = tmp_path / "rc.json"
+    f.write_text(json.dumps({"model": "bert", "bucket_mb": 64, "hipgraph": "true", "my_note": "x"}))
+    ap = RunConfig.add_arguments(argparse.ArgumentParser())
+    args = ap.parse_args(["--run-config", str(f), "--train-steps", "7", "--compress-bf16"])
+    import os
+    os.environ["TTD_RUN_WARMUP_STEPS"] = "2"
+    try:
+        rc = RunConfig.from_args(args)
+    finally:
+        del os.environ["TTD_RUN_WARMUP_STEPS"]
+    assert (rc.model, rc.bucket_mb, rc.hipgraph, rc.train_steps, rc.warmup_steps, rc.compress_bf16) == \
+        ("bert", 64.0, True, 7, 2, True)
+    assert rc.extra == {"my_note": "x"} and rc.to_dict()["extra"] == {"my_note": "x"}
+    with pytest.raises(ValueError):
+        rc.replace(optimizer="adagrad")
+    with pytest.raises(ValueError):
+        RunConfig(bucket_mb=0)
