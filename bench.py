@@ -423,6 +423,9 @@ def main():
             "dist": dinfo,
         }), flush=True)
     if world > 1:
+        if not on_cpu:
+            from tensorflow_train_distributed_amd.parallel import rccl
+            rccl.shutdown()
         dist.destroy_process_group()
 
 

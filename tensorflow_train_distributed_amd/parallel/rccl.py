@@ -196,9 +196,12 @@ class RcclCommunicator:
             self._h = None
 
     def __del__(self):
+        import sys
+        if sys.is_finalizing():  # the HIP runtime may already be gone: leave it to process exit
+            return
         try:
             self.destroy(abort=True)
-        except Exception:  # noqa: BLE001 - interpreter shutdown
+        except Exception:  # noqa: BLE001
             pass
 
 
@@ -267,3 +270,25 @@ def abort_all():
         c.destroy(abort=True)
     _COMMS.clear()
     _FAILED.clear()
+
+
+def shutdown():
+    """Orderly end of a run: finalize + destroy every native communicator (all ranks call it,
+    before torch.distributed.destroy_process_group)."""
+    for c in list(_COMMS.values()):
+        c.destroy(abort=False)
+    _COMMS.clear()
+    _FAILED.clear()
+
+
+def _at_exit():
+    # a run that ended without shutdown() (an exception): abort while the HIP runtime is alive
+    try:
+        abort_all()
+    except Exception:  # noqa: BLE001
+        pass
+
+
+import atexit  # noqa: E402
+
+atexit.register(_at_exit)
