@@ -522,6 +522,7 @@ struct EpiParams {
   // the other rows of `out` hold no data yet (the stride-2 1x1 projection dgrad wrote only the
   // pixels it samples), so the accumulated tensor needs no zero fill. 0 = every row.
   int bH, bW;
+  int feed_pf;  // 256-row kernel: prefetched feeding-BN epilogue allowed (TTD_FEED_PREFETCH, default 1)
 };
 
 __device__ __forceinline__ bool beta_row(const EpiParams& E, int m) {
@@ -1263,6 +1264,95 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
+// ---- prefetched "feeding BN" epilogue of the 256-row kernel (dgrad with beta accumulate and
+// the next BN's backward statistics: by = that BN's conv output, bmask = its ReLU bits, no
+// bias / residual / activation / remap / second BN: with the by2 variant instantiated too the
+// 256-row kernels spilled). A short-K data gradient spends most of a
+// tile in this epilogue, moving 3x the output tile through HBM; with one workgroup per CU the
+// generic row loop paid a full load latency per 8-row batch, twice per tile, exposed (ResNet
+// c1 dgrads ran at 2.3-3.3 TB/s: tools/dgrad_epi_ab.py). Here a thread's rows go in batches of
+// FQ: the first batch is loaded before the accumulators are staged through LDS and every next
+// batch before the current one is consumed, so the load latency hides under the staging and
+// the stores (two small batches live at a time: no spills next to the live accumulators).
+// Same arithmetic and rounding as epi_rows (out = bf16(bf16(acc) + old) * mask, sums of the
+// stored values).
+constexpr int FQ = 4;
+
+template <bool BY2>
+struct FeedRows {
+  uint4 old[FQ], y[FQ], y2[BY2 ? FQ : 1];
+  uint32_t mb[FQ];
+};
+
+template <int RPP, bool BY2>
+__device__ __forceinline__ void feed_load(FeedRows<BY2>& f, const EpiParams& E, int rb, int m0, int M, int n, int N) {
+  const bf16_t* out = static_cast<const bf16_t*>(E.out);
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) {
+    const int m = m0 + rb + u * RPP;
+    if (m < M && n < N) {
+      const long long o = static_cast<long long>(m) * E.ldo + n;
+      f.old[u] = (E.beta && beta_row(E, m)) ? *reinterpret_cast<const uint4*>(out + o) : make_uint4(0, 0, 0, 0);
+      f.y[u] = *reinterpret_cast<const uint4*>(E.by + o);
+      if constexpr (BY2) f.y2[u] = *reinterpret_cast<const uint4*>(E.by2 + o);
+      f.mb[u] = E.bmask ? E.bmask[o >> 3] : 0xffu;
+    }
+  }
+}
+
+template <int RPP, int PITCH, bool BY2>
+__device__ __forceinline__ void feed_rows(const FeedRows<BY2>& f, const EpiParams& E, const char* smem, int c, int rb,
+                                          int m0, int M, int n, int N, float (&s8)[8], float (&q8)[8],
+                                          float (&r8)[8]) {
+  if (n >= N) return;
+  bf16_t* out = static_cast<bf16_t*>(E.out);
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) {
+    const int r = rb + u * RPP, m = m0 + r;
+    if (m >= M) break;
+    float v[8], ov[8], yv[8];
+    unpack8(*reinterpret_cast<const uint4*>(smem + r * PITCH + c * 16), v);
+    unpack8(f.old[u], ov);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (f.mb[u] >> j) & 1u ? v[j] + ov[j] : 0.f;
+    const uint4 packed = pack8(v);
+    *reinterpret_cast<uint4*>(out + static_cast<long long>(m) * E.ldo + n) = packed;
+    unpack8(packed, v);  // statistics of the gradient actually stored
+    unpack8(f.y[u], yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s8[j] += v[j];
+      q8[j] += v[j] * yv[j];
+    }
+    if constexpr (BY2) {
+      unpack8(f.y2[u], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r8[j] += v[j] * yv[j];
+    }
+  }
+}
+
+// The whole pipelined feeding epilogue: NR rows per thread in NR / FQ batches.
+template <int NR, int RPP, int PITCH, bool BY2, class Stage>
+__device__ __forceinline__ void feed_epilogue(const EpiParams& E, char* smem, Stage&& stage, int c, int r0, int m0,
+                                              int M, int n, int N, float (&s8)[8], float (&q8)[8], float (&r8)[8]) {
+  static_assert(NR % FQ == 0, "rows per thread in whole batches");
+  constexpr int NBT = NR / FQ;
+  FeedRows<BY2> A, B;
+  stage(std::integral_constant<int, 0>{});
+  stage(std::integral_constant<int, 1>{});
+  feed_load<RPP>(A, E, r0, m0, M, n, N);  // the accumulators are dead: loads overlap the LDS barrier
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  barrier();
+#pragma unroll
+  for (int bt = 0; bt < NBT; bt += 2) {
+    if (bt + 1 < NBT) feed_load<RPP>(B, E, r0 + (bt + 1) * FQ * RPP, m0, M, n, N);
+    feed_rows<RPP, PITCH>(A, E, smem, c, r0 + bt * FQ * RPP, m0, M, n, N, s8, q8, r8);
+    if (bt + 2 < NBT) feed_load<RPP>(A, E, r0 + (bt + 2) * FQ * RPP, m0, M, n, N);
+    if (bt + 1 < NBT) feed_rows<RPP, PITCH>(B, E, smem, c, r0 + (bt + 1) * FQ * RPP, m0, M, n, N, s8, q8, r8);
+  }
+}
+
 template <int BN>
 struct Geo {
   static constexpr int BNH = BN / 2;          // B half rows
@@ -1515,37 +1605,47 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     return;
   }
   constexpr int PITCH = Gm::PITCH;
-#pragma unroll
-  for (int ha = 0; ha < 2; ++ha)
-#pragma unroll
-    for (int hb = 0; hb < 2; ++hb)
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-          const int r = ha * 128 + wm * 64 + a * 16 + i16, c = hb * BNH + wn * WC + b * 16 + 4 * g;
-          const f32x4_t v = acc[ha][hb][a][b] * alpha_e;
-          *reinterpret_cast<uint2*>(smem + r * PITCH + c * 2) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        }
-  __syncthreads();
   constexpr int CPR = BN / 8;     // 16-B chunks per row
   constexpr int RPP = T / CPR;    // rows per pass
   const int c = tid % CPR, r0 = tid / CPR;
   const int n = n0 + c * 8;
-  const bool nfull = n + 8 <= N;
-  const bool vst = nfull && (E.ldo & 7) == 0;
-  const bool vres = nfull && (E.ldr & 7) == 0;
-  float bias8[8], s8[8], q8[8], r8[8];
+  auto stage = [&](auto HA) {  // accumulator half HA -> LDS as bf16 (compile-time index)
+    constexpr int ha = decltype(HA)::value;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
-    s8[j] = q8[j] = r8[j] = 0.f;
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const int r = ha * 128 + wm * 64 + a * 16 + i16, cc = hb * BNH + wn * WC + b * 16 + 4 * g;
+            const f32x4_t v = acc[ha][hb][a][b] * alpha_e;
+            *reinterpret_cast<uint2*>(smem + r * PITCH + cc * 2) =
+                make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          }
+  };
+  float s8[8], q8[8], r8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s8[j] = q8[j] = r8[j] = 0.f;
+  // host guarantees for E.by: N % 8 == 0 and ldo % 8 == 0 (whole 16-B chunks)
+  const bool feed = E.feed_pf && E.by && !E.by2 && !E.residual && !E.bias && E.act == kActNone && !E.remap &&
+                    !E.aux && E.stat;
+  if (feed) {
+    feed_epilogue<BM / RPP, RPP, PITCH, false>(E, smem, stage, c, r0, m0, M, n, N, s8, q8, r8);
+  } else {
+    stage(std::integral_constant<int, 0>{});
+    stage(std::integral_constant<int, 1>{});
+    __syncthreads();
+    const bool nfull = n + 8 <= N;
+    const bool vst = nfull && (E.ldo & 7) == 0;
+    const bool vres = nfull && (E.ldr & 7) == 0;
+    float bias8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
+    if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
+      epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
+    else
+      epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
   }
-  if (E.beta || E.residual || E.by)  // batched loads only where there are loads (no cost to plain stores)
-    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
-  else
-    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
   if (E.stat) {
     // threads sharing a chunk column c: tid % CPR equal -> within a wave lanes c, c+CPR, ...
 #pragma unroll
@@ -2142,6 +2242,8 @@ struct TtdkEpilogue {
 
 inline EpiParams to_epi(const TtdkEpilogue* e) {
   EpiParams p;
+  static const int feed_pf = [] { const char* v = getenv("TTD_FEED_PREFETCH"); return v ? atoi(v) : 1; }();
+  p.feed_pf = feed_pf;
   p.mode = e->mode;
   p.out = e->out;
   p.ldo = e->ldo;

@@ -406,6 +406,11 @@ def dgrad_stat_rows(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
     return dgrad_stat_tile(x_shape, wt_shape)[2]
 
 
+# short-K pointwise data gradients with the BN-statistics epilogue up to this K run on the
+# 4-wave kernel instead of the 256-row one (TTD_DGRAD_STAT_4W_K; 0 = never)
+DGRAD_STAT_4W_K = int(_os.environ.get("TTD_DGRAD_STAT_4W_K", "0"))
+
+
 def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
     """(bm, bn, rows) of a unit-stride data-gradient launch with the BN-statistics epilogue
     (mirror of ttdk_conv_dgrad's tile choice when `stat` is set)."""
@@ -417,6 +422,8 @@ def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
     M = N * H * W
     Kg = R * S * K
     bbn = big_bn(M, C, Kg)
+    if pointwise and Kg <= DGRAD_STAT_4W_K:
+        bbn = 0  # 4-wave kernel, two workgroups per CU (A/B: tools/dgrad_epi_ab.py)
     if bbn and (pointwise or K % 64 == 0):
         return 256, bbn, -(-M // 256)
     bm, bn = _pick_tile(M, C)

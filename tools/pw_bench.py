@@ -29,7 +29,9 @@ def main():
     B = args.batch
     # (name, H, K_in, N_out)
     shapes = [("s2 c1 256->64", 56, 256, 64), ("s2 c3 64->256", 56, 64, 256), ("s3 c1 512->128", 28, 512, 128),
-              ("s3 c3 128->512", 28, 128, 512), ("s3b1 c1 256->128", 56, 256, 128)]
+              ("s3 c3 128->512", 28, 128, 512), ("s3b1 c1 256->128", 56, 256, 128),
+              ("s4 c1 1024->256", 14, 1024, 256), ("s4 c3 256->1024", 14, 256, 1024),
+              ("s5 c1 2048->512", 7, 2048, 512)]
     dev = "cuda"
 
     def ev():
