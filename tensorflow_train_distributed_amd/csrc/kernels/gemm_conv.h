@@ -1280,7 +1280,7 @@ constexpr int FQ = 4;
 
 template <bool BY2>
 struct FeedRows {
-  uint4 old[FQ], y[FQ], y2[BY2 ? FQ : 1];
+  uint4 old[FQ], y[FQ], y2[FQ];
   uint32_t mb[FQ];
 };
 
@@ -1294,7 +1294,7 @@ __device__ __forceinline__ void feed_load(FeedRows<BY2>& f, const EpiParams& E, 
       const long long o = static_cast<long long>(m) * E.ldo + n;
       f.old[u] = (E.beta && beta_row(E, m)) ? *reinterpret_cast<const uint4*>(out + o) : make_uint4(0, 0, 0, 0);
       f.y[u] = *reinterpret_cast<const uint4*>(E.by + o);
-      if constexpr (BY2) f.y2[u] = *reinterpret_cast<const uint4*>(E.by2 + o);
+      if (BY2 || E.by2) f.y2[u] = *reinterpret_cast<const uint4*>(E.by2 + o);
       f.mb[u] = E.bmask ? E.bmask[o >> 3] : 0xffu;
     }
   }
@@ -1324,7 +1324,7 @@ __device__ __forceinline__ void feed_rows(const FeedRows<BY2>& f, const EpiParam
       s8[j] += v[j];
       q8[j] += v[j] * yv[j];
     }
-    if constexpr (BY2) {
+    if (BY2 || E.by2) {
       unpack8(f.y2[u], yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) r8[j] += v[j] * yv[j];
@@ -1627,7 +1627,7 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
 #pragma unroll
   for (int j = 0; j < 8; ++j) s8[j] = q8[j] = r8[j] = 0.f;
   // host guarantees for E.by: N % 8 == 0 and ldo % 8 == 0 (whole 16-B chunks)
-  const bool feed = E.feed_pf && E.by && !E.by2 && !E.residual && !E.bias && E.act == kActNone && !E.remap &&
+  const bool feed = E.feed_pf && E.by && !E.residual && !E.bias && E.act == kActNone && !E.remap &&
                     !E.aux && E.stat;
   if (feed) {
     feed_epilogue<BM / RPP, RPP, PITCH, false>(E, smem, stage, c, r0, m0, M, n, N, s8, q8, r8);
