@@ -479,14 +479,21 @@ struct MNConvGather {
 // pre-activation saved by the forward epilogue; not added).
 enum Act : int { kActNone = 0, kActRelu = 1, kActGelu = 2, kActTanh = 3, kActDGelu = 4 };
 
+// tanh(u) = 1 - 2 / (1 + 2^(2u log2 e)): one v_exp_f32 + one v_rcp_f32 instead of the
+// libm tanhf (measured: the GELU epilogues of the BERT GEMMs were VALU-bound on it);
+// saturates to +-1 through exp2 -> inf / 0, absolute error ~1e-7 near 0
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * 2.8853900817779268f));
+}
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  return 0.5f * x * (1.f + fast_tanh(k0 * (x + k1 * x * x * x)));
 }
 
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float t = tanhf(k0 * (x + k1 * x * x * x));
+  const float t = fast_tanh(k0 * (x + k1 * x * x * x));
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
@@ -1702,24 +1709,44 @@ __device__ __forceinline__ void pers_epi(const f32x4_t (&acc)[2][2][4][2], const
   const int g = lane >> 4, i16 = lane & 15;
   const bool odd = g & 1;
   bf16_t* const out = static_cast<bf16_t*>(E.out);
+  // residual (dGELU) / old-output (beta) loads are software-pipelined one row block ahead: the
+  // loads of block it + 1 are in flight while block it is computed and stored (a load-use per
+  // block left every block's latency exposed)
+  constexpr bool LD = (EK & (kEkDGelu | kEkBeta)) != 0;
+  uint2 rvb[2][2][2], ovb[2][2][2];  // [slot][hb][b]
+  auto load_blk = [&](int it, uint2 (&rv)[2][2], uint2 (&ov)[2][2]) {
+    const int ha = it >> 2, a = it & 3;
+    const int m = m0 + ha * 128 + wm * 64 + a * 16 + i16;
+    if (CHECK && m >= M) return;
 #pragma unroll
-  for (int ha = 0; ha < 2; ++ha)
+    for (int hb = 0; hb < 2; ++hb) {
+      const int nb = n0 + hb * BNH + wn * WC + 4 * g;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
+      for (int b = 0; b < 2; ++b) {
+        if constexpr ((EK & kEkDGelu) != 0)
+          if (!CHECK || nb + 16 * b < N)
+            rv[hb][b] = *reinterpret_cast<const uint2*>(E.residual + static_cast<long long>(m) * E.ldr + nb + 16 * b);
+        if constexpr ((EK & kEkBeta) != 0)
+          if (!CHECK || nb + 16 * b < N)
+            ov[hb][b] = *reinterpret_cast<const uint2*>(out + static_cast<long long>(m) * E.ldo + nb + 16 * b);
+      }
+    }
+  };
+  if constexpr (LD) load_blk(0, rvb[0], ovb[0]);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int ha = it >> 2, a = it & 3;
+    if constexpr (LD)
+      if (it + 1 < 8) load_blk(it + 1, rvb[(it + 1) & 1], ovb[(it + 1) & 1]);
+    {
       const int m = m0 + ha * 128 + wm * 64 + a * 16 + i16;
       if (CHECK && m >= M) continue;
       const long long row = static_cast<long long>(m) * E.ldo;
 #pragma unroll
       for (int hb = 0; hb < 2; ++hb) {
         const int nb = n0 + hb * BNH + wn * WC + 4 * g;  // block b: nb + 16 b
-        uint2 rv[2], ov[2];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          if constexpr ((EK & kEkDGelu) != 0)
-            if (!CHECK || nb + 16 * b < N) rv[b] = *reinterpret_cast<const uint2*>(E.residual + static_cast<long long>(m) * E.ldr + nb + 16 * b);
-          if constexpr ((EK & kEkBeta) != 0)
-            if (!CHECK || nb + 16 * b < N) ov[b] = *reinterpret_cast<const uint2*>(out + row + nb + 16 * b);
-        }
+        const uint2(&rv)[2] = rvb[it & 1][hb];
+        const uint2(&ov)[2] = ovb[it & 1][hb];
         uint2 po[2], pa[2];
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
@@ -1760,6 +1787,7 @@ __device__ __forceinline__ void pers_epi(const f32x4_t (&acc)[2][2][4][2], const
         }
       }
     }
+  }
 }
 
 // Persistent 256 x BN GEMM for elementwise epilogues (bias, residual / dGELU, beta, aux copy,
