@@ -99,6 +99,36 @@ def test_sync_replicas_accumulator_semantics(cluster2):
     cl2.close()
 
 
+def test_sync_replicas_backup_worker_semantics(cluster2):
+    """SyncReplicasOptimizer(replicas_to_aggregate=2, total_num_replicas=3) (SURVEY.md §4.2
+    fault injection): the chief applies as soon as 2 fresh gradients are in — the slow (or dead)
+    third worker does not block the step — every worker still gets a token, and the straggler's
+    gradient for the old step is dropped as stale."""
+    cluster, _ = cluster2
+    vals = {"w": np.zeros(4, np.float32), "v": np.zeros(2, np.float32)}
+    workers = [PS.PSClient(cluster, {"w": 0, "v": 1}) for _ in range(3)]
+    chief = workers[0]
+    chief.init_vars(vals)
+    chief.set_accum_step(0)
+    assert workers[0].accum_apply(0, {"w": np.full(4, 2.0, np.float32), "v": np.full(2, 2.0, np.float32)}) == 2
+    assert workers[1].accum_apply(0, {"w": np.full(4, 4.0, np.float32), "v": np.full(2, 4.0, np.float32)}) == 2
+    res = {}
+    th = threading.Thread(target=lambda: res.setdefault("gs", chief.take_apply(2, 0.5, tokens_per_step=3)))
+    th.start()
+    th.join(10)
+    assert not th.is_alive() and res["gs"] == 1  # did not wait for the third replica
+    out = {k: np.zeros_like(v) for k, v in vals.items()}
+    chief.pull(out)
+    np.testing.assert_allclose(out["w"], -0.5 * 3.0)  # mean of the two fresh gradients
+    # the straggler computed against step 0: stale now, dropped
+    assert workers[2].accum_apply(0, {"w": np.full(4, 100.0, np.float32), "v": np.ones(2, np.float32)}) == 0
+    assert all(w.dequeue_token() == 1 for w in workers)  # one token per replica (total_num_replicas)
+    chief.pull(out)
+    np.testing.assert_allclose(out["w"], -0.5 * 3.0)
+    for w in workers:
+        w.close()
+
+
 def test_sharded_save_merge_restore(cluster2, tmp_path):
     cluster, _ = cluster2
     vals = {"x": np.arange(5, dtype=np.float32), "y": np.full(3, 7.0, np.float32)}
