@@ -33,9 +33,12 @@ def run(batch):
 
 def report(trace_csv, log_json):
     import csv
-    log = json.load(open(log_json))
+    # streaming pointwise (pw_*), halo 3x3 (c3_*) and stem launches are logged too but dispatch
+    # their own kernels, not gemm_kernel / gemm256_kernel: leave them out of the pairing
+    log = [e for e in json.load(open(log_json)) if not e[0].startswith(("pw_", "c3_", "stem_"))]
     rows = [r for r in csv.DictReader(open(trace_csv))
             if "gemm_kernel" in r["Kernel_Name"] or "gemm256_kernel" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # the last len(log) gemm dispatches belong to the logged step
     rows = rows[-len(log):]
     agg = {}
