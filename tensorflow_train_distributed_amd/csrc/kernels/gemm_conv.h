@@ -1283,7 +1283,7 @@ __device__ __forceinline__ void barrier() {
 // the stores (two small batches live at a time: no spills next to the live accumulators).
 // Same arithmetic and rounding as epi_rows (out = bf16(bf16(acc) + old) * mask, sums of the
 // stored values).
-constexpr int FQ = 4;
+constexpr int FQ = 4;  // (8-row batches measured 5-10 % slower on these kernels, ResNet +0.3-0.8 ms)
 
 template <bool BY2>
 struct FeedRows {
