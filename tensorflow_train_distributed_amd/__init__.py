@@ -20,5 +20,5 @@ from .utils.run_config import RunConfig  # noqa: E402
 from .utils import tracing as debugging  # noqa: E402  (tf.debugging.check_numerics)
 from .utils import tracing as profiler  # noqa: E402  (roctx ranges)
 from .train.graph import placeholder  # noqa: E402
-from .train.tape import GradientTape  # noqa: E402
+from .train.tape import GradientTape, clip_by_global_norm  # noqa: E402
 from .nn import reduce_mean, matmul, sigmoid, tanh  # noqa: E402  (tf.reduce_mean / tf.matmul / tf.sigmoid / tf.tanh)

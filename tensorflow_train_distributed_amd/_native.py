@@ -31,6 +31,8 @@ _LIBDIR = os.path.join(_PKG, "lib")
 _OBJDIR = os.path.join(_LIBDIR, "obj")
 
 RT_LIB = os.path.join(_LIBDIR, "libttd_rt.so")
+# kernel-side headers the host runtime also compiles (the collective engine's call plan)
+_RT_SHARED = [os.path.join(_CSRC, "kernels", "collective_plan.h")]
 HIP_LIB = os.path.join(_LIBDIR, "libttd_hip.so")
 
 HIP_ARCH = os.environ.get("TTD_HIP_ARCH", "gfx950")
@@ -82,7 +84,7 @@ def _build_objects(srcs, headers, compile_cmd, ext):
 def build_rt(force: bool = False) -> str:
     """Compile libttd_rt.so with g++ (host only)."""
     srcs = sorted(glob.glob(os.path.join(_CSRC, "runtime", "*.cc")))
-    hdrs = glob.glob(os.path.join(_CSRC, "runtime", "*.h"))
+    hdrs = glob.glob(os.path.join(_CSRC, "runtime", "*.h")) + _RT_SHARED
     cxx = os.environ.get("CXX", "g++")
     flags = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-fvisibility=hidden"]
     san = os.environ.get("TTD_RT_SANITIZE")  # e.g. "thread" or "address" (host-only builds)
@@ -123,11 +125,15 @@ def build_hip(force: bool = False) -> str:
 def _src_hash(kind):
     pats = {"rt": ("runtime", "*.cc", "*.h"), "hip": ("kernels", "*.hip", "*.h")}[kind]
     h = hashlib.sha1()
+    files = []
     for pat in pats[1:]:
-        for f in sorted(glob.glob(os.path.join(_CSRC, pats[0], pat))):
-            h.update(os.path.basename(f).encode())
-            with open(f, "rb") as fh:
-                h.update(fh.read())
+        files += sorted(glob.glob(os.path.join(_CSRC, pats[0], pat)))
+    if kind == "rt":
+        files += _RT_SHARED
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
     h.update(HIP_ARCH.encode())
     return h.hexdigest()
 

@@ -29,13 +29,18 @@
 //   2 reduce_to_one  reduce to rank 0 + broadcast (ReductionToOneDevice)
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "collective_plan.h"
 #include "common.h"
 
 namespace ttdk {
@@ -117,15 +122,31 @@ struct Engine {
   hipEvent_t join = nullptr;
   void* stage = nullptr;    // bf16 staging for compressed buckets
   size_t stage_bytes = 0;
-  bool failed = false;
+  std::atomic<bool> failed{false};
   std::string err;
   // per-bucket timing (ttdc_set_timing): events around each bucket's reduction on the
   // communicator stream, recorded after its fork wait is satisfied
   bool timing = false;
   std::vector<hipEvent_t> t_begin, t_end;
   int n_timed = 0;
+  // ---- watchdog: every join (outside stream capture) records a marker event on the
+  // communicator stream; a thread polls the oldest marker and the communicator's asynchronous
+  // error. A marker older than `timeout` (a peer that died mid-step leaves RCCL's kernels
+  // spinning and the compute stream waiting on the join) or an asynchronous error aborts the
+  // communicator: RCCL's kernels exit, the streams drain, and the next bucket / join call
+  // returns an error the recoverable session acts on (parallel/strategy.py recover()).
+  std::mutex mu;            // guards comm calls vs. the watchdog's abort, `pend`, `pool`
+  std::condition_variable cv;
+  bool stop = false;
+  std::thread wd;
+  struct Mark {
+    hipEvent_t ev;
+    std::chrono::steady_clock::time_point t;
+  };
+  std::deque<Mark> pend;
+  std::vector<hipEvent_t> pool;
+  std::atomic<int> aborts{0};
 };
-
 bool set_err(Engine* e, const std::string& m) {
   if (e) {
     e->err = m;
@@ -174,29 +195,72 @@ bool fork_from(Engine* e, hipStream_t producer) {
 
 bool reduce_on(Engine* e, void* buf, size_t count, ncclDataType_t dt, size_t esz, ncclRedOp_t op, int algo,
                hipStream_t s) {
-  if (count == 0) return true;
-  if (e->nranks == 1) {
-    // a one-rank group still goes through RCCL (the same code path as N ranks: it validates the
-    // buffers and lets a one-GPU run exercise the engine); SUM / AVG of one replica = identity
-    return settle(e, ncclAllReduce(buf, buf, count, dt, op, e->comm, s), "ncclAllReduce");
-  }
+  ttd_coll::Step plan[ttd_coll::kMaxSteps];
+  const int n = ttd_coll::plan(algo, static_cast<long long>(count), e->nranks, e->rank, plan);
+  if (n < 0) return set_err(e, "collective plan: bad argument");
   char* p = static_cast<char*>(buf);
-  if (algo == 1) {
-    const size_t per = count / e->nranks, main = per * e->nranks;
-    if (per > 0) {
-      char* mine = p + e->rank * per * esz;
-      if (!settle(e, ncclReduceScatter(p, mine, per, dt, op, e->comm, s), "ncclReduceScatter")) return false;
-      if (!settle(e, ncclAllGather(mine, p, per, dt, e->comm, s), "ncclAllGather")) return false;
+  for (int i = 0; i < n; ++i) {
+    const ttd_coll::Step& st = plan[i];
+    char* a = p + st.send * esz;
+    char* b = p + st.recv * esz;
+    const size_t c = static_cast<size_t>(st.count);
+    bool ok = true;
+    switch (st.kind) {
+      case ttd_coll::kAllReduce: ok = settle(e, ncclAllReduce(a, a, c, dt, op, e->comm, s), "ncclAllReduce"); break;
+      case ttd_coll::kReduceScatter:
+        ok = settle(e, ncclReduceScatter(a, b, c, dt, op, e->comm, s), "ncclReduceScatter");
+        break;
+      case ttd_coll::kAllGather: ok = settle(e, ncclAllGather(a, b, c, dt, e->comm, s), "ncclAllGather"); break;
+      case ttd_coll::kReduce: ok = settle(e, ncclReduce(a, a, c, dt, op, st.root, e->comm, s), "ncclReduce"); break;
+      case ttd_coll::kBroadcast: ok = settle(e, ncclBroadcast(a, a, c, dt, st.root, e->comm, s), "ncclBroadcast"); break;
+      default: ok = set_err(e, "collective plan: unknown step");
     }
-    if (main < count)
-      return settle(e, ncclAllReduce(p + main * esz, p + main * esz, count - main, dt, op, e->comm, s), "ncclAllReduce");
-    return true;
+    if (!ok) return false;
   }
-  if (algo == 2) {
-    if (!settle(e, ncclReduce(p, p, count, dt, op, 0, e->comm, s), "ncclReduce")) return false;
-    return settle(e, ncclBroadcast(p, p, count, dt, 0, e->comm, s), "ncclBroadcast");
+  return true;
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// Abort the communicator (caller holds e->mu): RCCL's kernels see the abort flag and exit.
+void abort_locked(Engine* e, const std::string& why) {
+  if (!e->comm) return;
+  ncclCommAbort(e->comm);
+  e->comm = nullptr;
+  e->aborts.fetch_add(1);
+  set_err(e, why);
+}
+
+void watchdog(Engine* e) {
+  hipSetDevice(e->device);
+  std::unique_lock<std::mutex> lk(e->mu);
+  while (!e->stop) {
+    e->cv.wait_for(lk, std::chrono::milliseconds(e->pend.empty() ? 50 : 2));
+    if (e->stop) break;
+    while (!e->pend.empty() && hipEventQuery(e->pend.front().ev) == hipSuccess) {
+      e->pool.push_back(e->pend.front().ev);
+      e->pend.pop_front();
+    }
+    if (!e->comm) continue;
+    ncclResult_t a = ncclSuccess;
+    if (ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
+      abort_locked(e, std::string("communicator failed: ") + ncclGetErrorString(a));
+      continue;
+    }
+    if (!e->pend.empty()) {
+      const double age =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - e->pend.front().t).count();
+      if (age > e->timeout) {
+        char b[160];
+        snprintf(b, sizeof b, "collectives made no progress for %.0f s (a peer died or hung): communicator aborted",
+                 age);
+        abort_locked(e, b);
+      }
+    }
   }
-  return settle(e, ncclAllReduce(p, p, count, dt, op, e->comm, s), "ncclAllReduce");
 }
 
 }  // namespace
@@ -228,7 +292,7 @@ TTDK_EXPORT int ttdc_unique_id(char* out) {
 
 // Create the communicator for (rank, nranks) from rank 0's unique id on `device`, plus its
 // stream (priority `prio`: 0 = normal, < 0 = higher). min/max_ctas <= 0 keep RCCL's defaults.
-// Returns nullptr on failure (ttdc_error(nullptr) says why).
+// Starts the watchdog thread. Returns nullptr on failure (ttdc_error(nullptr) says why).
 TTDK_EXPORT void* ttdc_create(const char* id_bytes, int nranks, int rank, int device, int prio, int min_ctas,
                               int max_ctas, double timeout_s, int nonblocking) {
   Engine* e = new Engine();
@@ -261,6 +325,7 @@ TTDK_EXPORT void* ttdc_create(const char* id_bytes, int nranks, int rank, int de
     delete e;
     return nullptr;
   }
+  e->wd = std::thread(watchdog, e);
   return e;
 }
 
@@ -268,17 +333,27 @@ TTDK_EXPORT void* ttdc_stream(void* h) { return static_cast<Engine*>(h)->cs; }
 
 namespace ttdk {
 namespace {
-// The reduction part of a bucket launch (after the fork).
+bool grow_stage(Engine* e, size_t need) {
+  if (need <= e->stage_bytes) return true;
+  // the old staging buffer may still be read by queued work
+  if (!hip_ok(e, hipStreamSynchronize(e->cs), "hipStreamSynchronize")) return false;
+  if (e->stage) hipFree(e->stage);
+  e->stage = nullptr;
+  e->stage_bytes = 0;
+  if (!hip_ok(e, hipMalloc(&e->stage, need), "hipMalloc")) return false;
+  e->stage_bytes = need;
+  return true;
+}
+
+// The reduction part of a bucket launch (after the fork). Caller holds e->mu.
 int bucket_body(Engine* e, void* buf, long long count, int dtype, int op, int algo, int compress) {
   if (compress && dtype == 0) {
     const size_t need = static_cast<size_t>(count) * 2;
     if (need > e->stage_bytes) {
-      // grow once (first step); the old staging buffer may still be read by queued work
-      if (!hip_ok(e, hipStreamSynchronize(e->cs), "hipStreamSynchronize")) return -1;
-      if (e->stage) hipFree(e->stage);
-      e->stage = nullptr;
-      if (!hip_ok(e, hipMalloc(&e->stage, need), "hipMalloc")) return -1;
-      e->stage_bytes = need;
+      // growing needs a stream synchronize + hipMalloc, both illegal under hipGraph capture:
+      // the reducer reserves its largest bucket up front (ttdc_reserve)
+      if (capturing(e->cs)) return set_err(e, "bf16 staging buffer too small under stream capture"), -1;
+      if (!grow_stage(e, need)) return -1;
     }
     hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(cast_grid(count)), dim3(256), 0, e->cs, static_cast<const float*>(buf),
                        static_cast<bf16_t*>(e->stage), count);
@@ -289,8 +364,59 @@ int bucket_body(Engine* e, void* buf, long long count, int dtype, int op, int al
   }
   return reduce_on(e, buf, count, to_nccl(dtype), dt_size(dtype), to_op(op), algo, e->cs) ? 0 : -1;
 }
+
+// Fault injection for the watchdog test: holds the communicator stream until *flag != 0 or
+// max_ms of wall clock passed (every wave exits by itself: no host action can leave it running).
+__global__ void stall_kernel(const volatile int* flag, unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (*flag == 0 && wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(100);
+}
+// Stand-in for one RCCL bucket kernel (tools/comm_interference.py): `ctas` workgroups of 256
+// threads with a 16 KB LDS footprint, each streaming read-modify-write over its share of `buf`
+// (the copy / reduce traffic of a ring step) for `ticks` of wall clock from its own start.
+__global__ __launch_bounds__(256) void comm_emulate_kernel(uint4* buf, long long n16, unsigned long long ticks) {
+  __shared__ uint4 lds[1024];
+  const unsigned long long t0 = wall_clock64();
+  const long long per = (n16 + gridDim.x - 1) / gridDim.x;
+  const long long lo = per * blockIdx.x, hi = lo + per < n16 ? lo + per : n16;
+  long long i = lo + threadIdx.x;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  while (wall_clock64() - t0 < ticks) {
+    if (i >= hi) i = lo + threadIdx.x;
+    if (i < hi) {
+      uint4 v = buf[i];
+      lds[threadIdx.x] = v;
+      acc.x ^= v.x;
+      buf[i] = v;
+      i += blockDim.x;
+    }
+  }
+  if (acc.x == 0x12345678u && threadIdx.x == 0) lds[1023] = acc;  // keep the loop's loads
+}
 }  // namespace
 }  // namespace ttdk
+
+// Interference harness: queue one emulated bucket all-reduce (comm_emulate_kernel) of `us`
+// microseconds on `stream`.
+TTDK_EXPORT int ttdc_emulate_bucket(hipStream_t stream, int ctas, double us, void* buf, long long nbytes) {
+  int dev = 0, rate_khz = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate_khz <= 0)
+    rate_khz = 100000;
+  const unsigned long long ticks = static_cast<unsigned long long>(us * rate_khz / 1000.0);
+  hipLaunchKernelGGL(comm_emulate_kernel, dim3(ctas > 0 ? ctas : 1), dim3(256), 0, stream, static_cast<uint4*>(buf),
+                     nbytes / 16, ticks);
+  return hipGetLastError();
+}
+
+// Pre-size the bf16 staging buffer of compressed buckets for buckets of up to `count` fp32
+// elements (call once before any step is captured).
+TTDK_EXPORT int ttdc_reserve(void* h, long long count) {
+  Engine* e = static_cast<Engine*>(h);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->failed) return -1;
+  return grow_stage(e, static_cast<size_t>(count) * 2) ? 0 : -1;
+}
 
 // Bucket launch: the communicator stream waits for the work already queued on `producer`,
 // then reduces buf[0:count) in place. compress (fp32 buffers only): cast to bf16 on the
@@ -298,7 +424,8 @@ int bucket_body(Engine* e, void* buf, long long count, int dtype, int op, int al
 TTDK_EXPORT int ttdc_bucket(void* h, void* buf, long long count, int dtype, int op, int algo, int compress,
                             hipStream_t producer) {
   Engine* e = static_cast<Engine*>(h);
-  if (e->failed) return -1;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->failed || !e->comm) return -1;
   if (count < 0 || algo < 0 || algo > 2) return set_err(e, "ttdc_bucket: bad argument"), -1;
   if (!fork_from(e, producer)) return -1;
   if (e->timing) {
@@ -337,17 +464,35 @@ TTDK_EXPORT int ttdc_timing(void* h, float* busy_ms, float* span_ms) {
 }
 
 
-// `consumer` waits for every collective queued so far (no host synchronisation). Also reports
-// an asynchronous communicator failure (a peer died / aborted) as an error.
+// `consumer` waits for every collective queued so far (no host synchronisation). Reports a
+// failure the watchdog detected (asynchronous communicator error, or no progress before the
+// deadline) as an error, and arms the watchdog with a marker after the queued collectives
+// (not under stream capture: a captured record never completes on its own).
 TTDK_EXPORT int ttdc_join(void* h, hipStream_t consumer) {
   Engine* e = static_cast<Engine*>(h);
-  if (e->failed) return -1;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->failed || !e->comm) return -1;
   ncclResult_t a = ncclSuccess;
   if (ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress)
     return set_err(e, std::string("communicator failed: ") + ncclGetErrorString(a)), -1;
   if (!hip_ok(e, hipEventRecord(e->join, e->cs), "hipEventRecord") ||
       !hip_ok(e, hipStreamWaitEvent(consumer, e->join, 0), "hipStreamWaitEvent"))
     return -1;
+  if (!capturing(e->cs) && !capturing(consumer)) {
+    hipEvent_t ev = nullptr;
+    if (!e->pool.empty()) {
+      ev = e->pool.back();
+      e->pool.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      ev = nullptr;
+    }
+    if (ev && hipEventRecord(ev, e->cs) == hipSuccess) {
+      e->pend.push_back(Engine::Mark{ev, std::chrono::steady_clock::now()});
+      e->cv.notify_one();
+    } else if (ev) {
+      e->pool.push_back(ev);
+    }
+  }
   return 0;
 }
 
@@ -356,7 +501,8 @@ TTDK_EXPORT int ttdc_join(void* h, hipStream_t consumer) {
 TTDK_EXPORT int ttdc_collective(void* h, int kind, void* buf, long long count, int dtype, int op, int root,
                                 hipStream_t s) {
   Engine* e = static_cast<Engine*>(h);
-  if (e->failed) return -1;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->failed || !e->comm) return -1;
   if (count <= 0) return 0;
   if (kind == 1)
     return settle(e, ncclBroadcast(buf, buf, count, to_nccl(dtype), root, e->comm, s), "ncclBroadcast") ? 0 : -1;
@@ -367,20 +513,47 @@ TTDK_EXPORT int ttdc_collective(void* h, int kind, void* buf, long long count, i
 // against the engine's deadline (a hung peer becomes an error instead of a hang).
 TTDK_EXPORT int ttdc_synchronize(void* h) {
   Engine* e = static_cast<Engine*>(h);
-  if (e->failed) return -1;
-  if (!hip_ok(e, hipEventRecord(e->join, e->cs), "hipEventRecord")) return -1;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->failed || !e->comm) return -1;
+    if (!hip_ok(e, hipEventRecord(e->join, e->cs), "hipEventRecord")) return -1;
+  }
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t q = hipEventQuery(e->join);
-    if (q == hipSuccess) return 0;
+    if (q == hipSuccess) return e->failed ? -1 : 0;
     if (q != hipErrorNotReady) return hip_ok(e, q, "hipEventQuery"), -1;
-    ncclResult_t a = ncclSuccess;
-    if (ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress)
-      return set_err(e, std::string("communicator failed: ") + ncclGetErrorString(a)), -1;
-    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > e->timeout)
-      return set_err(e, "collectives did not complete before the deadline"), -1;
+    {
+      std::lock_guard<std::mutex> lk(e->mu);
+      if (e->failed) return -1;  // the watchdog aborted the communicator
+      ncclResult_t a = ncclSuccess;
+      if (e->comm && ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
+        abort_locked(e, std::string("communicator failed: ") + ncclGetErrorString(a));
+        return -1;
+      }
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > e->timeout) {
+        abort_locked(e, "collectives did not complete before the deadline: communicator aborted");
+        return -1;
+      }
+    }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
+}
+
+// Number of times the watchdog / a deadline aborted this communicator (0 or 1).
+TTDK_EXPORT int ttdc_aborts(void* h) { return static_cast<Engine*>(h)->aborts.load(); }
+
+// Fault injection (tests): queue a kernel on the communicator stream that holds it until
+// *flag (device-visible host memory) becomes non-zero or max_ms passed.
+TTDK_EXPORT int ttdc_debug_stall(void* h, const int* flag, int max_ms) {
+  Engine* e = static_cast<Engine*>(h);
+  int rate_khz = 0;
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, e->device) != hipSuccess || rate_khz <= 0)
+    rate_khz = 100000;
+  const unsigned long long ticks = static_cast<unsigned long long>(rate_khz) * static_cast<unsigned long long>(max_ms);
+  std::lock_guard<std::mutex> lk(e->mu);
+  hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, e->cs, flag, ticks);
+  return hip_ok(e, hipGetLastError(), "stall kernel") ? 0 : -1;
 }
 
 // Bus bandwidth probe: `iters` all-reduces of buf[0:count) (fp32) on the communicator stream,
@@ -392,11 +565,16 @@ TTDK_EXPORT int ttdc_probe(void* h, void* buf, long long count, int iters, float
   hipEventCreate(&a);
   hipEventCreate(&b);
   int rc = 0;
-  if (!settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, e->comm, e->cs), "ncclAllReduce")) rc = -1;
-  hipEventRecord(a, e->cs);
-  for (int i = 0; rc == 0 && i < iters; ++i)
-    if (!settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, e->comm, e->cs), "ncclAllReduce")) rc = -1;
-  hipEventRecord(b, e->cs);
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->comm) rc = -1;
+    if (rc == 0 && !settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, e->comm, e->cs), "ncclAllReduce"))
+      rc = -1;
+    hipEventRecord(a, e->cs);
+    for (int i = 0; rc == 0 && i < iters; ++i)
+      if (!settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, e->comm, e->cs), "ncclAllReduce")) rc = -1;
+    hipEventRecord(b, e->cs);
+  }
   if (rc == 0 && ttdc_synchronize(e) == 0) {
     hipEventElapsedTime(ms, a, b);
     *ms /= iters;
@@ -412,6 +590,12 @@ TTDK_EXPORT int ttdc_probe(void* h, void* buf, long long count, int iters, float
 TTDK_EXPORT void ttdc_destroy(void* h, int abort) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->stop = true;
+  }
+  e->cv.notify_all();
+  if (e->wd.joinable()) e->wd.join();
   if (e->comm) {
     if (abort || e->failed) {
       ncclCommAbort(e->comm);
@@ -420,12 +604,15 @@ TTDK_EXPORT void ttdc_destroy(void* h, int abort) {
       if (settle(e, r, "ncclCommFinalize")) ncclCommDestroy(e->comm);
       else ncclCommAbort(e->comm);
     }
+    e->comm = nullptr;
   }
   if (!abort) hipStreamSynchronize(e->cs);
   for (int i = 0; i < 64; ++i) hipEventDestroy(e->fork[i]);
   hipEventDestroy(e->join);
   for (hipEvent_t ev : e->t_begin) hipEventDestroy(ev);
   for (hipEvent_t ev : e->t_end) hipEventDestroy(ev);
+  for (auto& m : e->pend) hipEventDestroy(m.ev);
+  for (hipEvent_t ev : e->pool) hipEventDestroy(ev);
   if (e->stage) hipFree(e->stage);
   hipStreamDestroy(e->cs);
   delete e;

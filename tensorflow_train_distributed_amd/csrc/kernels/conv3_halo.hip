@@ -267,7 +267,7 @@ template <int C, int BN, int TH, int W, int PRO, bool FLIP, int WM>
 hipError_t launch(const Pro& pa, const bf16_t* w, const EpiParams& E, int Nimg, int H, int N, hipStream_t st) {
   const int nsl = N / BN;
   const int tiles = Nimg * (H / TH);
-  int per_xcd = 256 / (8 * nsl);  // one persistent workgroup per CU in all
+  int per_xcd = big::device_cus() / (8 * nsl);  // one persistent workgroup per (free) CU in all
   if (per_xcd < 1) per_xcd = 1;
   const int need = ceil_div(tiles, 8);
   if (per_xcd > need) per_xcd = need;

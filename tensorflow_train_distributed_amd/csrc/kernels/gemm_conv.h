@@ -37,6 +37,7 @@
 namespace ttdk_rt {
 int& tail_split_flag();
 int& pers_flag();
+int& reserved_cus();
 }
 
 namespace ttdk {
@@ -2048,7 +2049,7 @@ inline float* tail_workspace(hipStream_t st, size_t floats) {
   return nullptr;
 }
 
-inline int device_cus() {
+inline int device_cus_total() {
   static int cus = [] {
     int dev = 0, n = 0;
     hipGetDevice(&dev);
@@ -2056,6 +2057,18 @@ inline int device_cus() {
     return n;
   }();
   return cus;
+}
+
+// CUs a persistent one-workgroup-per-CU grid may assume it owns: all of them, minus the CTA
+// budget of the collective engine while this process runs data-parallel (ttdk_set_reserved_cus,
+// set by parallel/rccl.py to RCCL's maxCTAs). A persistent grid statically partitions its work,
+// so a workgroup that waits for a CU an all-reduce CTA holds delays the whole launch by a full
+// share; sized to the free CUs it never waits (the reserved CUs idle, or take side-stream work,
+// when no bucket is in flight).
+inline int device_cus() {
+  const int total = device_cus_total();
+  const int r = ::ttdk_rt::reserved_cus();
+  return (r > 0 && total - r >= total / 2) ? total - r : total;
 }
 
 template <int BN, class OA, class OB, int F8 = 0, int PP = 0>

@@ -53,7 +53,22 @@ int& pers_flag() {
   static int on = getenv_int("TTD_BIG_PERS", 1);
   return on;
 }
+int& reserved_cus() {
+  static int n = getenv_int("TTD_RESERVED_CUS", 0);
+  return n;
+}
 }  // namespace ttdk_rt
+
+// CUs kept free of persistent grids for the collective engine's CTAs (see device_cus in
+// gemm_conv.h); returns the previous setting.
+TTDK_EXPORT int ttdk_set_reserved_cus(int n) {
+  const int old = ttdk_rt::reserved_cus();
+  ttdk_rt::reserved_cus() = n < 0 ? 0 : n;
+  return old;
+}
+
+// CUs the persistent kernels currently size their grids to.
+TTDK_EXPORT int ttdk_persistent_cus() { return big::device_cus(); }
 
 TTDK_EXPORT int ttdk_set_tail_split(int on) {
   const int old = ttdk_rt::tail_split_flag();

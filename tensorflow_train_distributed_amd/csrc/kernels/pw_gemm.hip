@@ -442,7 +442,7 @@ inline Cfg pick(int N, int K, bool dma) {
 template <int K, int BN, int BM, int PRO, int WM, bool DMA>
 hipError_t launch(const Pro& pa, const bf16_t* w, long long ldw, const EpiParams& E, int M, int N, hipStream_t st) {
   const int nsl = ceil_div(N, BN), tiles = ceil_div(M, BM);
-  int gq = 256 / (8 * nsl);  // one persistent workgroup per CU in all
+  int gq = big::device_cus() / (8 * nsl);  // one persistent workgroup per (free) CU in all
   if (gq < 1) gq = 1;
   const int need = ceil_div(tiles, 8);
   if (gq > need) gq = need;

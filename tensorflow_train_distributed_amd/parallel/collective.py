@@ -93,6 +93,13 @@ class BucketedAllReducer:
             self.comm = rccl.for_group(group, required=engine == "native")
         self.engine = "native-rccl" if self.comm is not None else ("torch-" + dist.get_backend(group)
                                                                    if self.world > 1 else "none")
+        # CUs the persistent kernels leave to the collectives while buckets are in flight
+        # (rccl.py: co-scheduling policy): the communicator's CTA budget on multi-rank groups
+        self.reserved_cus = int(getattr(self.comm, "max_ctas", 0) or 0) if self.world > 1 else 0
+        self._reserved_on = False
+        if self.comm is not None and compress_bf16 and self.buckets:
+            # the bf16 staging buffer at its final size before any step can be graph-captured
+            self.comm.reserve(max(e - s for s, e in self.buckets))
         self._next = 0
         self._works = []
         self._keep = []
@@ -133,12 +140,23 @@ class BucketedAllReducer:
         self._keep = []
         self.launch_log = []
 
+    def _reserve(self, on: bool):
+        if self.reserved_cus <= 0 or on == self._reserved_on:
+            return
+        from . import rccl
+        rccl.set_reserved_cus(self.reserved_cus if on else 0)
+        self._reserved_on = on
+
     def _launch(self, i):
         s, e = self.buckets[i]
         t = self.flat.grad[s:e]
         self.launch_log.append(i)
         if self.world == 1 and self.comm is None:
             return
+        if i == 0:
+            # from the first bucket on, RCCL CTAs may hold CUs: persistent grids launched from
+            # here to finish() use the remaining ones
+            self._reserve(True)
         if self.comm is not None:
             # in place on the communicator stream, ordered after the current (producing) stream
             self.comm.bucket(t, algorithm=self.algorithm, compress=self.compress)
@@ -194,6 +212,7 @@ class BucketedAllReducer:
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
+        self._reserve(False)
         if self.comm is not None:
             if self._timed is not None:
                 self._timed[0].record()  # the backward's last queued work

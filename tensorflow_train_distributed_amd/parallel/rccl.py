@@ -7,10 +7,22 @@ fork from the stream that produced the bucket's last gradient onto the communica
 then the in-place RCCL call(s); `join()` makes the consumer stream wait. No host
 synchronisation anywhere on the step path, and the calls are capture-safe (hipGraph).
 
+Co-scheduling policy (MI355X, one process per GPU): the fastest backward kernels are persistent,
+one workgroup per CU with a static work split (gemm256p, the pointwise / halo conv kernels), so
+a workgroup that finds its CU held by an all-reduce CTA delays the whole launch by a full share.
+A multi-rank communicator therefore gets a fixed CTA budget (RCCL maxCTAs, default 8 = 3 % of
+the 256 CUs: a ResNet-50 step moves ~100 MB of fp32 gradients, BERT-Large ~1.3 GB, both far
+below what 8 channels carry over xGMI in the backward's duration), and while the step's buckets
+are in flight the persistent grids size themselves to the remaining CUs
+(ttdk_set_reserved_cus, set by BucketedAllReducer from its first bucket launch to finish()).
+tools/comm_interference.py measures the policy on one GPU with an emulated all-reduce of the
+same CTA count launched at the real bucket points.
+
 Tuning knobs (environment, read at communicator creation):
   TTD_RCCL_MAX_CTAS / TTD_RCCL_MIN_CTAS  RCCL's CTA (workgroup) budget per collective: how many
                                          CUs a bucket all-reduce may occupy while it overlaps
-                                         the backward GEMMs (default: RCCL's own choice)
+                                         the backward GEMMs (default max 8 on multi-rank
+                                         groups; 0 = RCCL's own choice, no CU reservation)
   TTD_RCCL_PRIO                          communicator stream priority (default 0 = normal, below
                                          the main chain's high-priority stream)
   TTD_RCCL_TIMEOUT                       seconds before a collective that makes no progress (a
@@ -68,6 +80,18 @@ def _lib():
         lib.ttdc_timing.argtypes = [c_void_p, ctypes.POINTER(c_float), ctypes.POINTER(c_float)]
         lib.ttdc_destroy.restype = None
         lib.ttdc_destroy.argtypes = [c_void_p, c_int]
+        lib.ttdc_reserve.restype = c_int
+        lib.ttdc_reserve.argtypes = [c_void_p, c_longlong]
+        lib.ttdc_aborts.restype = c_int
+        lib.ttdc_aborts.argtypes = [c_void_p]
+        lib.ttdc_debug_stall.restype = c_int
+        lib.ttdc_debug_stall.argtypes = [c_void_p, c_void_p, c_int]
+        lib.ttdc_emulate_bucket.restype = c_int
+        lib.ttdc_emulate_bucket.argtypes = [c_void_p, c_int, c_double, c_void_p, c_longlong]
+        lib.ttdk_set_reserved_cus.restype = c_int
+        lib.ttdk_set_reserved_cus.argtypes = [c_int]
+        lib.ttdk_persistent_cus.restype = c_int
+        lib.ttdk_persistent_cus.argtypes = []
         _bound = True
     return lib
 
@@ -76,6 +100,28 @@ def rccl_version() -> int:
     """Version code of the RCCL the process actually loaded (torch's bundled one when torch
     came first: both export the soname librccl.so.1)."""
     return int(_lib().ttdc_version())
+
+
+DEFAULT_MAX_CTAS = 8
+
+
+def set_reserved_cus(n: int) -> int:
+    """CUs the persistent kernels leave to the collective engine's CTAs (0 = none); returns the
+    previous value. Host-side, takes effect for kernels launched after the call."""
+    return int(_lib().ttdk_set_reserved_cus(int(n)))
+
+
+def persistent_cus() -> int:
+    """CUs the persistent kernels currently size their grids to."""
+    return int(_lib().ttdk_persistent_cus())
+
+
+def emulate_bucket(stream, ctas: int, us: float, buf: torch.Tensor):
+    """Queue an emulated bucket all-reduce (`ctas` workgroups streaming over `buf` for `us`
+    microseconds) on `stream`: the one-GPU stand-in of an RCCL bucket kernel."""
+    rc = _lib().ttdc_emulate_bucket(_stream_ptr(stream), int(ctas), float(us), buf.data_ptr(), buf.numel() * buf.element_size())
+    if rc != 0:
+        raise errors.InternalError("emulated bucket launch failed (%d)" % rc)
 
 
 def unique_id() -> bytes:
@@ -102,7 +148,11 @@ class RcclCommunicator:
         env = os.environ.get
         prio = int(env("TTD_RCCL_PRIO", "0")) if priority is None else int(priority)
         min_ctas = int(env("TTD_RCCL_MIN_CTAS", "0")) if min_ctas is None else int(min_ctas)
-        max_ctas = int(env("TTD_RCCL_MAX_CTAS", "0")) if max_ctas is None else int(max_ctas)
+        if max_ctas is None:
+            max_ctas = int(env("TTD_RCCL_MAX_CTAS", str(DEFAULT_MAX_CTAS if int(nranks) > 1 else 0)))
+        max_ctas = int(max_ctas)
+        if min_ctas > max_ctas > 0:
+            min_ctas = max_ctas
         timeout = float(env("TTD_RCCL_TIMEOUT", "300")) if timeout is None else float(timeout)
         nonblocking = env("TTD_RCCL_NONBLOCKING", "0") == "1" if nonblocking is None else bool(nonblocking)
         self.device = torch.device(device)
@@ -120,14 +170,24 @@ class RcclCommunicator:
     @classmethod
     def for_group(cls, group=None, device=None, **kw) -> "RcclCommunicator":
         """Collective over `group`: rank 0 draws the unique id, the torch process group carries
-        it to the others."""
+        it to the others — together with a status byte, so a failure on rank 0 (no id) reaches
+        every rank through the same broadcast and all of them raise (no rank is left waiting in
+        a different collective)."""
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        ids = torch.zeros(128, dtype=torch.uint8, device=dev if dist.get_backend(group) == "nccl" else "cpu")
+        msg = torch.zeros(129, dtype=torch.uint8, device=dev if dist.get_backend(group) == "nccl" else "cpu")
+        why = ""
         if rank == 0:
-            ids.copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
-        dist.broadcast(ids, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-        return cls(bytes(ids.cpu().tolist()), world, rank, dev, **kw)
+            try:
+                msg[:128].copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
+                msg[128] = 1
+            except Exception as e:  # noqa: BLE001 - reported to every rank below
+                why = "%s: %s" % (type(e).__name__, e)
+        dist.broadcast(msg, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        host = msg.cpu()
+        if int(host[128]) != 1:
+            raise errors.UnavailableError("RCCL unique id unavailable on rank 0%s" % (": " + why if why else ""))
+        return cls(bytes(host[:128].tolist()), world, rank, dev, **kw)
 
     # ------------------------------------------------------------------ step path
     def _check(self, rc: int, what: str):
@@ -162,6 +222,21 @@ class RcclCommunicator:
         self._check(_lib().ttdc_collective(self._h, 1, t.data_ptr(), t.numel(), _DT[t.dtype], 0, int(root),
                                            _stream_ptr(stream)), "broadcast")
         return t
+
+    def reserve(self, count: int):
+        """Pre-size the bf16 staging buffer for compressed buckets of up to `count` fp32
+        elements (growing it later would need a stream sync + hipMalloc: illegal in capture)."""
+        self._check(_lib().ttdc_reserve(self._h, int(count)), "staging reserve")
+
+    @property
+    def aborted(self) -> bool:
+        """The watchdog (or a synchronize deadline) aborted this communicator."""
+        return bool(self._h) and _lib().ttdc_aborts(self._h) > 0
+
+    def debug_stall(self, flag_ptr: int, max_ms: int):
+        """Fault injection: hold the communicator stream until the int at flag_ptr (host memory
+        the device can read) is non-zero or max_ms passed."""
+        self._check(_lib().ttdc_debug_stall(self._h, flag_ptr, int(max_ms)), "debug stall")
 
     def synchronize(self):
         """Host wait for the communicator stream with a deadline (a dead peer raises)."""

@@ -338,7 +338,16 @@ def _launch_replicas(n: int):
     import subprocess
     import sys
     script = sys.argv[0] if sys.argv else ""
-    if os.environ.get("TTD_MIRRORED_SPAWN", "1") == "0" or not script or script == "-c" or not os.path.exists(script):
+    main = sys.modules.get("__main__")
+    spec = getattr(main, "__spec__", None)
+    # `python -m pkg.mod`: re-run as a module (a file path would break its relative imports)
+    entry = ["-m", spec.name] if spec is not None and spec.name not in ("__main__", None) else [script]
+    refuse = (os.environ.get("TTD_MIRRORED_SPAWN", "1") == "0" or not script or script == "-c"
+              or not os.path.exists(script)
+              # a test runner / an embedding process: relaunching would re-run the whole session
+              or os.path.basename(script).startswith(("pytest", "py.test")) or "pytest" in sys.modules
+              or (spec is not None and spec.name.split(".")[0] in ("pytest", "IPython", "ipykernel")))
+    if refuse:
         raise RuntimeError("MirroredStrategy over %d GPUs needs one process per GPU: launch the script with "
                            "`python -m torch.distributed.run --nproc-per-node %d ...` (or pass devices=[...] "
                            "with one device)" % (n, n))
@@ -348,7 +357,7 @@ def _launch_replicas(n: int):
     port = sck.getsockname()[1]
     sck.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), script] + sys.argv[1:]
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] + entry + sys.argv[1:]
     sys.exit(subprocess.call(cmd))
 
 

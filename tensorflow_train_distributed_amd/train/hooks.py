@@ -156,6 +156,7 @@ class CheckpointSaverHook(SessionRunHook):
         self._basename = checkpoint_basename
         self._listeners = listeners or []
         self.saved_paths: List[str] = []
+        self.agree_every = max(1, int(os.environ.get("TTD_CKPT_AGREE_STEPS", "50")))
 
     def begin(self):
         if self._dir:
@@ -179,7 +180,12 @@ class CheckpointSaverHook(SessionRunHook):
         fire = self._timer.should_trigger_for_step(step)
         agree = getattr(run_context.session, "agree", None)
         if agree is not None and self._timer._every_secs is not None:
-            fire = agree(fire)  # all-reduce replicas: replica 0's clock decides for everyone
+            # all-reduce replicas: replica 0's clock decides for everyone. The agreement is a
+            # broadcast + host sync, so it runs only on every agree_every-th global step (the
+            # replicas see the same global steps, so they all take part in the same ones); the
+            # save lands at most agree_every steps after the timer fired, and every other step
+            # keeps the host running ahead of the GPU.
+            fire = agree(fire) if step % self.agree_every == 0 else False
         if fire:
             self._timer.update_last_triggered_step(step)
             if self._save(run_context.session, step):

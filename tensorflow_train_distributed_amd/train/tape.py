@@ -202,6 +202,23 @@ class GradientTape:
         return out[0] if single else out
 
 
+def clip_by_global_norm(t_list, clip_norm, use_norm=None):
+    """tf.clip_by_global_norm: scale every tensor by clip_norm / max(global_norm, clip_norm).
+    Returns (clipped list, global_norm). None entries pass through. One fused norm over the
+    list (torch._foreach_norm), no host sync."""
+    ts = [t for t in t_list if t is not None]
+    if use_norm is None:
+        if ts:
+            norms = torch._foreach_norm([t.float() for t in ts])
+            use_norm = torch.linalg.vector_norm(torch.stack(norms))
+        else:
+            use_norm = torch.zeros(())
+    scale = clip_norm / torch.maximum(use_norm, torch.as_tensor(clip_norm, dtype=use_norm.dtype,
+                                                                    device=use_norm.device))
+    out = [None if t is None else t * scale.to(t.dtype) for t in t_list]
+    return out, use_norm
+
+
 def apply_gradients(optimizer, grads_and_vars, global_step=None, name=None,
                     experimental_aggregate_gradients: bool = True):
     """Optimizer.apply_gradients for flat-backed variables (see module docstring)."""
@@ -231,7 +248,14 @@ def apply_gradients(optimizer, grads_and_vars, global_step=None, name=None,
             if s.trainable and s.name not in passed:
                 fp.g[s.name].zero_()
     st = _replica_strategy()
-    if st is not None and experimental_aggregate_gradients and (copied or not getattr(fp, "_ttd_aggregated", False)):
+    # One aggregation point: gradients from tape.gradient are already replica-summed (the bucket
+    # all-reduce overlapped the backward). Whatever the caller did to them afterwards (clipping,
+    # scaling) ran on identical values on every replica, so reducing again would multiply every
+    # gradient by the world size. Only gradients that did not come from an aggregating tape
+    # (e.g. torch.autograd.grad) are all-reduced here. `copied` only says the flat buffer was
+    # refreshed from the caller's tensors.
+    del copied
+    if st is not None and experimental_aggregate_gradients and not getattr(fp, "_ttd_aggregated", False):
         import torch.distributed as dist
         dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=st.group)
     fp._ttd_aggregated = False

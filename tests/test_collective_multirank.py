@@ -167,7 +167,7 @@ def test_bench_self_launches_n_ranks(n):
     assert r["value"] > 0 and r["ms_per_step"] > 0
 
 
-def _tape_worker(rank, world, store, q):
+def _tape_worker(rank, world, store, q, clip=None):
     """tf.distribute custom training loop on a user-defined ttd.layers model: GradientTape +
     optimizer.apply_gradients inside strategy.run, replicas on gloo."""
     torch.set_num_threads(1)
@@ -191,6 +191,8 @@ def _tape_worker(rank, world, store, q):
             logits = model(x)
             loss = torch.nn.functional.cross_entropy(logits, y, reduction="sum") / (B * world)
         grads = tape.gradient(loss, model.trainable_variables)
+        if clip is not None:  # the caller rewrites the gradients before applying them
+            grads, _ = ttd.clip_by_global_norm(grads, clip)
         opt.apply_gradients(zip(grads, model.trainable_variables))
         return loss
 
@@ -202,9 +204,12 @@ def _tape_worker(rank, world, store, q):
     dist.destroy_process_group()
 
 
-def test_gradient_tape_apply_gradients_matches_big_batch(tmp_path):
+@pytest.mark.parametrize("clip", [None, 0.05, 1e9])
+def test_gradient_tape_apply_gradients_matches_big_batch(tmp_path, clip):
+    """clip: gradients clipped (0.05: every step clips) or rescaled by exactly 1 (1e9) between
+    tape.gradient and apply_gradients -- they must not be all-reduced a second time."""
     import tensorflow_train_distributed_amd as ttd
-    res = _spawn(_tape_worker, 2, tmp_path)
+    res = _spawn(_tape_worker, 2, tmp_path, clip)
     assert torch.equal(res[0]["w"], res[1]["w"])  # replicas identical (rank 0's init was broadcast)
     # the same 4 steps in one process over the whole global batch, from rank 0's initial weights
     ttd.layers.reset_naming(seed=100)
@@ -217,6 +222,8 @@ def test_gradient_tape_apply_gradients_matches_big_batch(tmp_path):
         with ttd.GradientTape() as tape:
             loss = torch.nn.functional.cross_entropy(model(X[i]), Y[i])
         grads = tape.gradient(loss, model.trainable_variables)
+        if clip is not None:
+            grads, _ = ttd.clip_by_global_norm(grads, clip)
         opt.apply_gradients(zip(grads, model.trainable_variables))
     assert flat.names() == res[0]["names"]
     torch.testing.assert_close(res[0]["w"], flat.master, rtol=2e-5, atol=2e-5)

@@ -1,12 +1,16 @@
 """The native RCCL collective engine (csrc/kernels/collective.hip, parallel/rccl.py) on one GPU.
 
 A one-GPU box can only host one-rank RCCL communicators (RCCL refuses two ranks on one device:
-"Duplicate GPU detected"), so these tests check what one rank can: the engine's stream ordering
-(bucket launches fork from the producing stream, `join` makes the consumer wait), the bf16
-compression casts, every reduction algorithm's code path, hipGraph capture of bucket
-launches, the bus-bandwidth probe, and BucketedAllReducer driving the engine. The N-rank
-arithmetic (mean over replicas, bucket order) is covered on gloo by test_collective_multirank.py
-over the same BucketedAllReducer, and by the driver's multi-GPU bench (`replicas_in_sync`).
+"Duplicate GPU detected"), and on one rank every algorithm's plan is a single all-reduce. So
+these tests check what one rank can: the engine's stream ordering (bucket launches fork from the
+producing stream, `join` makes the consumer wait), the bf16 compression casts, the one-rank
+identity of each algorithm's entry point, hipGraph capture of bucket launches, the bus-bandwidth
+probe, BucketedAllReducer driving the engine, the watchdog turning a stalled communicator stream
+into an error, and the persistent-grid CU reservation. What they do NOT run: the multi-rank
+branches (reduce-scatter / all-gather / reduce / broadcast). Their per-rank call plans are
+replayed against RCCL semantics on the CPU for 2..8 ranks (tests/test_collective_plan.py); the
+mean-over-replicas property is covered on gloo (test_collective_multirank.py) and by the
+driver's multi-GPU bench (`replicas_in_sync`).
 """
 import pytest
 import torch
@@ -143,3 +147,53 @@ def test_bucketed_allreducer_drives_the_engine():
         from tensorflow_train_distributed_amd.parallel import rccl
         rccl.abort_all()
         dist.destroy_process_group()
+
+
+def test_watchdog_aborts_a_stalled_communicator():
+    """A peer that never arrives leaves the communicator stream stuck: the watchdog thread sees
+    the join marker older than the deadline, aborts the communicator, and the next bucket / join
+    raises (UnavailableError: what the recoverable session acts on) instead of hanging."""
+    import time
+    from tensorflow_train_distributed_amd.parallel import rccl
+    from tensorflow_train_distributed_amd.utils import errors
+    dev = torch.device("cuda", 0)
+    c = rccl.RcclCommunicator(rccl.unique_id(), 1, 0, dev, timeout=1.0)
+    flag = torch.zeros(1, dtype=torch.int32).pin_memory()
+    try:
+        # stall the communicator stream (kernel exits by itself after 20 s at the latest)
+        c.debug_stall(flag.data_ptr(), 20000)
+        c.join()  # arms the watchdog: the marker sits behind the stall
+        t0 = time.time()
+        while not c.aborted and time.time() - t0 < 10:
+            time.sleep(0.05)
+        assert c.aborted, "watchdog did not abort within 10 s"
+        assert 0.8 < time.time() - t0 < 10
+        x = torch.zeros(1024, device=dev)
+        with pytest.raises(errors.UnavailableError):
+            c.bucket(x)
+        with pytest.raises(errors.UnavailableError):
+            c.join()
+        assert "no progress" in c.error
+    finally:
+        flag[0] = 1  # release the stall kernel
+        torch.cuda.synchronize()
+        c.destroy(abort=True)
+
+
+def test_persistent_grids_follow_the_cu_reservation():
+    from tensorflow_train_distributed_amd.parallel import rccl
+    total = torch.cuda.get_device_properties(0).multi_processor_count
+    old = rccl.set_reserved_cus(8)
+    try:
+        assert rccl.persistent_cus() == total - 8
+        # the persistent kernels still compute the same thing on fewer CUs
+        from tensorflow_train_distributed_amd.ops import gemm as G
+        a = torch.randn(65536, 1024, device="cuda").bfloat16()  # 1024 tiles: the persistent kernel
+        b = torch.randn(1024, 1024, device="cuda").bfloat16()
+        ref = (a.float() @ b.float())
+        out = G.gemm(a, b)
+        rel = float((out.float() - ref).norm() / ref.norm())
+        assert rel < 1e-2, rel
+    finally:
+        rccl.set_reserved_cus(old)
+    assert rccl.persistent_cus() == total
