@@ -287,14 +287,21 @@ def main():
     if main_prio and not on_cpu:
         prio = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
         prio.wait_stream(torch.cuda.current_stream())
+    graph_info = None
     if use_graph:
         # the whole step (both streams: the side-stream weight-gradient chain forks from and
         # joins the captured stream, so replay keeps the two branches concurrent) in one hipGraph
-        from tensorflow_train_distributed_amd.utils.graphs import capture
+        # whose kernel nodes keep the eager streams' priorities (utils/graphs.py)
+        from tensorflow_train_distributed_amd.utils.graphs import capture, capture_prioritized
         for _ in range(2):
             step()
         sync()
-        graph, out = capture(step, stream=prio)
+        if os.environ.get("TTD_GRAPH_PRIO", "1") != "0":
+            graph = capture_prioritized(step, stream=prio)
+            out = graph.outputs
+            graph_info = graph.info
+        else:
+            graph, out = capture(step, stream=prio)
         run = graph.replay
     else:
         run = step
@@ -381,6 +388,8 @@ def main():
     if rank == 0:
         cfg = dict(info["config"])
         cfg["hipgraph"] = bool(use_graph)
+        if graph_info is not None:
+            cfg["hipgraph_node_priority"] = graph_info
         if not on_cpu:
             cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         cfg["final_loss"] = loss

@@ -225,13 +225,18 @@ bool capturing(hipStream_t s) {
   return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
-// Abort the communicator (caller holds e->mu): RCCL's kernels see the abort flag and exit.
-void abort_locked(Engine* e, const std::string& why) {
+// Abort the communicator. Caller holds `lk` on e->mu; the engine is marked failed and detached
+// from the communicator first, then the lock is released around ncclCommAbort (which can wait for
+// queued work): every other call sees the failure at once instead of blocking on the lock.
+void abort_locked(Engine* e, std::unique_lock<std::mutex>& lk, const std::string& why) {
   if (!e->comm) return;
-  ncclCommAbort(e->comm);
+  ncclComm_t c = e->comm;
   e->comm = nullptr;
-  e->aborts.fetch_add(1);
   set_err(e, why);
+  e->aborts.fetch_add(1);
+  lk.unlock();
+  ncclCommAbort(c);
+  lk.lock();
 }
 
 void watchdog(Engine* e) {
@@ -247,7 +252,7 @@ void watchdog(Engine* e) {
     if (!e->comm) continue;
     ncclResult_t a = ncclSuccess;
     if (ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
-      abort_locked(e, std::string("communicator failed: ") + ncclGetErrorString(a));
+      abort_locked(e, lk, std::string("communicator failed: ") + ncclGetErrorString(a));
       continue;
     }
     if (!e->pend.empty()) {
@@ -257,7 +262,7 @@ void watchdog(Engine* e) {
         char b[160];
         snprintf(b, sizeof b, "collectives made no progress for %.0f s (a peer died or hung): communicator aborted",
                  age);
-        abort_locked(e, b);
+        abort_locked(e, lk, b);
       }
     }
   }
@@ -524,15 +529,15 @@ TTDK_EXPORT int ttdc_synchronize(void* h) {
     if (q == hipSuccess) return e->failed ? -1 : 0;
     if (q != hipErrorNotReady) return hip_ok(e, q, "hipEventQuery"), -1;
     {
-      std::lock_guard<std::mutex> lk(e->mu);
+      std::unique_lock<std::mutex> lk(e->mu);
       if (e->failed) return -1;  // the watchdog aborted the communicator
       ncclResult_t a = ncclSuccess;
       if (e->comm && ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
-        abort_locked(e, std::string("communicator failed: ") + ncclGetErrorString(a));
+        abort_locked(e, lk, std::string("communicator failed: ") + ncclGetErrorString(a));
         return -1;
       }
       if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > e->timeout) {
-        abort_locked(e, "collectives did not complete before the deadline: communicator aborted");
+        abort_locked(e, lk, "collectives did not complete before the deadline: communicator aborted");
         return -1;
       }
     }

@@ -35,6 +35,7 @@ import numpy as np
 import torch
 
 from ..train.flat import FlatParams, ParamSpec
+from ..utils import graphs
 
 
 @dataclass
@@ -309,7 +310,7 @@ class BertPretraining:
             ev = torch.cuda.Event()
             ev.record()
             side.wait_event(ev)
-            with torch.cuda.stream(side):
+            with graphs.side_scope(side), torch.cuda.stream(side):
                 wgrad(dy, x, wout)
                 if bout is not None:
                     K.colsum(dy, out=bout)
@@ -321,7 +322,7 @@ class BertPretraining:
                 ev0 = torch.cuda.Event()
                 ev0.record()
                 side.wait_event(ev0)
-                with torch.cuda.stream(side):
+                with graphs.side_scope(side), torch.cuda.stream(side):
                     self._refresh_transposed()
                     wt_ready = torch.cuda.Event()
                     wt_ready.record()
@@ -332,7 +333,7 @@ class BertPretraining:
             if side is None:
                 hook(name)
             else:
-                with torch.cuda.stream(side):
+                with graphs.side_scope(side), torch.cuda.stream(side):
                     hook(name)
 
         ids = batch.input_ids.reshape(-1)

@@ -30,6 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from ..train.flat import FlatParams, ParamSpec
+from ..utils import graphs
 
 STAGES_50 = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
 
@@ -472,7 +473,7 @@ class ResNet:
                 ev = torch.cuda.Event()
                 ev.record()
                 side.wait_event(ev)
-            with torch.cuda.stream(side):
+            with graphs.side_scope(side), torch.cuda.stream(side):
                 G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
                 if ready:
                     self._ready(c.name + "_bn/moving_variance")
@@ -561,7 +562,7 @@ class ResNet:
                 ev = torch.cuda.Event()
                 ev.record()
                 side.wait_event(ev)
-                with torch.cuda.stream(side):
+                with graphs.side_scope(side), torch.cuda.stream(side):
                     sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
                 # h / h8 stay referenced (c1's ctx) past the join below; cd's outputs were made on
                 # the side stream, whose next work is always ordered after this step's main stream
@@ -638,7 +639,7 @@ class ResNet:
                 ev.record()
                 side.wait_event(ev)
                 self._cd_done = None
-                with torch.cuda.stream(side):
+                with graphs.side_scope(side), torch.cuda.stream(side):
                     dx, _ = self._convbn_bwd(blk["cd"], dh, cd, dstat=cd_stat, sampled_only=sampled, wgrad_last=True)
                     cd_done = self._cd_done
                 assert cd_done is not None, "projection backward took a path without the wgrad_last event"
@@ -654,7 +655,7 @@ class ResNet:
             if cd_done is not None:
                 # c3 / c2 weight gradients are now queued on the side stream behind the projection's:
                 # the bucket hook for the projection variables can fire (in flat-layout order)
-                with torch.cuda.stream(side):
+                with graphs.side_scope(side), torch.cuda.stream(side):
                     self._ready(blk["cd"].name + "_bn/moving_variance")
                 torch.cuda.current_stream().wait_event(cd_done)
             elif blk["cd"] is not None:

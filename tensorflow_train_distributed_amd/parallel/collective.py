@@ -94,8 +94,11 @@ class BucketedAllReducer:
         self.engine = "native-rccl" if self.comm is not None else ("torch-" + dist.get_backend(group)
                                                                    if self.world > 1 else "none")
         # CUs the persistent kernels leave to the collectives while buckets are in flight
-        # (rccl.py: co-scheduling policy): the communicator's CTA budget on multi-rank groups
-        self.reserved_cus = int(getattr(self.comm, "max_ctas", 0) or 0) if self.world > 1 else 0
+        # (rccl.py: co-scheduling policy). Opt-in: at the default CTA budget the measured
+        # interference is < 1 % without it (tools/comm_interference.py)
+        import os
+        self.reserved_cus = (int(getattr(self.comm, "max_ctas", 0) or 0)
+                             if self.world > 1 and os.environ.get("TTD_RESERVE_COMM_CUS", "0") == "1" else 0)
         self._reserved_on = False
         if self.comm is not None and compress_bf16 and self.buckets:
             # the bf16 staging buffer at its final size before any step can be graph-captured

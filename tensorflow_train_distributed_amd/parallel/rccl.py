@@ -271,12 +271,12 @@ class RcclCommunicator:
             self._h = None
 
     def __del__(self):
-        import sys
-        if sys.is_finalizing():  # the HIP runtime may already be gone: leave it to process exit
-            return
         try:
+            import sys
+            if sys.is_finalizing():  # the HIP runtime may already be gone: leave it to process exit
+                return
             self.destroy(abort=True)
-        except Exception:  # noqa: BLE001
+        except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 
 

@@ -486,3 +486,46 @@ def test_stem_forward_kernel_matches_conv_oracle(N, cin):
     # same values as the generic implicit-GEMM conv (both round the fp32 sum once)
     y2 = G.conv_fwd(xs, w, (2, 2), (3, 3))
     assert _rel(ys, y2) < 8e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [
+    # (N, H, C = dx channels, K = dz channels, R): ResNet-50 b1024 per-image stage shapes of the
+    # c1 data gradients that accumulate into the shortcut gradient (stage 2, 3, 4) and a 3x3
+    (48, 56, 256, 64, 1),
+    (96, 28, 512, 128, 1),
+    (192, 14, 1024, 256, 1),
+    (64, 28, 128, 128, 3),
+])
+def test_pipelined_feeding_bn_epilogue_vs_fp32_conv(cfg):
+    """The 256-row kernel's prefetched feeding-BN epilogue (dgrad + accumulate into the shortcut
+    gradient + ReLU mask of the feeding unit + its BN-backward sums, gemm_conv.h feed_epilogue)
+    against an fp32 torch convolution oracle (torch.nn.grad.conv2d_input), not the engine's own
+    un-fused dgrad."""
+    from torch.nn.grad import conv2d_input
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    N, H, C, K, R = cfg
+    p = R // 2
+    torch.manual_seed(5)
+    dz = torch.randn(N, H, H, K, device="cuda").bfloat16()
+    w = (torch.randn(K, R, R, C, device="cuda") / (R * R * K) ** 0.5).bfloat16()  # [K, R, S, C]
+    wt = w.permute(3, 1, 2, 0).contiguous()  # the dgrad operand [C, R, S, K]
+    y = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    keep = torch.rand(N * H * H * C, device="cuda") > 0.4
+    bits = keep.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)
+    mask = bits.sum(1).to(torch.uint8)
+    old = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    dx = conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), dz.float().permute(0, 3, 1, 2),
+                      padding=p).permute(0, 2, 3, 1)
+    ref_g = (dx + old.float()) * keep.view(N, H, H, C)
+    out = old.clone()
+    got, partial, T = G.conv_dgrad(dz, wt, (N, H, H, C), (1, 1), (p, p), out=out, beta=1, bn_stat=(y, mask))[:3]
+    assert _rel(got, ref_g) < 1e-2
+    assert bool(((got.float() != 0) <= keep.view(N, H, H, C)).all())
+    sums = partial.sum(0)
+    gs, yf = ref_g.view(-1, C), y.float().view(-1, C)
+    # statistics of the fused gradient vs the fp32 oracle's (bf16 storage of g: ~1e-3 relative)
+    assert _rel(sums[0], gs.sum(0)) < 2e-2
+    assert _rel(sums[1], (gs * yf).sum(0)) < 2e-2
+    # ... and exactly consistent with the gradient it stored
+    torch.testing.assert_close(sums[1], (got.float().view(-1, C) * yf).sum(0), rtol=2e-3, atol=5e-2)
