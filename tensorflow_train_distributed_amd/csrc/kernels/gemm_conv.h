@@ -35,7 +35,6 @@
 // process-wide runtime switches shared by every translation unit of libttd_hip (defined in
 // gemm_conv.hip; everything below lives in an anonymous namespace, i.e. per TU)
 namespace ttdk_rt {
-int& tail_split_flag();
 int& pers_flag();
 int& reserved_cus();
 }
@@ -1393,8 +1392,8 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   const int nblk = tiles_m * tiles_n;
   const int t = xcd_remap(blockIdx.x, nblk);
   const int tile_n = t % tiles_n;
-  // m_base: first GEMM row of this launch (the split-K tail launch of `launch` below); the tile
-  // row index used for the BN statistics rows is absolute
+  // m_base: first GEMM row of this launch (0 for every launch today); the tile row index used
+  // for the BN statistics rows is absolute
   const int tile_m = m_base / BM + t / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1939,116 +1938,6 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
   }
 }
 
-// Split-K tail epilogue: rows [m_base, M) of the GEMM were computed as S fp32 slabs
-// ws[S][M - m_base][N] (alpha applied); sum them, stage the tile as bf16 and run the same
-// fused epilogue (epi_rows + BN statistics) the 256-row kernel runs, for tile rows
-// m_base/256 + blockIdx.x / tn.
-template <int BN>
-__global__ __launch_bounds__(THR, 1) void tail_epilogue_kernel(const float* __restrict__ ws, int S, long long slab,
-                                                               EpiParams E, int M, int N, int m_base, int tn) {
-  using Gm = Geo<BN>;
-  constexpr int PITCH = Gm::PITCH;
-  __shared__ __attribute__((aligned(16))) char smem[Gm::EPI];
-  const int tile_n = blockIdx.x % tn, tile_m = m_base / BM + blockIdx.x / tn;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int q = tid; q < BM * (BN / 4); q += THR) {
-    const int r = q / (BN / 4), c4 = q % (BN / 4);
-    const int m = m0 + r, n = n0 + c4 * 4;
-    f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-    if (m < M && n < N) {
-      const float* p = ws + static_cast<long long>(m - m_base) * N + n;
-      for (int k = 0; k < S; ++k) v += *reinterpret_cast<const f32x4_t*>(p + k * slab);
-    }
-    *reinterpret_cast<uint2*>(smem + r * PITCH + c4 * 8) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-  }
-  __syncthreads();
-  constexpr int CPR = BN / 8, RPP = THR / CPR;
-  const int c = tid % CPR, r0 = tid / CPR;
-  const int n = n0 + c * 8;
-  const bool nfull = n + 8 <= N;
-  const bool vst = nfull && (E.ldo & 7) == 0;
-  const bool vres = nfull && (E.ldr & 7) == 0;
-  float bias8[8], s8[8], q8[8], r8[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bias8[j] = (E.bias && n + j < N) ? E.bias[n + j] : 0.f;
-    s8[j] = q8[j] = r8[j] = 0.f;
-  }
-  if (E.beta || E.residual || E.by)
-    epi_rows<BM, RPP, PITCH, true>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
-  else
-    epi_rows<BM, RPP, PITCH, false>(E, smem, c, r0, n, m0, M, N, vst, vres, bias8, s8, q8, r8);
-  if (!E.stat) return;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-#pragma unroll
-    for (int o = CPR; o < 64; o <<= 1) {
-      s8[j] += __shfl_xor(s8[j], o, 64);
-      q8[j] += __shfl_xor(q8[j], o, 64);
-      if (E.stat2) r8[j] += __shfl_xor(r8[j], o, 64);
-    }
-  }
-  float* red = reinterpret_cast<float*>(smem + BM * PITCH);  // [8 waves][3][BN]
-  if (lane < CPR) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[(wave * 3 + 0) * BN + c * 8 + j] = s8[j];
-      red[(wave * 3 + 1) * BN + c * 8 + j] = q8[j];
-      red[(wave * 3 + 2) * BN + c * 8 + j] = r8[j];
-    }
-  }
-  __syncthreads();
-  for (int t2 = tid; t2 < BN; t2 += THR) {
-    if (n0 + t2 < N) {
-      float ss = 0.f, qq = 0.f, rr = 0.f;
-#pragma unroll
-      for (int k = 0; k < THR / 64; ++k) {
-        ss += red[(k * 3 + 0) * BN + t2];
-        qq += red[(k * 3 + 1) * BN + t2];
-        rr += red[(k * 3 + 2) * BN + t2];
-      }
-      E.stat[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t2] = ss;
-      E.stat[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t2] = qq;
-      if (E.stat2) {
-        E.stat2[(static_cast<long long>(tile_m) * 2 + 0) * N + n0 + t2] = ss;
-        E.stat2[(static_cast<long long>(tile_m) * 2 + 1) * N + n0 + t2] = rr;
-      }
-    }
-  }
-}
-
-// grow-only fp32 scratch per stream for the tail slabs (allocated on first use of a size, so a
-// hipGraph capture after one eager step allocates nothing)
-inline float* tail_workspace(hipStream_t st, size_t floats) {
-  struct Buf {
-    hipStream_t st;
-    float* p;
-    size_t n;
-  };
-  static Buf bufs[8] = {};
-  for (auto& b : bufs) {
-    if (b.p && b.st == st) {
-      if (b.n >= floats) return b.p;
-      hipStreamSynchronize(st);
-      hipFree(b.p);
-      b.p = nullptr;
-      if (hipMalloc(&b.p, floats * sizeof(float)) != hipSuccess) { b.p = nullptr; return nullptr; }
-      b.n = floats;
-      return b.p;
-    }
-  }
-  for (auto& b : bufs) {
-    if (!b.p) {
-      if (hipMalloc(&b.p, floats * sizeof(float)) != hipSuccess) { b.p = nullptr; return nullptr; }
-      b.st = st;
-      b.n = floats;
-      return b.p;
-    }
-  }
-  return nullptr;
-}
-
 inline int device_cus_total() {
   static int cus = [] {
     int dev = 0, n = 0;
@@ -2076,52 +1965,13 @@ hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, 
                   int K, int splits, hipStream_t st) {
   const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
   const int ktiles = K / (F8 ? 128 : 64);
-  // Wave quantisation: one workgroup per CU, so a launch of R full rounds plus a thin last round
-  // pays a whole round for the remainder (ResNet-50 b1024 stage 4/5: 784 or 392 tiles on 256
-  // CUs = 3.06 / 1.53 rounds). Such launches run the full rounds as usual and the remaining
-  // tile rows split-K across the whole chip into fp32 slabs, then one fused-epilogue pass
-  // (tail_epilogue_kernel) finishes them. Standalone this is 5-7 % faster on those launches,
-  // but inside the ResNet step the idle CUs of the thin round are already filled by the
-  // side-stream weight gradients and the three extra launches on the main chain cost more
-  // (b1024: 79.2 -> 80.0 ms), so it is off by default: TTD_TAIL_SPLIT=1 / ttdk_set_tail_split.
-  const int tail_on = ::ttdk_rt::tail_split_flag();
+  // (Wave quantisation — a launch of R full rounds plus a thin last round on one workgroup per
+  // CU — is left to the side stream's weight gradients, which fill the idle CUs of the thin
+  // round. A split-K tail for these launches was tried in rounds 1-2: 5-7 % faster standalone,
+  // slower inside the two-stream step, and its b1024 data gradients disagreed with the plain
+  // kernel far beyond rounding (profiles/r3_tail_split_check.json: gradient cosine 0.81), so it is gone.)
   const int cus = device_cus();
   const int tiles = tm * tn;
-  const int full = tiles / cus, rem = tiles % cus;
-  if (tail_on && splits <= 1 && F8 == 0 && pe.mode == 0 && !pe.remap && full >= 1 && rem > 0 &&
-      rem * 8 <= cus * 5 && ktiles >= 12 && (full * cus) % tn == 0 && N % 4 == 0 && pe.ldo == N) {
-    const int tm_main = full * cus / tn, tm_tail = tm - tm_main;
-    const int m_base = tm_main * BM;
-    int S = cus / (tm_tail * tn);
-    if (S > ktiles / 4) S = ktiles / 4;
-    if (S > 8) S = 8;  // slab traffic grows with S; past ~8 the shorter K-slices stop paying
-    if (S >= 2) {
-      const int per = ceil_div(ktiles, S);
-      S = ceil_div(ktiles, per);
-      const long long slab = static_cast<long long>(M - m_base) * N;
-      float* ws = tail_workspace(st, static_cast<size_t>(slab) * S);
-      if (ws) {
-        hipLaunchKernelGGL((gemm256_kernel<BN, OA, OB, F8, PP>), dim3(tm_main * tn, 1), dim3(OA::THREADS), 0, st, pa, pb,
-                           pe, M, N, K, tm_main, tn, ktiles, 0);
-        EpiParams e = pe;
-        e.mode = 1;
-        e.out = ws - static_cast<long long>(m_base) * N;  // rows indexed absolutely by the kernel
-        e.ldo = N;
-        e.slab_stride = slab;
-        e.beta = 0;
-        hipLaunchKernelGGL((gemm256_kernel<BN, OA, OB, F8, PP>), dim3(tm_tail * tn, S), dim3(OA::THREADS), 0, st, pa, pb,
-                           e, M, N, K, tm_tail, tn, per, m_base);
-        // fold the slabs into slab 0 across the whole chip (the epilogue pass has only the tail's
-        // few tiles as workgroups), then the fused epilogue reads one slab
-        const long long vec = (slab + 3) / 4;
-        hipLaunchKernelGGL(splitk_fold_kernel, dim3(ceil_div(vec, 256), 1), dim3(256), 0, st, ws, S, slab, S,
-                           static_cast<float*>(nullptr), 0);
-        hipLaunchKernelGGL(tail_epilogue_kernel<BN>, dim3(tm_tail * tn), dim3(THR), 0, st, ws, 1, slab, pe, M, N, m_base,
-                           tn);
-        return hipGetLastError();
-      }
-    }
-  }
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles;
   const int per = ceil_div(ktiles, splits);

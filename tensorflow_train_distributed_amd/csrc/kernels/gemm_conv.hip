@@ -42,13 +42,8 @@ TTDK_EXPORT int ttdk_splitk_reduce(const float* ws, int splits, long long n, flo
   return splitk_reduce(ws, splits, n, out, beta, st);
 }
 
-// Runtime switch of the split-K tail for wave-quantised 256-row GEMM launches (gemm_conv.h
-// big::launch); returns the previous setting.
+// process-wide runtime switches (declared in gemm_conv.h)
 namespace ttdk_rt {
-int& tail_split_flag() {
-  static int on = getenv_int("TTD_TAIL_SPLIT", 0);
-  return on;
-}
 int& pers_flag() {
   static int on = getenv_int("TTD_BIG_PERS", 1);
   return on;
@@ -70,11 +65,6 @@ TTDK_EXPORT int ttdk_set_reserved_cus(int n) {
 // CUs the persistent kernels currently size their grids to.
 TTDK_EXPORT int ttdk_persistent_cus() { return big::device_cus(); }
 
-TTDK_EXPORT int ttdk_set_tail_split(int on) {
-  const int old = ttdk_rt::tail_split_flag();
-  ttdk_rt::tail_split_flag() = on;
-  return old;
-}
 
 // Runtime switch of the persistent register-epilogue 256-row GEMM (gemm256p_kernel); returns
 // the previous setting.

@@ -57,7 +57,6 @@ _SIGS = {
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_conv_wgrad_bn": [P, P, P, P, G, P, P, I, I, I, I, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
-    "ttdk_set_tail_split": [I],
     "ttdk_set_big_pers": [I],
     # gemm_f32.hip
     "ttdk_gemm_f32": [P, L, I, P, L, I, P, L, P, I, I, I, I, P],

@@ -325,53 +325,6 @@ def test_conv_wgrad_with_fused_bn_backward_operand(shape):
     assert torch.equal(dg1, dg2) and torch.equal(db1, db2)
 
 
-@pytest.mark.parametrize("C,K,R", [(256, 256, 3), (1024, 256, 1)])
-def test_wave_quantised_launch_split_k_tail_matches_oracle(C, K, R):
-    """272 tiles of 256 rows on 256 CUs: the 256-row GEMM runs the full round normally and the
-    last 16 tile rows split-K into fp32 slabs + the fused-epilogue tail pass (gemm_conv.h
-    `launch`). Forward with BN statistics and data gradient with the BN-backward statistics
-    epilogue + accumulate, vs fp32 convolutions."""
-    from tensorflow_train_distributed_amd.ops import _lib
-    from tensorflow_train_distributed_amd.ops import gemm as G
-    old_flag = _lib.query("ttdk_set_tail_split", 1)
-    try:
-        _tail_case(G, C, K, R)
-    finally:
-        _lib.query("ttdk_set_tail_split", old_flag)
-
-
-def _tail_case(G, C, K, R):
-    torch.manual_seed(5)
-    N, H = 272, 16
-    p = R // 2
-    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
-    w = (torch.randn(K, R, R, C, device="cuda") / (R * R * C) ** 0.5).bfloat16()
-    M = N * H * H
-    T = -(-M // 256)
-    stat = torch.empty((T, 2, K), device="cuda")
-    y = G.conv_fwd(x, w, (1, 1), (p, p), stat=stat, tile=(256, 256))
-    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=p).permute(0, 2, 3, 1)
-    assert _rel(y, ref) < 1e-2
-    yf = y.float().view(-1, K)
-    torch.testing.assert_close(stat.sum(0)[0], yf.sum(0), rtol=1e-3, atol=1e-1)
-    torch.testing.assert_close(stat.sum(0)[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
-    # data gradient (C output channels of the dgrad) with the BN-backward statistics epilogue
-    dy = torch.randn(N, H, H, K, device="cuda").bfloat16()
-    wt = w.permute(3, 1, 2, 0).contiguous()
-    yb = torch.randn(N, H, H, C, device="cuda").bfloat16()
-    keep = torch.rand(M * C, device="cuda") > 0.3
-    mask = (keep.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1).to(torch.uint8)
-    old = torch.randn(N, H, H, C, device="cuda").bfloat16()
-    out = old.clone()
-    got, partial, T2 = G.conv_dgrad(dy, wt, (N, H, H, C), (1, 1), (p, p), out=out, beta=1, bn_stat=(yb, mask))[:3]
-    dref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=p)
-    gref = (dref.permute(0, 2, 3, 1) + old.float()) * keep.view(N, H, H, C)
-    assert _rel(got, gref) < 1e-2
-    gs = got.float().view(-1, C)
-    torch.testing.assert_close(partial.sum(0)[0], gs.sum(0), rtol=1e-3, atol=1e-1)
-    torch.testing.assert_close(partial.sum(0)[1], (gs * yb.float().view(-1, C)).sum(0), rtol=1e-3, atol=1e-1)
-
-
 def test_stem_weight_gradient_kernel_matches_oracle():
     """stem_wgrad.hip: 7x7/s2/p3 weight gradient over the 3 real channels of an 8-channel
     image with dz = coef0*g + coef1*y + coef2 formed on the fly, vs fp32 torch."""
