@@ -20,9 +20,11 @@
 //   bwd_kv  : 128 keys per workgroup; loops over 64-query tiles of Q/dO (one LDS image read
 //             by rows for S, dP and by columns (ds_read_b64_tr_b16) for dV^T, dK^T); dK, dV
 //             accumulate in registers — no cross-workgroup sums.
-//   bwd_q   : 128 queries per workgroup; recomputes S, dP per key tile; dQ in registers
-//             (deterministic, no float atomics).
-//   delta   : delta = rowsum(dO * O) per (b, h, q).
+//   bwd_q   : 128 queries per workgroup; first delta = rowsum(dO * O) of its query rows (the
+//             dO fragments are already in registers; O is read once, here) — stored for
+//             bwd_kv, which runs after it; then recomputes S, dP per key tile; dQ in registers
+//             (deterministic, no float atomics). (A separate delta pass re-read O and dO:
+//             227 us per BERT-Large b128 layer, 5.5 ms per step.)
 #include "tile_common.h"
 
 namespace ttdk {
@@ -50,7 +52,7 @@ struct AttnParams {
   bf16_t* out2;  // bwd_kv: dV
   long long ld_out, ld_out2;
   float* lse;          // [B*H][S] log2 domain
-  const float* delta;  // [B*H][S]
+  float* delta;        // [B*H][S]: written by bwd_q, read by bwd_kv
   const int* seqlen;   // [B] or null
   int B, H, S;
   float scale_log2;    // log2(e) / sqrt(D)
@@ -241,37 +243,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   }
 }
 
-// ------------------------------------------------------------------------------ delta
-// delta[b*H+h][s] = sum_d dO * O ; one 8-lane group per (token, head).
-__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ o, long long ldo,
-                                                         const bf16_t* __restrict__ dout, long long lddo,
-                                                         float* __restrict__ delta, int B, int H, int S) {
-  const long long gid = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
-  const long long pair = gid >> 3;  // (token, head)
-  const int c = gid & 7;
-  const long long ntok = static_cast<long long>(B) * S;
-  const bool ok = pair < ntok * H;
-  float acc = 0.f;
-  long long tok = 0;
-  int h = 0;
-  if (ok) {
-    tok = pair / H;
-    h = static_cast<int>(pair - tok * H);
-    float a[8], d[8];
-    unpack8(ldg16(o + tok * ldo + h * D + c * 8), a);
-    unpack8(ldg16(dout + tok * lddo + h * D + c * 8), d);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += a[j] * d[j];
-  }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
-  if (ok && c == 0) {
-    const long long b = tok / S, s = tok - b * S;
-    delta[(b * H + h) * S + s] = acc;
-  }
-}
-
 // ------------------------------------------------------------------------------ bwd dK, dV
 template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
@@ -453,13 +424,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const long long row = tok0 + q0 + qb * 16 + i16;
+    float acc = 0.f;  // this lane's 16 of the row's 64 dims of dO . O
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       qf[qb][ks] = ldg_frag(P.q + row * P.ldq + h * D + ks * 32 + g * 8);
       df[qb][ks] = ldg_frag(P.dout + row * P.lddo + h * D + ks * 32 + g * 8);
+      float a[8], d[8];
+      unpack8(ldg16(P.o + row * P.ldo + h * D + ks * 32 + g * 8), a);
+      unpack8(__builtin_bit_cast(uint4, df[qb][ks]), d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += a[j] * d[j];
     }
-    lse2[qb] = P.lse[static_cast<long long>(bh) * P.S + q0 + qb * 16 + i16];
-    del[qb] = P.delta[static_cast<long long>(bh) * P.S + q0 + qb * 16 + i16];
+    // the 4 lane groups g hold the row's 4 slices
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    del[qb] = acc;
+    const long long srow = static_cast<long long>(bh) * P.S + q0 + qb * 16 + i16;
+    lse2[qb] = P.lse[srow];
+    if (g == 0) P.delta[srow] = acc;
   }
   f32x4_t dq[2][4];
 #pragma unroll
@@ -603,20 +585,18 @@ TTDK_EXPORT int ttdk_attn_bwd(const bf16_t* q, long long ldq, const bf16_t* k, l
   if (S % QBLK || (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) & 7 || !aligned16(q) || !aligned16(k) ||
       !aligned16(v) || !aligned16(o) || !aligned16(dout) || (p_drop > 0.f && !rng))
     return hipErrorInvalidValue;
-  const long long pairs = static_cast<long long>(B) * S * H;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3(static_cast<unsigned>((pairs * 8 + 255) / 256)), dim3(256), 0, st, o, ldo,
-                     dout, lddo, delta, B, H, S);
   AttnParams P = make_params(B, H, S, seqlen, p_drop, rng, site);
   P.q = q; P.k = k; P.v = v; P.o = o; P.dout = dout;
   P.ldq = ldq; P.ldk = ldk; P.ldv = ldv; P.ldo = ldo; P.lddo = lddo;
   P.lse = const_cast<float*>(lse);
   P.delta = delta;
   dim3 grid(B * H * (S / QBLK)), block(256);
-  P.out = dk; P.ld_out = lddk; P.out2 = dv; P.ld_out2 = lddv;
-  if (p_drop > 0.f) hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, block, 0, st, P);
-  else hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, block, 0, st, P);
+  // dQ first: it computes delta (rowsum dO . O) on the way and stores it for dK / dV
   P.out = dq; P.ld_out = lddq; P.out2 = nullptr;
   if (p_drop > 0.f) hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, block, 0, st, P);
   else hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, block, 0, st, P);
+  P.out = dk; P.ld_out = lddk; P.out2 = dv; P.ld_out2 = lddv;
+  if (p_drop > 0.f) hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, block, 0, st, P);
+  else hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, block, 0, st, P);
   return hipGetLastError();
 }

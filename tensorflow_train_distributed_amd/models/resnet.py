@@ -102,12 +102,14 @@ class ResNet:
         self.sampled_dgrad = os.environ.get("TTD_SAMPLED_DGRAD", "1") != "0"
         # streaming pointwise kernel (ops.gemm.pw_conv) with the neighbouring BN pass fused in as its
         # operand prologue, on the shapes where it measured faster (tools/pw_bench.py); TTD_FUSE_PW=0: off
-        self.fuse_pw = os.environ.get("TTD_FUSE_PW", "1") != "0" and precision == "bf16"
+        # (fp8 runs them too: only the 3x3 convs with >= 128 input channels take fp8 operands, and
+        # none of the fused producer / consumer pairs below is one of those)
+        self.fuse_pw = os.environ.get("TTD_FUSE_PW", "1") != "0"
         # individual switches (A/B and debugging): plain pw forward, c2->c3, c3->next c1, dgrad
         self.pw_parts = {"plain": True, "c23": True, "c31": True, "dgrad": True}
         # halo-tiled 3x3 kernel (ops.gemm.conv3_halo) for the shapes it is compiled for, with the
         # producing BN apply / BN backward fused in as its operand prologue; TTD_FUSE_C3=0: off
-        self.fuse_c3 = os.environ.get("TTD_FUSE_C3", "1") != "0" and precision == "bf16"
+        self.fuse_c3 = os.environ.get("TTD_FUSE_C3", "1") != "0"
         # halo-kernel data gradient of those convs: 2 = after the BN-backward pass, with the feeding
         # unit's BN-backward sums in its epilogue (tools/conv3_bench.py: 648 -> 529 us at b1024);
         # 1 = with the BN backward as its operand prologue (slower: 920 vs 863 us incl. the pass)
@@ -512,7 +514,7 @@ class ResNet:
         if grad_scale is None:
             grad_scale = 1.0 / N
         fp8 = self._fp8 is not None
-        if images.shape[-1] == self.in_store or (self._stem_packed_ok(tuple(images.shape)) and not fp8):
+        if images.shape[-1] == self.in_store or self._stem_packed_ok(tuple(images.shape)):
             x = images  # the dedicated stem kernels read the packed RGB (no channel-padding pass)
         else:
             x = K.pad_channels(images.contiguous(), self.in_store)
@@ -546,15 +548,16 @@ class ResNet:
             side = self._wgrad_stream
             c1 = None
             # c2 on the halo kernel: c1's BN apply + ReLU run inside c2's operand load
-            c3ok = not fp8 and self._c3_ok(blk["c2"], h.shape[1] if pend is None else pend[0].shape[1],
-                                           h.shape[2] if pend is None else pend[0].shape[2])
+            c3ok = not self._fp8_conv(blk["c2"]) and self._c3_ok(blk["c2"], h.shape[1] if pend is None else pend[0].shape[1],
+                                                                 h.shape[2] if pend is None else pend[0].shape[2])
             if pend is not None:
                 # this block's input h = relu(bn3(y3) + shortcut) is produced by c1's operand load
                 y3p, stp, resp, resbnp, ctxp = pend
                 h = torch.empty_like(y3p)
                 hm = torch.empty(h.numel() // 8, dtype=torch.uint8, device=h.device)
                 ctxp[2] = hm  # the producing unit's ReLU bits (its backward reads them)
-                o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm), defer=c3ok)
+                o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm), defer=c3ok,
+                                    want8=fp8 and not c3ok and self._fp8_conv(blk["c2"]))
                 pend = None
             if blk["cd"] is not None and side is not None:
                 # projection shortcut on the side stream, concurrent with the c1 -> c2 chain
@@ -593,7 +596,8 @@ class ResNet:
             else:
                 sc, cd = h, None
             sc_bn = (cd[3].scale, cd[3].shift) if cd is not None and self.fuse_proj else None
-            defer3 = nxt is not None and not fp8 and self._pw_part("c31") and self._pw_fwd_ok(nxt["c1"], True)
+            defer3 = (nxt is not None and self._pw_part("c31") and self._pw_fwd_ok(nxt["c1"], True)
+                      and not self._fp8_conv(nxt["c1"]))
             c3_in = y2 if fuse23 else o2
             c3_pro = (c2[3].scale, c2[3].shift, None, None, o2, c2[2]) if fuse23 else None
             if defer3:
