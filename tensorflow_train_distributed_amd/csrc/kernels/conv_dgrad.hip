@@ -65,6 +65,40 @@ TTDK_EXPORT int ttdk_conv_dgrad(const bf16_t* dy, const bf16_t* wt, const TtdkCo
   return dispatch<KConvDgrad, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
 }
 
+// Pointwise (1x1, stride 1) data gradient whose operand is the BN backward of the unit's output
+// gradient, formed in the 256-row kernel's LDS (EpiParams::py / pcoef / pdz):
+//   dz = coef[0][k]*g + coef[1][k]*y + coef[2][k]  (g: the masked output gradient, y: the unit's conv output)
+//   dx = dz . W  (+ the usual epilogue: accumulate, feeding-BN statistics)
+// dz is also stored (by the workgroups of tile column 0) for the weight gradient. Returns
+// hipErrorNotSupported when the shape is not on the 256-row kernel (the caller keeps the pass).
+TTDK_EXPORT int ttdk_conv_dgrad_bnpro(const bf16_t* g_in, const bf16_t* wt, const TtdkConv* g, const bf16_t* y,
+                                      const float* coef, bf16_t* dz, const TtdkEpilogue* epi, hipStream_t st) {
+  if (!(g->R == 1 && g->S == 1 && g->ph == 0 && g->pw == 0 && g->sh == 1 && g->sw == 1)) return hipErrorNotSupported;
+  EpiParams pe = to_epi(epi);
+  if (pe.by && (pe.stat == nullptr || pe.mode != 0 || g->C % 8 || pe.ldo % 8 || pe.residual || pe.act))
+    return hipErrorInvalidValue;
+  if ((pe.by2 || pe.stat2) && !(pe.by && pe.by2 && pe.stat2)) return hipErrorInvalidValue;
+  const int N = g->C, K = g->K;
+  const int M = g->N * g->P * g->Q;
+  const int bbn = big_bn(M, N, K);
+  if (!bbn || K % 64 || pe.mode != 0 || pe.remap) return hipErrorNotSupported;
+  pe.py = y;
+  pe.pcoef = coef;
+  pe.pdz = dz;
+  pe.pld = K;
+  const big::DenseP pa{g_in, K, M}, pb{wt, K, N};
+  if (bbn == 256)
+    return big::launch<256, big::OpDenseKBN<128, 2>, big::OpDenseK<128, 2>, 0, 0>(pa, pb, pe, M, N, K, 1, st);
+  return big::launch<128, big::OpDenseKBN<128, 2>, big::OpDenseK<64, 2>, 0, 0>(pa, pb, pe, M, N, K, 1, st);
+}
+
+// Whether ttdk_conv_dgrad_bnpro runs this shape (its BN statistics rows are 256-row tiles).
+TTDK_EXPORT int ttdk_conv_dgrad_bnpro_ok(const TtdkConv* g) {
+  const int M = g->N * g->P * g->Q;
+  return g->R == 1 && g->S == 1 && g->ph == 0 && g->pw == 0 && g->sh == 1 && g->sw == 1 && g->K % 64 == 0 &&
+         big_bn(M, g->C, g->K) != 0;
+}
+
 // ---- strided dgrad by sub-pixel (phase) decomposition
 // For stride s, the input pixels h = s*i + a of one phase a only receive taps r ≡ (a + ph)
 // (mod s), so dx restricted to that phase is a UNIT-stride dgrad over dy with the tap subset

@@ -530,6 +530,16 @@ struct EpiParams {
   // pixels it samples), so the accumulated tensor needs no zero fill. 0 = every row.
   int bH, bW;
   int feed_pf;  // 256-row kernel: prefetched feeding-BN epilogue allowed (TTD_FEED_PREFETCH, default 1)
+  // BN-backward operand prologue of the 256-row kernel (OpDenseKBN A operand, 1x1 dgrads): the A
+  // tile read by DMA is the unit's masked output gradient g; in LDS it becomes
+  // dz = a[k]*g + b[k]*py + c[k] (pcoef = [3][K] a | b | c, py = the unit's conv output, row
+  // stride pld) before any fragment is read, and the workgroups of tile column 0 store dz to pdz
+  // (the weight gradient's operand): the separate BN backward-apply pass and this GEMM's
+  // re-read of its output disappear.
+  const bf16_t* py;
+  const float* pcoef;
+  bf16_t* pdz;
+  long long pld;
 };
 
 __device__ __forceinline__ bool beta_row(const EpiParams& E, int m) {
@@ -1229,17 +1239,29 @@ struct OpWgradMN {
   }
 };
 
+// dense K-major A operand whose tile gets the BN-backward prologue (EpiParams::py/pcoef/pdz)
+template <int HROWS, int ESZ, int T = THR>
+struct OpDenseKBN : OpDenseK<HROWS, ESZ, T> {};
+
 template <class OP>
 struct Traits {
   static constexpr bool kmaj = true;
+  static constexpr bool bnpro = false;
+};
+template <int HR, int E, int T>
+struct Traits<OpDenseKBN<HR, E, T>> {
+  static constexpr bool kmaj = true;
+  static constexpr bool bnpro = true;
 };
 template <int HR, int T>
 struct Traits<OpDenseMN<HR, T>> {
   static constexpr bool kmaj = false;
+  static constexpr bool bnpro = false;
 };
 template <int HR, int T>
 struct Traits<OpWgradMN<HR, T>> {
   static constexpr bool kmaj = false;
+  static constexpr bool bnpro = false;
 };
 
 // fragment readers
@@ -1368,7 +1390,8 @@ struct Geo {
   static constexpr int STAGE = 2 * AH + 2 * BH;
   static constexpr int PITCH = BN * 2 + 16;
   static constexpr int EPI = BM * PITCH + 8 * 3 * BN * 4;  // staged tile + [8 waves][3][BN] statistics
-  static constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  static constexpr int COEF = 2 * STAGE;  // BN prologue: [2 stages][64 lanes x 16 B] ([3][64] fp32 used)
+  static constexpr int SMEM = (2 * STAGE + 2048 > EPI) ? 2 * STAGE + 2048 : EPI;
 };
 
 // F8: 0 = bf16, 1 = fp8 e4m3 x e4m3, 2 = e5m2 (A) x e4m3 (B)  (dgrad: gradients in e5m2)
@@ -1531,14 +1554,74 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     }
     if (kt0 < kt1 && !lag) barrier();
   } else {
+  // BN-backward operand prologue (OpDenseKBN): every thread's A pieces of a K-tile are the same
+  // logical 16-B k-chunk (8 channels) of 4 rows; their y values are loaded into registers one
+  // K-tile ahead (before that tile's remaining DMAs, so the counted waits retire them too), the
+  // tile's 3 x 64 coefficients are DMA'd next to the operand stages, and once the tile has landed
+  // each thread rewrites its own pieces in LDS (one extra barrier per K-tile).
+  constexpr bool BNP = Traits<OA>::bnpro;
+  static_assert(!BNP || (PP == 0 && F8 == 0 && T == THR && GA == 2), "BN prologue: bf16 two-barrier 512-thread path");
+  uint4 yv[2][GA];
+  const int pchunk = (tid & 7) ^ ((tid >> 4) & 7);
+  auto prow = [&](int h, int i) { return m0 + h * 128 + ((i * T + tid) >> 3); };
+  auto load_y = [&](int kt) {
+    if constexpr (BNP) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+          const int r = min(prow(h, i), M - 1);
+          yv[h][i] = *reinterpret_cast<const uint4*>(E.py + static_cast<long long>(r) * E.pld + kt * 64 + pchunk * 8);
+        }
+    }
+  };
+  auto issue_coef = [&](int kt) {
+    if constexpr (BNP) {
+      const float* src = lane < 48 ? E.pcoef + static_cast<long long>(lane >> 4) * K + kt * 64 + (lane & 15) * 4
+                                   : reinterpret_cast<const float*>(g_zero);
+      glds(src, smem + Gm::COEF + ((kt - kt0) & 1) * 1024);
+    }
+  };
+  auto transform = [&](int kt, char* b) {
+    if constexpr (BNP) {
+      const float* cf = reinterpret_cast<const float*>(smem + Gm::COEF + ((kt - kt0) & 1) * 1024) + pchunk * 8;
+      float ca[8], cbv[8], cc[8];
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        *reinterpret_cast<f32x4_t*>(ca + j) = *reinterpret_cast<const f32x4_t*>(cf + j);
+        *reinterpret_cast<f32x4_t*>(cbv + j) = *reinterpret_cast<const f32x4_t*>(cf + 64 + j);
+        *reinterpret_cast<f32x4_t*>(cc + j) = *reinterpret_cast<const f32x4_t*>(cf + 128 + j);
+      }
+      const bool store = tile_n == 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+          uint4* q = reinterpret_cast<uint4*>(b + (h ? A1 : A0) + (i * T + tid) * 16);
+          float gv[8], yf[8];
+          unpack8(*q, gv);
+          unpack8(yv[h][i], yf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gv[j] = ca[j] * gv[j] + cbv[j] * yf[j] + cc[j];  // = bwd_apply_kernel
+          const uint4 o = pack8(gv);
+          *q = o;
+          const int r = prow(h, i);
+          if (store && r < M)
+            *reinterpret_cast<uint4*>(E.pdz + static_cast<long long>(r) * E.pld + kt * 64 + pchunk * 8) = o;
+        }
+    }
+  };
   if (kt0 < kt1) {
     char* b0 = buf(kt0);
+    load_y(kt0);
+    issue_coef(kt0);
     la.template issue<0>(b0 + A0, kt0, wave);
     lb.template issue<1>(b0 + B1, kt0, wave);
     la.template issue<1>(b0 + A1, kt0, wave);
     lb.template issue<0>(b0 + B0, kt0, wave);
     if (kt0 + 1 < kt1) {
       char* b1 = buf(kt0 + 1);
+      issue_coef(kt0 + 1);
       la.template issue<0>(b1 + A0, kt0 + 1, wave);
       lb.template issue<1>(b1 + B1, kt0 + 1, wave);
       wait_vm<GA + GB>();
@@ -1546,6 +1629,10 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
       wait_vm<0>();
     }
     barrier();
+    if constexpr (BNP) {
+      transform(kt0, b0);
+      barrier();
+    }
     read_a(b0 + A0, fa[0]);
     read_b(b0 + B0, fb[0]);
   }
@@ -1553,7 +1640,10 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     const bool has1 = kt + 1 < kt1, has2 = kt + 2 < kt1;
     char* cb = buf(kt);
     // q0: (A0, B0)
-    if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
+    if (has1) {
+      load_y(kt + 1);
+      la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
+    }
     mma(fa[0], fb[0], acc[0][0]);
     read_b(cb + B1, fb[1]);
     // q1: (A0, B1)
@@ -1562,7 +1652,10 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     read_a(cb + A1, fa[1]);
     // q2: (A1, B1)
     barrier();
-    if (has2) la.template issue<0>(cb + A0, kt + 2, wave);
+    if (has2) {
+      issue_coef(kt + 2);
+      la.template issue<0>(cb + A0, kt + 2, wave);
+    }
     mma(fa[1], fb[1], acc[1][1]);
     // q3: (A1, B0); retire tile kt+1 ((kt+2).A0 may stay in flight), prefetch its A0/B0
     if (has1) {
@@ -1571,6 +1664,14 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     barrier();
     if (has2) lb.template issue<1>(cb + B1, kt + 2, wave);
     mma(fa[1], fb[0], acc[1][0]);
+    if constexpr (BNP) {
+      // after the last MFMA of the tile: the fragment registers are dead here (no spills at
+      // BN = 256), and the VALU work still overlaps the MFMAs in flight
+      if (has1) {
+        transform(kt + 1, buf(kt + 1));
+        barrier();
+      }
+    }
     if (has1) {
       char* nb = buf(kt + 1);
       read_a(nb + A0, fa[0]);
@@ -2161,6 +2262,10 @@ inline EpiParams to_epi(const TtdkEpilogue* e) {
   p.stat2 = e->stat2;
   p.bH = e->bH;
   p.bW = e->bW;
+  p.py = nullptr;
+  p.pcoef = nullptr;
+  p.pdz = nullptr;
+  p.pld = 0;
   return p;
 }
 

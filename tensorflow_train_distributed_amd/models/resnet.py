@@ -114,6 +114,10 @@ class ResNet:
         # unit's BN-backward sums in its epilogue (tools/conv3_bench.py: 648 -> 529 us at b1024);
         # 1 = with the BN backward as its operand prologue (slower: 920 vs 863 us incl. the pass)
         self.c3_dgrad = int(os.environ.get("TTD_C3_DGRAD", "2"))
+        # 1x1 data gradients on the 256-row kernel form the unit's BN backward (dz = a*g + b*y + c)
+        # in LDS as their operand and store dz for the weight gradient: no separate backward-apply
+        # pass, no re-read of dz (ops.gemm.conv_dgrad(bn_pro=...)); TTD_DGRAD_BNPRO=0: off
+        self.bn_pro = os.environ.get("TTD_DGRAD_BNPRO", "1") != "0"
         # stem weight gradient on its dedicated kernel (3 real input channels, BN backward on the fly)
         self.stem_kernel = os.environ.get("TTD_STEM_WGRAD", "1") != "0"
         # dedicated stem forward kernel (stem_fwd.hip: K = 7 x 32 over the 3 real channels)
@@ -423,6 +427,33 @@ class ResNet:
                                            bn_stat=(fy, fmask))
             self._wgrad(c, x, dz, wname)
             return out, (partial, T)
+        stride, pad = (c.stride, c.stride), (c.pad, c.pad)
+        if (need_dx and dstat is not None and self.fuse_bn_bwd and self.bn_pro and not wgrad_last and not sampled_only
+                and self.device.type == "cuda"
+                and G.dgrad_bnpro_ok(tuple(x.shape), (c.cin_store, c.k, c.k, Kc), stride, pad)):
+            # BN backward formed inside the data gradient's operand tile (dz stored there once for
+            # the weight gradient, which therefore starts after this launch)
+            coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
+                                      dstat[0], dstat[1])
+            dz = torch.empty_like(y)
+            wt = K.krsc_to_crsk(P.c[wname])
+            bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
+            pro = (y, coef, dz)
+            if feeds is not None and G.dgrad_stat_rows(tuple(x.shape), tuple(wt.shape), stride, pad) is not None:
+                _, fy, fmask, _ = feeds
+                if feeds2 is not None:
+                    out, partial, T, partial2 = G.conv_dgrad(dout, wt, x.shape, stride, pad, out=dx, beta=dx_beta,
+                                                             bn_stat=(fy, fmask), bn_stat2=feeds2[1], beta_s2=bs2,
+                                                             bn_pro=pro)
+                    self._wgrad(c, x, dz, wname)
+                    return out, (partial, T, partial2)
+                out, partial, T = G.conv_dgrad(dout, wt, x.shape, stride, pad, out=dx, beta=dx_beta,
+                                               bn_stat=(fy, fmask), beta_s2=bs2, bn_pro=pro)
+                self._wgrad(c, x, dz, wname)
+                return out, (partial, T)
+            out = G.conv_dgrad(dout, wt, x.shape, stride, pad, out=dx, beta=dx_beta, beta_s2=bs2, bn_pro=pro)
+            self._wgrad(c, x, dz, wname)
+            return out, None
         if dstat is not None:
             dz = K.bn_backward_from_partial(dout.view(M, Kc), y.view(M, Kc), P.var[pre + "gamma"], st,
                                             P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1]).view(N, Pp, Q, Kc)
@@ -435,7 +466,6 @@ class ResNet:
         if not need_dx:
             return None, None
         wt = K.krsc_to_crsk(P.c[wname])
-        stride, pad = (c.stride, c.stride), (c.pad, c.pad)
         bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
         if (feeds is not None and feeds2 is None and dx is None and self.fuse_bn_bwd and self.c3_dgrad == 2
                 and self._c3_ok(c, x.shape[1], x.shape[2])):

@@ -430,8 +430,32 @@ def dgrad_stat_tile(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
     return bm, bn, -(-M // bm)
 
 
+def _bnpro_call(dy, wt, g, bn_pro, e):
+    y, coef, dz = bn_pro
+    C, R, S, K = wt.shape
+    if not _lib.fn("ttdk_conv_dgrad_bnpro_ok")(ctypes.byref(g)):
+        raise ValueError("conv_dgrad: the BN-backward operand prologue needs a 1x1 unit-stride dgrad on the 256-row "
+                         "kernel")
+    _check(y, torch.bfloat16, "bn_pro y")
+    _check(dz, torch.bfloat16, "bn_pro dz")
+    if tuple(y.shape) != tuple(dy.shape) or tuple(dz.shape) != tuple(dy.shape) or coef.dtype != torch.float32 \
+            or coef.numel() != 3 * K or not coef.is_contiguous():
+        raise ValueError("conv_dgrad: bn_pro operands must match dy ([..., K]) and coef [3, K] fp32")
+    _log("dgrad_bnpro_1x1", g.N * g.H * g.W, C, K)
+    _lib.call("ttdk_conv_dgrad_bnpro", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), y.data_ptr(), coef.data_ptr(),
+              dz.data_ptr(), ctypes.byref(e), _lib.stream())
+
+
+def dgrad_bnpro_ok(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
+    """Whether conv_dgrad(bn_pro=...) runs: a 1x1 unit-stride data gradient on the 256-row
+    kernel (K % 64 == 0)."""
+    C, R, S, K = wt_shape
+    g = conv_geom(tuple(x_shape), (K, R, S, C), stride, padding)
+    return bool(_lib.fn("ttdk_conv_dgrad_bnpro_ok")(ctypes.byref(g)))
+
+
 def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
-               tile=(0, 0), bn_stat=None, bn_stat2=None, sampled_only=False, beta_s2=None):
+               tile=(0, 0), bn_stat=None, bn_stat2=None, sampled_only=False, beta_s2=None, bn_pro=None):
     """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
 
     For strided 1x1 convs only the sampled pixels are written: pass a zero-initialised `out`
@@ -484,6 +508,8 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
             ws = torch.empty_like(wt)
             _lib.call("ttdk_conv_dgrad_subpixel", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), ws.data_ptr(),
                       ctypes.byref(e), _lib.stream())
+        elif bn_pro is not None:
+            _bnpro_call(dy, wt, g, bn_pro, e)
         else:
             bm, bn, _ = dgrad_stat_tile(tuple(x_shape), tuple(wt.shape))
             _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * g.H * g.W, C, R * S * K)
@@ -491,6 +517,9 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
                       _lib.stream())
         return (out, partial, T) if partial2 is None else (out, partial, T, partial2)
     e = _epi(out, ldo=C, beta=beta, residual=residual, beta_s2=beta_s2 if beta else None)
+    if bn_pro is not None:
+        _bnpro_call(dy, wt, g, bn_pro, e)
+        return out
     if _subpixel_ok(g, R, S, stride, padding) and residual is None and tile == (0, 0):
         # strided dgrad as s*s unit-stride phase GEMMs (skips the zero taps of the direct gather)
         if _LOG is not None:  # one GEMM per phase, in ttdk_conv_dgrad_subpixel's launch order

@@ -482,3 +482,53 @@ def test_pipelined_feeding_bn_epilogue_vs_fp32_conv(cfg):
     assert _rel(sums[1], (gs * yf).sum(0)) < 2e-2
     # ... and exactly consistent with the gradient it stored
     torch.testing.assert_close(sums[1], (got.float().view(-1, C) * yf).sum(0), rtol=2e-3, atol=5e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [
+    # (N, H, K = dz channels, C = dx channels, feed): ResNet-50 1x1 dgrads at per-image stage shapes —
+    # c3 (4*mid -> mid, BN = 128 / 256 tiles) and c1 (mid -> 4*mid, accumulate + feeding-BN epilogue)
+    (32, 28, 512, 128, False),
+    (64, 14, 1024, 256, False),
+    (16, 28, 128, 512, True),
+    (48, 14, 256, 1024, True),
+    (17, 17, 256, 256, True),  # ragged M (4913 rows): clamped operand rows, partial last tile
+])
+def test_dgrad_with_bn_backward_operand_prologue(cfg):
+    """conv_dgrad(bn_pro=...): the 1x1 data gradient whose A operand is the BN backward of the
+    unit's masked output gradient, formed in LDS (dz = a*g + b*y + c), stored once for the weight
+    gradient — vs an fp32 oracle: torch BN-backward formula + torch.nn.grad.conv2d_input."""
+    from torch.nn.grad import conv2d_input
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    N, H, K, C, feed = cfg
+    torch.manual_seed(7)
+    M = N * H * H
+    g = torch.randn(N, H, H, K, device="cuda").bfloat16()       # masked output gradient of the unit
+    y = torch.randn(N, H, H, K, device="cuda").bfloat16()       # the unit's conv output (BN input)
+    coef = torch.randn(3, K, device="cuda") * torch.tensor([[1.0], [0.1], [0.01]], device="cuda")
+    w = (torch.randn(K, 1, 1, C, device="cuda") / K ** 0.5).bfloat16()
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    assert G.dgrad_bnpro_ok((N, H, H, C), tuple(wt.shape))
+    dz_ref = coef[0] * g.float() + coef[1] * y.float() + coef[2]
+    dx_ref = conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), dz_ref.bfloat16().float().permute(0, 3, 1, 2)
+                          ).permute(0, 2, 3, 1)
+    dz = torch.empty_like(g)
+    if feed:
+        fy = torch.randn(N, H, H, C, device="cuda").bfloat16()
+        keep = torch.rand(M * C, device="cuda") > 0.4
+        bits = keep.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)
+        mask = bits.sum(1).to(torch.uint8)
+        old = torch.randn(N, H, H, C, device="cuda").bfloat16()
+        out = old.clone()
+        got, partial, T = G.conv_dgrad(g, wt, (N, H, H, C), out=out, beta=1, bn_stat=(fy, mask), bn_pro=(y, coef, dz))
+        ref = (dx_ref + old.float()) * keep.view(N, H, H, C)
+        assert _rel(got, ref) < 1e-2
+        sums = partial.sum(0)
+        gs = got.float().view(-1, C)
+        torch.testing.assert_close(sums[0], gs.sum(0), rtol=2e-3, atol=5e-2)
+        torch.testing.assert_close(sums[1], (gs * fy.float().view(-1, C)).sum(0), rtol=2e-3, atol=5e-2)
+    else:
+        got = G.conv_dgrad(g, wt, (N, H, H, C), bn_pro=(y, coef, dz))
+        assert _rel(got, dx_ref) < 1e-2
+    # dz stored once for the weight gradient: every element, bf16 of the same expression
+    assert _rel(dz, dz_ref) < 4e-3
