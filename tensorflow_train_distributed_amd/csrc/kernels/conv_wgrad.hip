@@ -29,6 +29,18 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
   }
   DenseParams pa{dy, g->K, M, K};
   hipError_t e;
+  bool folded = false;
+  if (bbn && splits > 1 && big::inkernel_fold()) {
+    // the 256-row kernel folds its own slabs (the last split of each tile sums them into dw)
+    int* ctr = big::tile_counters(st, ceil_div(M, big::BM) * ceil_div(N, bbn));
+    if (ctr) {
+      pe.mode = 3;
+      pe.kout = dw;
+      pe.kctr = ctr;
+      pe.beta = beta;
+      folded = true;
+    }
+  }
   if (bbn && is_pointwise(g)) {
     e = bbn == 256 ? big::dense<256>(dy, g->K, false, x, g->C, false, pe, M, N, K, splits, st)
                    : big::dense<128>(dy, g->K, false, x, g->C, false, pe, M, N, K, splits, st);
@@ -44,7 +56,7 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
     GatherParams pb{x, g->H, g->W, g->C, g->P, g->Q, g->R, g->S, g->sh, g->sw, g->ph, g->pw, g->dh, g->dw, N, K};
     e = dispatch<MNDense, MNConvGather>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
   }
-  if (e != hipSuccess || splits == 1) return e;
+  if (e != hipSuccess || splits == 1 || folded) return e;
   return splitk_reduce(ws, splits, static_cast<long long>(M) * N, dw, beta, st);
 }
 

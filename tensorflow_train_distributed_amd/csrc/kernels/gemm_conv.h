@@ -37,6 +37,7 @@
 namespace ttdk_rt {
 int& pers_flag();
 int& reserved_cus();
+int& fold_flag();
 }
 
 namespace ttdk {
@@ -540,6 +541,12 @@ struct EpiParams {
   const float* pcoef;
   bf16_t* pdz;
   long long pld;
+  // mode 3 (256-row kernel): split-K with the fold inside the launch. Every split writes its fp32
+  // slab as in mode 1; the workgroup that finishes a tile last (per-tile arrival counter kctr,
+  // reset by that workgroup) sums the tile's slabs in split order and writes kout (+= with beta):
+  // no separate fold launch re-reading every slab over the whole chip.
+  float* kout;
+  int* kctr;
 };
 
 __device__ __forceinline__ bool beta_row(const EpiParams& E, int m) {
@@ -1686,7 +1693,7 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   const int g = lane >> 4, i16 = lane & 15;
   const float alpha_e = epi_alpha(E);
   if (E.mode != 0) {
-    float* out = static_cast<float*>(E.out) + (E.mode == 1 ? blockIdx.y * E.slab_stride : 0);
+    float* out = static_cast<float*>(E.out) + (E.mode == 1 || E.mode == 3 ? blockIdx.y * E.slab_stride : 0);
 #pragma unroll
     for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
@@ -1701,15 +1708,48 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
             f32x4_t v = acc[ha][hb][a][b] * alpha_e;
             float* o = out + out_row(E, m) * E.ldo + n;
             if (n + 3 < N && (E.ldo & 3) == 0) {
-              if (E.beta) v += *reinterpret_cast<const f32x4_t*>(o);
+              if (E.beta && E.mode == 2) v += *reinterpret_cast<const f32x4_t*>(o);
               *reinterpret_cast<f32x4_t*>(o) = v;
             } else {
 #pragma unroll
               for (int j = 0; j < 4; ++j)
-                if (n + j < N) o[j] = v[j] + (E.beta ? o[j] : 0.f);
+                if (n + j < N) o[j] = v[j] + (E.beta && E.mode == 2 ? o[j] : 0.f);
             }
           }
       }
+    if (E.mode == 3) {
+      // release this split's slab (device scope: other XCDs' L2s must see it), count arrivals
+      __threadfence();
+      __syncthreads();
+      __shared__ int last_split;
+      if (tid == 0) last_split = atomicAdd(E.kctr + t, 1) == static_cast<int>(gridDim.y) - 1;
+      __syncthreads();
+      if (last_split) {
+        __threadfence();  // acquire: the other splits' slabs
+        const float* ws = static_cast<const float*>(E.out);
+        const int S = gridDim.y;
+        float* ko = E.kout;
+        for (int q = tid; q < BM * (BN / 4); q += T) {
+          const int r = q / (BN / 4), c4 = q - r * (BN / 4);
+          const int m = m0 + r, n = n0 + c4 * 4;
+          if (m >= M || n >= N) continue;
+          const long long o = static_cast<long long>(m) * E.ldo + n;
+          if (n + 3 < N && (E.ldo & 3) == 0) {
+            f32x4_t v = *reinterpret_cast<const f32x4_t*>(ws + o);
+            for (int sp = 1; sp < S; ++sp) v += *reinterpret_cast<const f32x4_t*>(ws + sp * E.slab_stride + o);
+            if (E.beta) v += *reinterpret_cast<const f32x4_t*>(ko + o);
+            *reinterpret_cast<f32x4_t*>(ko + o) = v;
+          } else {
+            for (int jj = 0; jj < 4 && n + jj < N; ++jj) {
+              float v = ws[o + jj];
+              for (int sp = 1; sp < S; ++sp) v += ws[sp * E.slab_stride + o + jj];
+              ko[o + jj] = v + (E.beta ? ko[o + jj] : 0.f);
+            }
+          }
+        }
+        if (tid == 0) E.kctr[t] = 0;  // ready for the next launch on this counter block
+      }
+    }
     return;
   }
   constexpr int PITCH = Gm::PITCH;
@@ -2039,6 +2079,39 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
   }
 }
 
+// Per-stream arrival counters of the in-kernel split-K fold (EpiParams mode 3): zeroed once at
+// allocation, every launch leaves them zero again (the last workgroup of a tile resets its
+// counter). Allocated on first use (an eager warm-up step precedes any hipGraph capture).
+// Returns nullptr when more than kMaxCtr tiles are asked for (the caller keeps the fold kernel).
+constexpr int kMaxCtr = 1 << 16;
+inline int* tile_counters(hipStream_t st, int tiles) {
+  if (tiles > kMaxCtr) return nullptr;
+  struct Buf {
+    hipStream_t st;
+    int* p;
+  };
+  static Buf bufs[16] = {};
+  for (auto& b : bufs)
+    if (b.p && b.st == st) return b.p;
+  for (auto& b : bufs) {
+    if (!b.p) {
+      if (hipMalloc(&b.p, kMaxCtr * sizeof(int)) != hipSuccess) return b.p = nullptr, nullptr;
+      if (hipMemsetAsync(b.p, 0, kMaxCtr * sizeof(int), st) != hipSuccess) return nullptr;
+      b.st = st;
+      return b.p;
+    }
+  }
+  return nullptr;
+}
+
+// In-kernel split-K fold (TTD_SPLITK_FOLD_INKERNEL=1; off by default). Measured slower in both
+// steps (ResNet-50 b1024 73.0 -> 82.7 ms, BERT-Large b128 187.1 -> 195.8 ms): the device-scope
+// release of every split writes back its XCD's whole L2 (cross-XCD visibility of the slab),
+// which the concurrent main-chain kernels pay for, and a tile's last split sums up to
+// hundreds of slabs alone (ResNet's few-tile weight gradients) where the fold pass spreads
+// that work over the chip.
+inline bool inkernel_fold() { return ::ttdk_rt::fold_flag() != 0; }
+
 inline int device_cus_total() {
   static int cus = [] {
     int dev = 0, n = 0;
@@ -2266,6 +2339,8 @@ inline EpiParams to_epi(const TtdkEpilogue* e) {
   p.pcoef = nullptr;
   p.pdz = nullptr;
   p.pld = 0;
+  p.kout = nullptr;
+  p.kctr = nullptr;
   return p;
 }
 

@@ -38,6 +38,40 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
   return dispatch<MNDenseS, MNDenseS>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
 }
 
+// Split-K GEMM into an fp32 output: C (+)= alpha * A.B over `splits` K-slices with fp32 slabs in
+// `ws` [splits][M][N]. On the 256-row kernel the launch folds its own slabs (EpiParams mode 3);
+// elsewhere a fold pass follows.
+TTDK_EXPORT int ttdk_gemm_bf16_splitk(const bf16_t* A, long long lda, int a_kmajor, const bf16_t* B, long long ldb,
+                                      int b_kmajor, int M, int N, int K, int splits, float* ws, float* out, int beta,
+                                      float alpha, hipStream_t st) {
+  TtdkEpilogue te{};
+  te.mode = 1;
+  te.out = ws;
+  te.ldo = N;
+  te.slab_stride = static_cast<long long>(M) * N;
+  te.alpha = alpha;
+  EpiParams pe = to_epi(&te);
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool vec = al(A) && al(B) && lda % 8 == 0 && ldb % 8 == 0 && (a_kmajor ? K % 8 == 0 : M % 8 == 0) &&
+                   (b_kmajor ? K % 8 == 0 : N % 8 == 0);
+  const int bbn = big_bn(M, N, K);
+  const int ktiles = K / 64;
+  if (splits > 1 && vec && bbn && (a_kmajor || M % 8 == 0) && big::inkernel_fold() && ktiles >= splits) {
+    int* ctr = big::tile_counters(st, ceil_div(M, big::BM) * ceil_div(N, bbn));
+    if (ctr) {
+      pe.mode = 3;
+      pe.kout = out;
+      pe.kctr = ctr;
+      pe.beta = beta;
+      return bbn == 256 ? big::dense<256>(A, lda, a_kmajor, B, ldb, b_kmajor, pe, M, N, K, splits, st)
+                        : big::dense<128>(A, lda, a_kmajor, B, ldb, b_kmajor, pe, M, N, K, splits, st);
+    }
+  }
+  const int rc = ttdk_gemm_bf16(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, splits, 0, 0, &te, st);
+  if (rc != hipSuccess) return rc;
+  return splitk_reduce(ws, splits, static_cast<long long>(M) * N, out, beta, st);
+}
+
 TTDK_EXPORT int ttdk_splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {
   return splitk_reduce(ws, splits, n, out, beta, st);
 }
@@ -52,7 +86,19 @@ int& reserved_cus() {
   static int n = getenv_int("TTD_RESERVED_CUS", 0);
   return n;
 }
+int& fold_flag() {
+  static int on = getenv_int("TTD_SPLITK_FOLD_INKERNEL", 0);
+  return on;
+}
 }  // namespace ttdk_rt
+
+// Runtime switch of the in-kernel split-K fold (gemm_conv.h inkernel_fold); returns the previous
+// setting.
+TTDK_EXPORT int ttdk_set_inkernel_fold(int on) {
+  const int old = ttdk_rt::fold_flag();
+  ttdk_rt::fold_flag() = on;
+  return old;
+}
 
 // CUs kept free of persistent grids for the collective engine's CTAs (see device_cus in
 // gemm_conv.h); returns the previous setting.

@@ -256,6 +256,15 @@ class ResNet:
     # stage-2 c3 (256 -> 64) and c1 (64 -> 256, accumulating into the shortcut gradient)
     PW_DGRAD_SHAPES = {(256, 64), (64, 256)}
 
+    # 1x1 dgrads with the BN backward as LDS operand prologue where it measured faster than the
+    # backward-apply pass + plain dgrad (tools/dgrad_bnpro_bench.py, b1024,
+    # profiles/r3_dgrad_bnpro_ab_b1024.txt): stage-3/4 c3 (dz 512 / 1024 ch -> 128 / 256: 1.30x /
+    # 1.06x) and the stage-3 c1s (-> 256 / 512 ch: 1.08x / 1.03x). Wider outputs recompute the
+    # operand per column tile (stage-4/5 c1: 0.88x / 0.81x) and 32-K-tile loops lose the
+    # ping-pong schedule (stage-5 c3: 0.81x): those keep the pass.
+    BNPRO_MAX_K = 1024
+    BNPRO_MAX_N = 512
+
     def _pw_dgrad_ok(self, c: ConvSpec) -> bool:
         from ..ops import gemm as G
         return (self.fuse_pw and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0
@@ -429,7 +438,7 @@ class ResNet:
             return out, (partial, T)
         stride, pad = (c.stride, c.stride), (c.pad, c.pad)
         if (need_dx and dstat is not None and self.fuse_bn_bwd and self.bn_pro and not wgrad_last and not sampled_only
-                and self.device.type == "cuda"
+                and self.device.type == "cuda" and Kc <= self.BNPRO_MAX_K and c.cin_store <= self.BNPRO_MAX_N
                 and G.dgrad_bnpro_ok(tuple(x.shape), (c.cin_store, c.k, c.k, Kc), stride, pad)):
             # BN backward formed inside the data gradient's operand tile (dz stored there once for
             # the weight gradient, which therefore starts after this launch)

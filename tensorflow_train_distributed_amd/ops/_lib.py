@@ -50,10 +50,12 @@ G = ctypes.POINTER(ConvGeom)
 _SIGS = {
     # gemm_conv.hip
     "ttdk_gemm_bf16": [P, L, I, P, L, I, I, I, I, I, I, I, E, P],
+    "ttdk_gemm_bf16_splitk": [P, L, I, P, L, I, I, I, I, I, P, P, I, F, P],
     "ttdk_conv_fwd": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad_bnpro": [P, P, G, P, P, P, E, P],
     "ttdk_conv_dgrad_bnpro_ok": [G],
+    "ttdk_set_inkernel_fold": [I],
     "ttdk_conv_dgrad_subpixel": [P, P, G, P, E, P],
     "ttdk_conv_dgrad_subpixel_stat_rows": [G],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],

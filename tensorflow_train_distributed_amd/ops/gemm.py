@@ -135,13 +135,12 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     if out.dtype == torch.float32:
         splits = effective_splits(K, splits)
         if splits > 1:
-            ws = torch.empty((splits, M, N), dtype=torch.float32, device=a.device)
-            e = _epi(ws, mode=1, ldo=N, slab_stride=M * N, alpha=alpha)
-            _lib.call("ttdk_gemm_bf16", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K,
-                      splits, tile[0], tile[1], ctypes.byref(e), _lib.stream())
             if not out.is_contiguous():
                 raise ValueError("split-K output must be contiguous")
-            _lib.call("ttdk_splitk_reduce", ws.data_ptr(), splits, M * N, out.data_ptr(), beta, _lib.stream())
+            ws = torch.empty((splits, M, N), dtype=torch.float32, device=a.device)
+            # the 256-row kernel folds its own slabs (last split of each tile); else a fold pass
+            _lib.call("ttdk_gemm_bf16_splitk", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K,
+                      splits, ws.data_ptr(), out.data_ptr(), beta, float(alpha), _lib.stream())
             return out
         e = _epi(out, mode=2, beta=beta, alpha=alpha)
     else:

@@ -532,3 +532,58 @@ def test_dgrad_with_bn_backward_operand_prologue(cfg):
         assert _rel(got, dx_ref) < 1e-2
     # dz stored once for the weight gradient: every element, bf16 of the same expression
     assert _rel(dz, dz_ref) < 4e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,splits,beta", [(1024, 1536, 64 * 96, 8, 1), (768, 384, 64 * 40, 5, 0),
+                                                (1000, 1032, 64 * 33, 4, 1)])
+def test_splitk_in_kernel_fold_256row(M, N, K, splits, beta):
+    """Split-K on the 256-row kernel folds its own fp32 slabs: the last split to finish a tile
+    (per-tile arrival counter) sums the tile's slabs in split order into the output (+= with
+    beta). vs fp32 reference; bitwise deterministic across runs; counters left at zero (a second
+    launch on the same stream is also right)."""
+    from tensorflow_train_distributed_amd.ops import _lib
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(4)
+    a = torch.randn(K, M, device="cuda").bfloat16()
+    b = torch.randn(K, N, device="cuda").bfloat16()
+    ref = a.float().t() @ b.float()
+    base = torch.randn(M, N, device="cuda")
+    outs = []
+    old = _lib.query("ttdk_set_inkernel_fold", 1)  # opt-in path (measured slower in the steps)
+    try:
+        for _ in range(3):
+            out = base.clone()
+            G.gemm(a, b, trans_a=True, out=out, splits=splits, beta=beta)
+            outs.append(out)
+    finally:
+        _lib.query("ttdk_set_inkernel_fold", old)
+    want = ref + base if beta else ref
+    assert _rel(outs[0], want) < 1e-4
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [((64, 28, 28, 256), (512, 1, 1, 256), 1, 0), ((32, 14, 14, 256), (256, 3, 3, 256), 1, 1)])
+def test_conv_wgrad_in_kernel_fold(shape):
+    """Conv weight gradients on the 256-row kernel with split-K fold inside the launch vs fp32."""
+    from torch.nn.grad import conv2d_weight
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    xs, ws, st, pd = shape
+    torch.manual_seed(8)
+    x = torch.randn(xs, device="cuda").bfloat16()
+    N, H, W, C = xs
+    K, R, S, _ = ws
+    P = (H + 2 * pd - R) // st + 1
+    dy = torch.randn(N, P, P, K, device="cuda").bfloat16()
+    from tensorflow_train_distributed_amd.ops import _lib
+    old = _lib.query("ttdk_set_inkernel_fold", 1)
+    try:
+        got = G.conv_wgrad(x, dy, ws, (st, st), (pd, pd))
+        got2 = G.conv_wgrad(x, dy, ws, (st, st), (pd, pd))
+    finally:
+        _lib.query("ttdk_set_inkernel_fold", old)
+    ref = conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, S), dy.float().permute(0, 3, 1, 2), stride=st,
+                        padding=pd).permute(0, 2, 3, 1)
+    assert _rel(got, ref) < 1e-3
+    assert torch.equal(got, got2)
