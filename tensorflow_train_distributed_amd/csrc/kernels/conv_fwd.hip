@@ -29,6 +29,36 @@ TTDK_EXPORT int ttdk_conv_fwd(const bf16_t* x, const bf16_t* w, const TtdkConv* 
   return dispatch<KConvFwd, KDense>(&pa, &pb, pe, M, N, K, 1, bm, bn, st);
 }
 
+// Pointwise (1x1, stride 1) forward conv whose input is the RAW conv output y3 of the previous
+// conv+BN+residual+ReLU unit: the 256-row kernel forms that unit's output
+// h = relu(sc*y3 + sh + r) (r = the residual, or rsc*r + rsh with `proj`) in LDS as its operand
+// and stores h + its ReLU bits (tile column 0) — the unit's BN apply pass disappears.
+// coef = [sc | sh (| rsc | rsh)] fp32 [2 or 4][C]. hipErrorNotSupported when the shape is not on
+// the 256-row kernel (the caller keeps the pass). `stat` rows are 256-row tiles.
+TTDK_EXPORT int ttdk_conv_fwd_bnpro(const bf16_t* y3, const bf16_t* w, const TtdkConv* g, const bf16_t* res,
+                                    const float* coef, int proj, bf16_t* h_out, uint8_t* mask_out,
+                                    const TtdkEpilogue* epi, hipStream_t st) {
+  if (!is_pointwise(g) || !res || !h_out || !mask_out) return hipErrorNotSupported;
+  EpiParams pe = to_epi(epi);
+  const int M = g->N * g->P * g->Q, N = g->K, K = g->C;
+  const int bbn = big_bn(M, N, K);
+  if (!bbn || K % 64 || pe.remap || pe.mode != 0) return hipErrorNotSupported;
+  pe.py = res;
+  pe.pcoef = coef;
+  pe.pdz = h_out;
+  pe.pmask = mask_out;
+  pe.pld = K;
+  const big::DenseP pa{y3, K, M}, pb{w, K, N};
+  if (proj) {
+    if (bbn == 256)
+      return big::launch<256, big::OpDenseKBN<128, 2, big::THR, 3>, big::OpDenseK<128, 2>, 0, 0>(pa, pb, pe, M, N, K, 1, st);
+    return big::launch<128, big::OpDenseKBN<128, 2, big::THR, 3>, big::OpDenseK<64, 2>, 0, 0>(pa, pb, pe, M, N, K, 1, st);
+  }
+  if (bbn == 256)
+    return big::launch<256, big::OpDenseKBN<128, 2, big::THR, 2>, big::OpDenseK<128, 2>, 0, 0>(pa, pb, pe, M, N, K, 1, st);
+  return big::launch<128, big::OpDenseKBN<128, 2, big::THR, 2>, big::OpDenseK<64, 2>, 0, 0>(pa, pb, pe, M, N, K, 1, st);
+}
+
 // fp8 forward conv / GEMM on the block-scaled MFMA: x8 [N,H,W,C] and w8 [K][R][S][C] in fp8
 // e4m3 (per-tensor scales folded into epi->alpha by the caller). C % 128 == 0, 256-row tiles.
 TTDK_EXPORT int ttdk_conv_fwd_fp8(const uint8_t* x8, const uint8_t* w8, const TtdkConv* g, int bn,

@@ -537,9 +537,14 @@ struct EpiParams {
   // stride pld) before any fragment is read, and the workgroups of tile column 0 store dz to pdz
   // (the weight gradient's operand): the separate BN backward-apply pass and this GEMM's
   // re-read of its output disappear.
+  // Forward modes (OpDenseKBN<.., 2 | 3>, the next unit's 1x1 conv consuming a raw conv output):
+  // A tile = y3 (DMA); in LDS it becomes h = relu(sc[k]*y3 + sh[k] + r) with r = py (residual)
+  // (mode 3: r*rsc[k] + rsh[k], the projection shortcut's BN), pcoef = [sc | sh (| rsc | rsh)];
+  // tile column 0 stores h to pdz and its ReLU bits to pmask — the BN apply pass disappears.
   const bf16_t* py;
   const float* pcoef;
   bf16_t* pdz;
+  uint8_t* pmask;
   long long pld;
   // mode 3 (256-row kernel): split-K with the fold inside the launch. Every split writes its fp32
   // slab as in mode 1; the workgroup that finishes a tile last (per-tile arrival counter kctr,
@@ -1246,29 +1251,31 @@ struct OpWgradMN {
   }
 };
 
-// dense K-major A operand whose tile gets the BN-backward prologue (EpiParams::py/pcoef/pdz)
-template <int HROWS, int ESZ, int T = THR>
+// dense K-major A operand whose tile gets a BN operand prologue (EpiParams::py/pcoef/pdz/pmask):
+// MODE 1 BN backward apply, 2 BN forward apply + residual + ReLU, 3 the same with the residual's
+// own BN (projection shortcut)
+template <int HROWS, int ESZ, int T = THR, int MODE = 1>
 struct OpDenseKBN : OpDenseK<HROWS, ESZ, T> {};
 
 template <class OP>
 struct Traits {
   static constexpr bool kmaj = true;
-  static constexpr bool bnpro = false;
+  static constexpr int bnpro = 0;
 };
-template <int HR, int E, int T>
-struct Traits<OpDenseKBN<HR, E, T>> {
+template <int HR, int E, int T, int MODE>
+struct Traits<OpDenseKBN<HR, E, T, MODE>> {
   static constexpr bool kmaj = true;
-  static constexpr bool bnpro = true;
+  static constexpr int bnpro = MODE;
 };
 template <int HR, int T>
 struct Traits<OpDenseMN<HR, T>> {
   static constexpr bool kmaj = false;
-  static constexpr bool bnpro = false;
+  static constexpr int bnpro = 0;
 };
 template <int HR, int T>
 struct Traits<OpWgradMN<HR, T>> {
   static constexpr bool kmaj = false;
-  static constexpr bool bnpro = false;
+  static constexpr int bnpro = 0;
 };
 
 // fragment readers
@@ -1566,8 +1573,9 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   // K-tile ahead (before that tile's remaining DMAs, so the counted waits retire them too), the
   // tile's 3 x 64 coefficients are DMA'd next to the operand stages, and once the tile has landed
   // each thread rewrites its own pieces in LDS (one extra barrier per K-tile).
-  constexpr bool BNP = Traits<OA>::bnpro;
+  constexpr int BNP = Traits<OA>::bnpro;
   static_assert(!BNP || (PP == 0 && F8 == 0 && T == THR && GA == 2), "BN prologue: bf16 two-barrier 512-thread path");
+  constexpr int NCOEF = BNP == 1 ? 3 : (BNP == 2 ? 2 : 4);  // fp32 [NCOEF][K] arrays in pcoef
   uint4 yv[2][GA];
   const int pchunk = (tid & 7) ^ ((tid >> 4) & 7);
   auto prow = [&](int h, int i) { return m0 + h * 128 + ((i * T + tid) >> 3); };
@@ -1584,20 +1592,21 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   };
   auto issue_coef = [&](int kt) {
     if constexpr (BNP) {
-      const float* src = lane < 48 ? E.pcoef + static_cast<long long>(lane >> 4) * K + kt * 64 + (lane & 15) * 4
-                                   : reinterpret_cast<const float*>(g_zero);
+      const float* src = lane < 16 * NCOEF ? E.pcoef + static_cast<long long>(lane >> 4) * K + kt * 64 + (lane & 15) * 4
+                                           : reinterpret_cast<const float*>(g_zero);
       glds(src, smem + Gm::COEF + ((kt - kt0) & 1) * 1024);
     }
   };
   auto transform = [&](int kt, char* b) {
     if constexpr (BNP) {
       const float* cf = reinterpret_cast<const float*>(smem + Gm::COEF + ((kt - kt0) & 1) * 1024) + pchunk * 8;
-      float ca[8], cbv[8], cc[8];
+      float c0[8], c1[8], c2[8], c3[8];
 #pragma unroll
       for (int j = 0; j < 8; j += 4) {
-        *reinterpret_cast<f32x4_t*>(ca + j) = *reinterpret_cast<const f32x4_t*>(cf + j);
-        *reinterpret_cast<f32x4_t*>(cbv + j) = *reinterpret_cast<const f32x4_t*>(cf + 64 + j);
-        *reinterpret_cast<f32x4_t*>(cc + j) = *reinterpret_cast<const f32x4_t*>(cf + 128 + j);
+        *reinterpret_cast<f32x4_t*>(c0 + j) = *reinterpret_cast<const f32x4_t*>(cf + j);
+        *reinterpret_cast<f32x4_t*>(c1 + j) = *reinterpret_cast<const f32x4_t*>(cf + 64 + j);
+        if constexpr (NCOEF >= 3) *reinterpret_cast<f32x4_t*>(c2 + j) = *reinterpret_cast<const f32x4_t*>(cf + 128 + j);
+        if constexpr (NCOEF >= 4) *reinterpret_cast<f32x4_t*>(c3 + j) = *reinterpret_cast<const f32x4_t*>(cf + 192 + j);
       }
       const bool store = tile_n == 0;
 #pragma unroll
@@ -1608,13 +1617,39 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
           float gv[8], yf[8];
           unpack8(*q, gv);
           unpack8(yv[h][i], yf);
+          if constexpr (BNP == 1) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) gv[j] = ca[j] * gv[j] + cbv[j] * yf[j] + cc[j];  // = bwd_apply_kernel
+            for (int j = 0; j < 8; ++j) gv[j] = c0[j] * gv[j] + c1[j] * yf[j] + c2[j];  // = bwd_apply_kernel
+          } else {  // = apply_kernel: y*scale + shift, + residual (or its BN), ReLU
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gv[j] = gv[j] * c0[j] + c1[j];
+            if constexpr (BNP == 3) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) gv[j] += yf[j] * c2[j] + c3[j];
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) gv[j] += yf[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gv[j] = fmaxf(gv[j], 0.f);
+          }
           const uint4 o = pack8(gv);
           *q = o;
           const int r = prow(h, i);
-          if (store && r < M)
-            *reinterpret_cast<uint4*>(E.pdz + static_cast<long long>(r) * E.pld + kt * 64 + pchunk * 8) = o;
+          if (store && r < M) {
+            const long long off = static_cast<long long>(r) * E.pld + kt * 64 + pchunk * 8;
+            *reinterpret_cast<uint4*>(E.pdz + off) = o;
+            if constexpr (BNP != 1) {  // ReLU bit per element of the stored value
+              const uint32_t wv[4] = {o.x, o.y, o.z, o.w};
+              uint32_t mb = 0;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const uint32_t hh = (wv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+                mb |= ((hh & 0x7fffu) != 0 && !(hh & 0x8000u) ? 1u : 0u) << j;
+              }
+              E.pmask[off >> 3] = static_cast<uint8_t>(mb);
+            }
+          }
         }
     }
   };
@@ -2338,6 +2373,7 @@ inline EpiParams to_epi(const TtdkEpilogue* e) {
   p.py = nullptr;
   p.pcoef = nullptr;
   p.pdz = nullptr;
+  p.pmask = nullptr;
   p.pld = 0;
   p.kout = nullptr;
   p.kctr = nullptr;

@@ -118,6 +118,10 @@ class ResNet:
         # in LDS as their operand and store dz for the weight gradient: no separate backward-apply
         # pass, no re-read of dz (ops.gemm.conv_dgrad(bn_pro=...)); TTD_DGRAD_BNPRO=0: off
         self.bn_pro = os.environ.get("TTD_DGRAD_BNPRO", "1") != "0"
+        # the block output h = relu(bn3(y3) + shortcut) formed inside the next block's c1 conv
+        # (256-row kernel operand prologue, stores h + ReLU bits): no BN apply pass for the
+        # stage-3/4 blocks the streaming pointwise kernel does not take; TTD_FWD_BNPRO=0: off
+        self.fwd_pro = os.environ.get("TTD_FWD_BNPRO", "1") != "0"
         # stem weight gradient on its dedicated kernel (3 real input channels, BN backward on the fly)
         self.stem_kernel = os.environ.get("TTD_STEM_WGRAD", "1") != "0"
         # dedicated stem forward kernel (stem_fwd.hip: K = 7 x 32 over the 3 real channels)
@@ -265,6 +269,15 @@ class ResNet:
     BNPRO_MAX_K = 1024
     BNPRO_MAX_N = 512
 
+    def _fwd_pro_ok(self, c: ConvSpec, x_shape) -> bool:
+        """c (a 1x1 unit-stride conv) can take its input's BN apply + residual + ReLU as the
+        256-row kernel's operand prologue (ops.gemm.conv_fwd_bnpro), same shape rule as the
+        backward prologue."""
+        from ..ops import gemm as G
+        return (self.fwd_pro and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0
+                and c.cin_store <= self.BNPRO_MAX_K and c.cout <= self.BNPRO_MAX_N and not self._fp8_conv(c)
+                and G.conv_fwd_bnpro_ok(tuple(x_shape), (c.cout, 1, 1, c.cin_store)))
+
     def _pw_dgrad_ok(self, c: ConvSpec) -> bool:
         from ..ops import gemm as G
         return (self.fuse_pw and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0
@@ -328,6 +341,18 @@ class ResNet:
                 x = side  # the unit's input as the backward needs it
             else:
                 y, partial, T = G.conv3_halo(x, w4, stat=True)
+        elif pro is not None and not self._pw_fwd_ok(c, True):
+            # the producing unit's BN apply + residual + ReLU inside this conv's operand tile
+            psc, psh, pres, pres_bn, side, side_mask = pro
+            if psh.data_ptr() == psc.data_ptr() + 4 * psc.numel():  # BNState rows scale, shift
+                coef = torch.as_strided(psc, (2, psc.numel()), (psc.numel(), 1))
+            else:
+                coef = torch.stack([psc, psh])
+            if pres_bn is not None:
+                coef = torch.cat([coef.reshape(-1), pres_bn[0], pres_bn[1]])
+            w4 = P.c[c.name + "_conv/kernel"]
+            y, partial, T = G.conv_fwd_bnpro(x, w4, coef, pres, side, side_mask, proj=pres_bn is not None)
+            x = side  # the unit's input as the backward needs it
         elif pro is not None or (not use8 and self._pw_part("plain") and self._pw_fwd_ok(c, False)):
             w2 = P.c[c.name + "_conv/kernel"].view(c.cout, c.cin_store)
             if pro is not None:
@@ -637,6 +662,9 @@ class ResNet:
             sc_bn = (cd[3].scale, cd[3].shift) if cd is not None and self.fuse_proj else None
             defer3 = (nxt is not None and self._pw_part("c31") and self._pw_fwd_ok(nxt["c1"], True)
                       and not self._fp8_conv(nxt["c1"]))
+            if not defer3 and nxt is not None:
+                # or on the 256-row kernel's operand prologue (stage-3/4 widths)
+                defer3 = self._fwd_pro_ok(nxt["c1"], tuple(c3_in.shape[:3]) + (blk["c3"].cout,))
             c3_in = y2 if fuse23 else o2
             c3_pro = (c2[3].scale, c2[3].shift, None, None, o2, c2[2]) if fuse23 else None
             if defer3:

@@ -56,6 +56,7 @@ _SIGS = {
     "ttdk_conv_dgrad_bnpro": [P, P, G, P, P, P, E, P],
     "ttdk_conv_dgrad_bnpro_ok": [G],
     "ttdk_set_inkernel_fold": [I],
+    "ttdk_conv_fwd_bnpro": [P, P, G, P, P, I, P, P, E, P],
     "ttdk_conv_dgrad_subpixel": [P, P, G, P, E, P],
     "ttdk_conv_dgrad_subpixel_stat_rows": [G],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],

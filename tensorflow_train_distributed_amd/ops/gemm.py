@@ -237,6 +237,11 @@ def gemm_f32(a, b, *, trans_a=False, trans_b=False, out=None, bias=None, beta=0)
     return out
 
 
+# workgroups a split-K weight gradient on the 256-row kernel aims for (one per CU: 256 = one
+# wave over the chip; fewer leave CUs to the data-gradient chain it overlaps; TTD_WGRAD_WGS)
+BIG_WGRAD_WGS = int(_os.environ.get("TTD_WGRAD_WGS", "256"))
+
+
 def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
     """Split-K factor for a weight-gradient GEMM (long K = tokens, small M x N). Mirrors the
     launcher's kernel choice: the 256x256 LDS-DMA kernel (M, N >= 256, M*N >= 2^20, one
@@ -244,7 +249,7 @@ def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
     bbn = big_bn(M, N, K)
     if bbn:
         tiles = -(-M // 256) * -(-N // bbn)
-        return max(1, min((K // 64) // 32, -(-256 // tiles)))
+        return max(1, min((K // 64) // 32, -(-BIG_WGRAD_WGS // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
@@ -360,6 +365,41 @@ def conv_fwd(x, w, stride=(1, 1), padding=(0, 0), *, out=None, residual=None, ac
     _lib.call("ttdk_conv_fwd", x.data_ptr(), w.data_ptr(), ctypes.byref(g), tile[0], tile[1], ctypes.byref(e),
               _lib.stream())
     return out
+
+
+def conv_fwd_bnpro_ok(x_shape, w_shape):
+    """Whether conv_fwd_bnpro runs: a 1x1 unit-stride conv on the 256-row kernel."""
+    N, H, W, C = x_shape
+    K = w_shape[0]
+    return (tuple(w_shape[1:3]) == (1, 1) and C % 64 == 0 and C == w_shape[3]
+            and big_bn(N * H * W, K, C) != 0)
+
+
+def conv_fwd_bnpro(y3, w, coef, res, h_out, mask_out, *, proj=False):
+    """1x1 conv whose input is the RAW output y3 of the previous conv+BN+residual+ReLU unit: the
+    kernel forms h = relu(sc*y3 + sh + res) (proj: + rsc*res + rsh) in LDS as its operand and
+    stores h and its ReLU bits (the apply pass that would have produced them disappears).
+    coef: fp32 [2, C] = (sc, sh) or [4, C] with proj. Returns (y, partial [T, 2, K], T): the
+    conv output and its per-256-row-tile BN (sum, sum of squares)."""
+    _check(y3, torch.bfloat16, "y3")
+    _check(w, torch.bfloat16, "w")
+    _check(res, torch.bfloat16, "res")
+    if not conv_fwd_bnpro_ok(tuple(y3.shape), tuple(w.shape)):
+        raise ValueError("conv_fwd_bnpro: needs a 1x1 conv on the 256-row kernel")
+    if tuple(res.shape) != tuple(y3.shape) or tuple(h_out.shape) != tuple(y3.shape) or \
+            mask_out.numel() * 8 != y3.numel() or coef.dtype != torch.float32 or not coef.is_contiguous() or \
+            coef.numel() != (4 if proj else 2) * y3.shape[-1]:
+        raise ValueError("conv_fwd_bnpro: operand shapes")
+    g = conv_geom(y3.shape, w.shape, (1, 1), (0, 0))
+    M = g.N * g.P * g.Q
+    T = -(-M // 256)
+    out = torch.empty((g.N, g.P, g.Q, g.K), dtype=torch.bfloat16, device=y3.device)
+    partial = torch.empty((T, 2, g.K), dtype=torch.float32, device=y3.device)
+    e = _epi(out, ldo=g.K, stat=partial)
+    _log("fwd_bnpro_1x1", M, g.K, g.C)
+    _lib.call("ttdk_conv_fwd_bnpro", y3.data_ptr(), w.data_ptr(), ctypes.byref(g), res.data_ptr(), coef.data_ptr(),
+              1 if proj else 0, h_out.data_ptr(), mask_out.data_ptr(), ctypes.byref(e), _lib.stream())
+    return out, partial, T
 
 
 # strided (non-pointwise) dgrad via sub-pixel phase decomposition; TTD_SUBPIXEL_DGRAD=0 keeps
@@ -548,7 +588,7 @@ def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
         # ~1 wave of 256 workgroups, but >= 32 K-tiles per split: fp32 slabs cost 8 B per output
         # element per split (write + reduce read)
         tiles = -(-M // 256) * -(-N // bbn)
-        return max(1, min((K // 64) // 32, -(-256 // tiles)))
+        return max(1, min((K // 64) // 32, -(-BIG_WGRAD_WGS // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)

@@ -587,3 +587,40 @@ def test_conv_wgrad_in_kernel_fold(shape):
                         padding=pd).permute(0, 2, 3, 1)
     assert _rel(got, ref) < 1e-3
     assert torch.equal(got, got2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(32, 28, 512, 128, False), (64, 14, 1024, 256, True), (17, 17, 512, 256, False)])
+def test_conv_fwd_with_bn_apply_operand_prologue(cfg):
+    """conv_fwd_bnpro: the 1x1 conv consuming the RAW output y3 of a conv+BN+residual+ReLU unit
+    forms h = relu(sc*y3 + sh + r) (projection: + rsc*r + rsh) as its operand in LDS, stores h
+    and its ReLU bits, and emits its own BN partial sums — vs the unfused engine ops (bn_apply
+    pass + conv) and an fp32 conv of the same h."""
+    import torch.nn.functional as F
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    N, H, C, Kout, proj = cfg
+    torch.manual_seed(9)
+    y3 = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    r = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    rsc, rsh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    w = (torch.randn(Kout, 1, 1, C, device="cuda") / C ** 0.5).bfloat16()
+    coef = torch.cat([sc, sh, rsc, rsh]) if proj else torch.cat([sc, sh])
+    M = N * H * H
+    h = torch.empty_like(y3)
+    hm = torch.empty(M * C // 8, dtype=torch.uint8, device="cuda")
+    y, partial, T = G.conv_fwd_bnpro(y3, w, coef, r, h, hm, proj=proj)
+    # reference: the engine's own apply pass (same arithmetic) and an fp32 conv of its output
+    mask_ref = torch.empty_like(hm)
+    h_ref = K.bn_apply(y3.view(M, C), sc, sh, residual=r.view(M, C), residual_bn=(rsc, rsh) if proj else None,
+                       relu=True, mask=mask_ref).view(N, H, H, C)
+    assert torch.equal(h, h_ref)
+    assert torch.equal(hm, mask_ref)
+    y_ref = F.conv2d(h_ref.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert _rel(y, y_ref) < 1e-2
+    yf = y.float().view(-1, Kout)
+    sums = partial.sum(0)
+    torch.testing.assert_close(sums[0], yf.sum(0), rtol=2e-3, atol=5e-2)
+    torch.testing.assert_close(sums[1], (yf * yf).sum(0), rtol=2e-3, atol=5e-1)
+    assert T == -(-M // 256)

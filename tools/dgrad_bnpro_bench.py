@@ -67,5 +67,41 @@ def main():
         print(json.dumps(res[-1]), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--fwd" not in sys.argv:
     main()
+
+
+def forward_ab():
+    """Forward: BN apply pass (+ residual + ReLU + mask) then the next 1x1 conv with BN statistics,
+    vs conv_fwd_bnpro (the apply formed in the conv's operand tile)."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    dev = torch.device("cuda", 0)
+    B = 1024
+    for name, H, C, Kout, proj in [("s3_c3->c1", 28, 512, 128, False), ("s3->s4b1_c1", 28, 512, 256, False),
+                                   ("s4_c3->c1", 14, 1024, 256, False), ("s4b1_proj", 14, 1024, 256, True)]:
+        M = B * H * H
+        y3 = torch.randn(B, H, H, C, device=dev).bfloat16()
+        r = torch.randn(B, H, H, C, device=dev).bfloat16()
+        sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+        coef = torch.cat([sc, sh, sc, sh]) if proj else torch.cat([sc, sh])
+        w = (torch.randn(Kout, 1, 1, C, device=dev) / C ** 0.5).bfloat16()
+        h = torch.empty_like(y3)
+        hm = torch.empty(M * C // 8, dtype=torch.uint8, device=dev)
+        T = -(-M // 256)
+        partial = torch.empty((T, 2, Kout), device=dev)
+
+        def unfused():
+            K.bn_apply(y3.view(M, C), sc, sh, residual=r.view(M, C), residual_bn=(sc, sh) if proj else None,
+                       relu=True, out=h.view(M, C), mask=hm)
+            G.conv_fwd(h, w, stat=partial, tile=(256, G.big_bn(M, Kout, C)))
+
+        def fused():
+            G.conv_fwd_bnpro(y3, w, coef, r, h, hm, proj=proj)
+        ta, tb = timed(unfused), timed(fused)
+        print(json.dumps({"shape": name, "unfused_us": round(ta, 1), "fused_us": round(tb, 1),
+                          "speedup": round(ta / tb, 3)}), flush=True)
+
+
+if __name__ == "__main__" and "--fwd" in sys.argv:
+    forward_ab()
