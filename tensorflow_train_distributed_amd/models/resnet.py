@@ -268,14 +268,17 @@ class ResNet:
     # ping-pong schedule (stage-5 c3: 0.81x): those keep the pass.
     BNPRO_MAX_K = 1024
     BNPRO_MAX_N = 512
+    # forward apply prologue (h = relu(bn3(y3) + shortcut) formed in the next c1's operand tile):
+    # faster at the stage-3 widths (512 -> 128: 1.18x, 512 -> 256: 1.04x), slower at stage 4
+    # (1024 -> 256: 0.90x, with the projection BN 0.87x): tools/dgrad_bnpro_bench.py --fwd
+    FWDPRO_MAX_K = 512
 
     def _fwd_pro_ok(self, c: ConvSpec, x_shape) -> bool:
-        """c (a 1x1 unit-stride conv) can take its input's BN apply + residual + ReLU as the
-        256-row kernel's operand prologue (ops.gemm.conv_fwd_bnpro), same shape rule as the
-        backward prologue."""
+        """c (a 1x1 unit-stride conv) takes its input's BN apply + residual + ReLU as the 256-row
+        kernel's operand prologue (ops.gemm.conv_fwd_bnpro)."""
         from ..ops import gemm as G
         return (self.fwd_pro and self.device.type == "cuda" and c.k == 1 and c.stride == 1 and c.pad == 0
-                and c.cin_store <= self.BNPRO_MAX_K and c.cout <= self.BNPRO_MAX_N and not self._fp8_conv(c)
+                and c.cin_store <= self.FWDPRO_MAX_K and c.cout <= self.BNPRO_MAX_N and not self._fp8_conv(c)
                 and G.conv_fwd_bnpro_ok(tuple(x_shape), (c.cout, 1, 1, c.cin_store)))
 
     def _pw_dgrad_ok(self, c: ConvSpec) -> bool:
@@ -301,7 +304,7 @@ class ResNet:
                 and G.conv3_rows(H, W, c.cin_store, c.cout) > 0)
 
     def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False, pool=False, defer=False,
-                    residual_bn=None, pro=None):
+                    residual_bn=None, pro=None, pro_big=False):
         """conv + BN (+residual) (+ReLU). x8 = (fp8 copy of x, its scale slot) selects the fp8
         forward GEMM; want8 makes the BN-apply pass also emit an fp8 copy of the output.
         defer=True: no apply pass — returns the raw conv output (the consumer applies this BN
@@ -310,7 +313,8 @@ class ResNet:
         BN+ReLU output; returns (pooled, ctx, argmax).
         pro=(scale, shift, res, res_bn, side, side_mask): x is the RAW conv output of the producing
         unit; its BN apply (+ residual) runs inside this conv's operand load (streaming pointwise
-        kernel) and the applied tensor / its ReLU bits land in side / side_mask (this unit's input).
+        kernel, or pro_big: the 256-row kernel's operand prologue) and the applied tensor / its ReLU
+        bits land in side / side_mask (this unit's input).
         Returns (out, ctx) or (out, ctx, out8) when want8."""
         from ..ops import gemm as G
         from ..ops import kernels as K
@@ -341,7 +345,7 @@ class ResNet:
                 x = side  # the unit's input as the backward needs it
             else:
                 y, partial, T = G.conv3_halo(x, w4, stat=True)
-        elif pro is not None and not self._pw_fwd_ok(c, True):
+        elif pro is not None and pro_big:
             # the producing unit's BN apply + residual + ReLU inside this conv's operand tile
             psc, psh, pres, pres_bn, side, side_mask = pro
             if psh.data_ptr() == psc.data_ptr() + 4 * psc.numel():  # BNState rows scale, shift
@@ -585,9 +589,10 @@ class ResNet:
         if fp8:
             self._fp8_step_begin()
 
-        def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None, pro=None):
+        def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None, pro=None,
+                 pro_big=False):
             r = self._convbn_fwd(c, inp, relu, residual=residual, x8=inp8, want8=want8, defer=defer,
-                                 residual_bn=residual_bn, pro=pro)
+                                 residual_bn=residual_bn, pro=pro, pro_big=pro_big)
             return r if want8 else (r[0], r[1], None)
 
         from ..utils import tracing
@@ -616,12 +621,12 @@ class ResNet:
                                                                  h.shape[2] if pend is None else pend[0].shape[2])
             if pend is not None:
                 # this block's input h = relu(bn3(y3) + shortcut) is produced by c1's operand load
-                y3p, stp, resp, resbnp, ctxp = pend
+                y3p, stp, resp, resbnp, ctxp, pbig = pend
                 h = torch.empty_like(y3p)
                 hm = torch.empty(h.numel() // 8, dtype=torch.uint8, device=h.device)
                 ctxp[2] = hm  # the producing unit's ReLU bits (its backward reads them)
                 o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm), defer=c3ok,
-                                    want8=fp8 and not c3ok and self._fp8_conv(blk["c2"]))
+                                    want8=fp8 and not c3ok and self._fp8_conv(blk["c2"]), pro_big=pbig)
                 pend = None
             if blk["cd"] is not None and side is not None:
                 # projection shortcut on the side stream, concurrent with the c1 -> c2 chain
@@ -662,14 +667,15 @@ class ResNet:
             sc_bn = (cd[3].scale, cd[3].shift) if cd is not None and self.fuse_proj else None
             defer3 = (nxt is not None and self._pw_part("c31") and self._pw_fwd_ok(nxt["c1"], True)
                       and not self._fp8_conv(nxt["c1"]))
+            c3_in = y2 if fuse23 else o2
+            defer_big = False
             if not defer3 and nxt is not None:
                 # or on the 256-row kernel's operand prologue (stage-3/4 widths)
-                defer3 = self._fwd_pro_ok(nxt["c1"], tuple(c3_in.shape[:3]) + (blk["c3"].cout,))
-            c3_in = y2 if fuse23 else o2
+                defer3 = defer_big = self._fwd_pro_ok(nxt["c1"], tuple(c3_in.shape[:3]) + (blk["c3"].cout,))
             c3_pro = (c2[3].scale, c2[3].shift, None, None, o2, c2[2]) if fuse23 else None
             if defer3:
                 y3, c3, _ = unit(blk["c3"], c3_in, True, defer=True, pro=c3_pro)
-                pend = (y3, c3[3], sc, sc_bn, c3)
+                pend = (y3, c3[3], sc, sc_bn, c3, defer_big)
                 o3, h8 = None, None
             else:
                 o3, c3, h8 = unit(blk["c3"], c3_in, True, residual=sc, inp8=o2_8, residual_bn=sc_bn, pro=c3_pro,
