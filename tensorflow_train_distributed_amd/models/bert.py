@@ -145,6 +145,10 @@ class BertPretraining:
                     if o2 != o + j * width:
                         raise AssertionError("q/k/v %s not contiguous" % name_a)
         self.rng = None
+        # workgroups each side-stream weight-gradient GEMM aims for (split-K count): 192 of the 256
+        # CUs leave room for the data-gradient chain's kernels (b128: 180.0 -> 176.8 ms/step over
+        # two A/B pairs; 128: 177.4); TTD_BERT_WGRAD_WGS
+        self.wgrad_wgs = int(os.environ.get("TTD_BERT_WGRAD_WGS", "192"))
         # encoder weight gradients on a second HIP stream (TTD_WGRAD_STREAM=0: single stream)
         self.wgrad_stream = os.environ.get("TTD_WGRAD_STREAM", "1") != "0" and self.device.type == "cuda"
         # data-gradient GEMMs read [in][out] copies of the encoder weights (K-major B: ~10 % faster
@@ -288,7 +292,7 @@ class BertPretraining:
 
         def wgrad(dy, x, out):
             M, N, Kd = dy.shape[1], x.shape[1], dy.shape[0]
-            G.gemm(dy, x, trans_a=True, out=out, splits=G.gemm_wgrad_splits(M, N, Kd))
+            G.gemm(dy, x, trans_a=True, out=out, splits=G.gemm_wgrad_splits(M, N, Kd, big_wgs=self.wgrad_wgs))
 
         # encoder weight gradients (+ bias column sums) run on a second HIP stream, overlapping
         # the data-gradient chain; the bucket hooks are issued from it so collectives order after

@@ -242,14 +242,14 @@ def gemm_f32(a, b, *, trans_a=False, trans_b=False, out=None, bias=None, beta=0)
 BIG_WGRAD_WGS = int(_os.environ.get("TTD_WGRAD_WGS", "256"))
 
 
-def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8):
+def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8, big_wgs=None):
     """Split-K factor for a weight-gradient GEMM (long K = tokens, small M x N). Mirrors the
     launcher's kernel choice: the 256x256 LDS-DMA kernel (M, N >= 256, M*N >= 2^20, one
     workgroup per CU -> aim for ~1-2 waves of 256 workgroups) or the 4-wave 128x128 kernel."""
     bbn = big_bn(M, N, K)
     if bbn:
         tiles = -(-M // 256) * -(-N // bbn)
-        return max(1, min((K // 64) // 32, -(-BIG_WGRAD_WGS // tiles)))
+        return max(1, min((K // 64) // 32, -(-(big_wgs or BIG_WGRAD_WGS) // tiles)))
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
     tiles = -(-M // bm) * -(-N // bn)
