@@ -289,19 +289,23 @@ def main():
         prio.wait_stream(torch.cuda.current_stream())
     graph_info = None
     if use_graph:
-        # the whole step (both streams: the side-stream weight-gradient chain forks from and
-        # joins the captured stream, so replay keeps the two branches concurrent) in one hipGraph
-        # whose kernel nodes keep the eager streams' priorities (utils/graphs.py)
-        from tensorflow_train_distributed_amd.utils.graphs import capture, capture_prioritized
-        for _ in range(2):
-            step()
-        sync()
-        if os.environ.get("TTD_GRAPH_PRIO", "1") != "0":
-            graph = capture_prioritized(step, stream=prio)
+        from tensorflow_train_distributed_amd.utils import graphs
+        mode = os.environ.get("TTD_GRAPH_MODE", "segmented" if world == 1 else "single")
+        if mode == "segmented":
+            # per-stream linear graph segments replayed on the eager step's own streams (main
+            # high priority, weight gradients normal priority); cross-stream edges are event nodes
+            # (utils/graphs.py). The native RCCL engine's comm stream forks and joins inside its own
+            # library, so N>1 captures the step as one graph instead.
+            main_s = prio if prio is not None else torch.cuda.Stream(device=dev)
+            graph = graphs.capture_segmented(step, main=main_s, warmup=2)
             out = graph.outputs
-            graph_info = graph.info
+            graph_info = dict(graph.info, mode="segmented")
         else:
-            graph, out = capture(step, stream=prio)
+            for _ in range(2):
+                step()
+            sync()
+            graph, out = graphs.capture(step, stream=prio)
+            graph_info = {"mode": "single"}
         run = graph.replay
     else:
         run = step
@@ -389,7 +393,7 @@ def main():
         cfg = dict(info["config"])
         cfg["hipgraph"] = bool(use_graph)
         if graph_info is not None:
-            cfg["hipgraph_node_priority"] = graph_info
+            cfg["hipgraph_capture"] = graph_info
         if not on_cpu:
             cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         cfg["final_loss"] = loss

@@ -311,10 +311,8 @@ class BertPretraining:
                 if bout is not None:
                     K.colsum(dy, out=bout)
                 return
-            ev = torch.cuda.Event()
-            ev.record()
-            side.wait_event(ev)
-            with graphs.side_scope(side), torch.cuda.stream(side):
+            graphs.fork(torch.cuda.current_stream(), side)
+            with torch.cuda.stream(side):
                 wgrad(dy, x, wout)
                 if bout is not None:
                     K.colsum(dy, out=bout)
@@ -323,13 +321,10 @@ class BertPretraining:
         wt_ready = None
         if self.transposed_dgrad:
             if side is not None:  # overlaps the forward pass; the encoder backward waits for it
-                ev0 = torch.cuda.Event()
-                ev0.record()
-                side.wait_event(ev0)
-                with graphs.side_scope(side), torch.cuda.stream(side):
+                graphs.fork(torch.cuda.current_stream(), side)
+                with torch.cuda.stream(side):
                     self._refresh_transposed()
-                    wt_ready = torch.cuda.Event()
-                    wt_ready.record()
+                    wt_ready = graphs.mark(side)
             else:
                 self._refresh_transposed()
 
@@ -337,7 +332,7 @@ class BertPretraining:
             if side is None:
                 hook(name)
             else:
-                with graphs.side_scope(side), torch.cuda.stream(side):
+                with torch.cuda.stream(side):
                     hook(name)
 
         ids = batch.input_ids.reshape(-1)
@@ -440,7 +435,7 @@ class BertPretraining:
                      if fuse_bias else None)
         delta = torch.empty((B * NH, S), dtype=torch.float32, device=dev)
         if wt_ready is not None:
-            torch.cuda.current_stream().wait_event(wt_ready)
+            graphs.join_mark(torch.cuda.current_stream(), wt_ready)
         for l in reversed(range(L)):
             x, qkv, ao, lse, s1, m1, r1, y1, pre, inter, s2, m2, r2 = ctx.pop()
             G1 = torch.empty((Tk, H), dtype=bf, device=dev)
@@ -486,7 +481,7 @@ class BertPretraining:
             layer_hook(self._ln(l, "attention/self/value/bias"))
             dy = G0
         if side is not None:
-            torch.cuda.current_stream().wait_stream(side)
+            graphs.join(torch.cuda.current_stream(), side)
         keep.clear()
 
         # ---------------------------------------------------------------- backward: embeddings

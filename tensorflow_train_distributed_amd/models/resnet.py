@@ -434,7 +434,7 @@ class ResNet:
             if self._wgrad_stream is not None:
                 # the bucket this completes may hold side-stream gradients: collectives issued
                 # from here must order after that stream too
-                torch.cuda.current_stream().wait_stream(self._wgrad_stream)
+                graphs.join(torch.cuda.current_stream(), self._wgrad_stream)
             self._ready(c.name + "_bn/moving_variance")
             return None, None
         if (need_dx and dstat is not None and feeds is not None and feeds2 is None
@@ -524,8 +524,7 @@ class ResNet:
         out = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, sampled_only=sampled_only, beta_s2=bs2)
         if wgrad_last:
             # data gradient first (its consumer waits on this event), then the weight gradient
-            self._cd_done = torch.cuda.Event()
-            self._cd_done.record()
+            self._cd_done = graphs.mark(torch.cuda.current_stream())
             # its gradient-ready hook waits for the caller: the variables before it in the flat
             # layout (the block's c3 and c2) are not final yet
             self._wgrad(c, x, dz, wname, ready=False)
@@ -540,10 +539,8 @@ class ResNet:
         side = self._wgrad_stream
         if side is not None:
             if torch.cuda.current_stream() != side:  # (a stream waiting on its own event breaks hipGraph capture)
-                ev = torch.cuda.Event()
-                ev.record()
-                side.wait_event(ev)
-            with graphs.side_scope(side), torch.cuda.stream(side):
+                graphs.fork(torch.cuda.current_stream(), side)
+            with torch.cuda.stream(side):
                 G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
                 if ready:
                     self._ready(c.name + "_bn/moving_variance")
@@ -631,10 +628,8 @@ class ResNet:
             if blk["cd"] is not None and side is not None:
                 # projection shortcut on the side stream, concurrent with the c1 -> c2 chain
                 main = torch.cuda.current_stream()
-                ev = torch.cuda.Event()
-                ev.record()
-                side.wait_event(ev)
-                with graphs.side_scope(side), torch.cuda.stream(side):
+                graphs.fork(main, side)
+                with torch.cuda.stream(side):
                     sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
                 # h / h8 stay referenced (c1's ctx) past the join below; cd's outputs were made on
                 # the side stream, whose next work is always ordered after this step's main stream
@@ -659,7 +654,7 @@ class ResNet:
             else:
                 o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]), pro=pro2)
             if blk["cd"] is not None and side is not None:
-                main.wait_stream(side)
+                graphs.join(main, side)
             elif blk["cd"] is not None:
                 sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
             else:
@@ -712,11 +707,9 @@ class ResNet:
             if cd_side:
                 # projection branch (BN backward + strided dgrad, then its weight gradient) on the side
                 # stream, concurrent with the c3 -> c2 chain; c1's dgrad below accumulates into dx
-                ev = torch.cuda.Event()
-                ev.record()
-                side.wait_event(ev)
+                graphs.fork(torch.cuda.current_stream(), side)
                 self._cd_done = None
-                with graphs.side_scope(side), torch.cuda.stream(side):
+                with torch.cuda.stream(side):
                     dx, _ = self._convbn_bwd(blk["cd"], dh, cd, dstat=cd_stat, sampled_only=sampled, wgrad_last=True)
                     cd_done = self._cd_done
                 assert cd_done is not None, "projection backward took a path without the wgrad_last event"
@@ -732,9 +725,9 @@ class ResNet:
             if cd_done is not None:
                 # c3 / c2 weight gradients are now queued on the side stream behind the projection's:
                 # the bucket hook for the projection variables can fire (in flat-layout order)
-                with graphs.side_scope(side), torch.cuda.stream(side):
+                with torch.cuda.stream(side):
                     self._ready(blk["cd"].name + "_bn/moving_variance")
-                torch.cuda.current_stream().wait_event(cd_done)
+                graphs.join_mark(torch.cuda.current_stream(), cd_done)
             elif blk["cd"] is not None:
                 dx, _ = self._convbn_bwd(blk["cd"], g_sc, cd, dstat=cd_stat, sampled_only=sampled)
             else:
@@ -748,7 +741,7 @@ class ResNet:
             dstem = K.maxpool_bwd(dh, arg, s_out.shape, 3, 2, 1)
             self._convbn_bwd(self.stem, dstem, s_ctx, need_dx=False)
         if self._wgrad_stream is not None:
-            torch.cuda.current_stream().wait_stream(self._wgrad_stream)
+            graphs.join(torch.cuda.current_stream(), self._wgrad_stream)
             self._wgrad_stream = None
         self._side_keep = []
         bwd_range.__exit__(None, None, None)

@@ -17,10 +17,9 @@ replay reuses exactly the same addresses.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import os
-from typing import Any, Callable, List, Optional, Tuple
+from typing import Any, Callable, Optional, Tuple
 
 import torch
 
@@ -88,21 +87,10 @@ class GraphedStep:
 
 
 # ---------------------------------------------------------------------------------------------
-# Priority-preserving capture.
-#
-# The eager ResNet step runs its main data-gradient chain on a high-priority stream and the
-# weight gradients on a normal-priority side stream, so the side stream only takes the CUs the
-# main chain's kernels leave idle (their tail waves). Stream capture does not carry stream
-# priority into the graph's kernel nodes, so a plain replay lets the two branches compete as
-# equals. Here the engine marks its side-stream blocks (side_scope); after capture every kernel
-# node gets hipLaunchAttributePriority (side blocks low, everything else high) and the graph is
-# instantiated with hipGraphInstantiateFlagUseNodePriority, so replay dispatches like eager.
+# HIP entry points the torch API does not expose (event nodes, capture dependencies).
 
 _HIP = None
 _P = ctypes.c_void_p
-_KERNEL_NODE = 0             # hipGraphNodeTypeKernel
-_ATTR_PRIORITY = 8           # hipLaunchAttributePriority
-_FLAG_USE_NODE_PRIORITY = 8  # hipGraphInstantiateFlagUseNodePriority
 
 
 def _hip():
@@ -112,129 +100,223 @@ def _hip():
     return _HIP
 
 
-def _capture_graph(stream) -> Optional[int]:
-    """The hipGraph_t being captured on `stream` (None when it is not capturing)."""
+# ---------------------------------------------------------------------------------------------
+# Segmented two-stream capture (what the bench replays).
+#
+# Stream capture does not carry stream priority into kernel nodes, and per-node priorities
+# (hipLaunchAttributePriority + hipGraphInstantiateFlagUseNodePriority) are refused on ROCm 7.2
+# (round-3 probe), so a single multi-branch graph lets the main chain and the side-stream weight
+# gradients compete as equals and replays slower than the eager two-stream ResNet step. The step
+# is instead recorded as LINEAR graphs, one per
+# stream, replayed on the very streams the eager step uses (main chain: high priority; weight
+# gradients: normal priority) — the hardware sees the eager step's queues and priorities.
+# Cross-stream dependencies become event record / wait NODES added to the capture graphs by hand
+# (hipEventRecordWithFlags(..., hipEventRecordExternal) is refused under capture on ROCm 7.2),
+# and every join (main waits for a side stream) cuts the capture into a new segment, so at replay
+# each wait node is enqueued after the record it waits for (segments are launched in capture
+# order: main_k, the side streams' segment k, main_k+1, ...). The engines express their stream
+# forks and joins through fork() / join() / record() / wait() below, which are plain torch
+# events outside such a capture.
+
+_SEG = None  # the active SegmentedCapture
+
+
+def _ev_create():
+    e = _P(0)
+    if _hip().hipEventCreateWithFlags(ctypes.byref(e), 2) != 0:  # hipEventDisableTiming
+        raise RuntimeError("hipEventCreateWithFlags failed")
+    return e
+
+
+def _add_event_node(stream, ev, wait: bool):
     hip = _hip()
-    status = ctypes.c_int(0)
-    cid = ctypes.c_ulonglong(0)
-    graph = _P(0)
-    deps = _P(0)
-    ndeps = ctypes.c_size_t(0)
-    rc = hip.hipStreamGetCaptureInfo_v2(_P(stream.cuda_stream), ctypes.byref(status), ctypes.byref(cid), ctypes.byref(graph), ctypes.byref(deps),
-            ctypes.byref(ndeps))
-    if rc != 0 or status.value != 1 or not graph.value:  # hipStreamCaptureStatusActive
-        return None
-    return graph.value
+    status, cid, graph, deps, n = ctypes.c_int(0), ctypes.c_ulonglong(0), _P(0), _P(0), ctypes.c_size_t(0)
+    rc = hip.hipStreamGetCaptureInfo_v2(_P(stream.cuda_stream), ctypes.byref(status), ctypes.byref(cid),
+                                        ctypes.byref(graph), ctypes.byref(deps), ctypes.byref(n))
+    if rc != 0 or status.value != 1:
+        raise RuntimeError("segmented capture: stream is not capturing (rc %d, status %d)" % (rc, status.value))
+    node = _P(0)
+    add = hip.hipGraphAddEventWaitNode if wait else hip.hipGraphAddEventRecordNode
+    rc = add(ctypes.byref(node), graph, deps, n, ev)
+    if rc != 0:
+        raise RuntimeError("hipGraphAddEvent%sNode failed (%d)" % ("Wait" if wait else "Record", rc))
+    # the node becomes the stream's dependency set: later captured work orders after it
+    rc = hip.hipStreamUpdateCaptureDependencies(_P(stream.cuda_stream), ctypes.byref(node), ctypes.c_size_t(1), 1)
+    if rc != 0:
+        raise RuntimeError("hipStreamUpdateCaptureDependencies failed (%d)" % rc)
 
 
-def graph_nodes(graph: int) -> List[int]:
-    hip = _hip()
-    n = ctypes.c_size_t(0)
-    if hip.hipGraphGetNodes(_P(graph), None, ctypes.byref(n)) != 0:
-        return []
-    arr = (_P * n.value)()
-    if n.value and hip.hipGraphGetNodes(_P(graph), arr, ctypes.byref(n)) != 0:
-        return []
-    return [int(a) for a in arr[:n.value] if a]
+class SegmentedCapture:
+    """Records `fn` as per-stream linear graph segments (see the comment above)."""
 
+    def __init__(self, main: torch.cuda.Stream):
+        self.main = main
+        self.pools = {}
+        self.segments = []  # (stream, CUDAGraph) in launch order
+        self.cur = {}       # stream -> CUDAGraph being captured
+        self.events = []    # persistent hipEvent_t (referenced by the graphs)
+        self.n_ev = 0
+        self.tail = {}      # stream -> event recorded at the end of its last closed segment
+        self.seg_index = 0  # segments closed so far (a mark remembers the one it was recorded in)
 
-_SIDE_NODES: Optional[set] = None  # set while a prioritized capture records
+    # -- capture bookkeeping
+    def _begin(self, s):
+        key = s.cuda_stream
+        if key not in self.pools:
+            self.pools[key] = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            g.capture_begin(pool=self.pools[key], capture_error_mode="relaxed")
+        self.cur[key] = (s, g)
 
+    def _end_all(self):
+        main_key = self.main.cuda_stream
+        order = [main_key] + [k for k in self.cur if k != main_key]
+        for k in order:
+            if k not in self.cur:
+                continue
+            s, g = self.cur[k]
+            if k != main_key:
+                # a side segment may end with work main has not waited for yet (a join to an
+                # earlier mark cut it): its tail event lets a later join wait for all of it
+                ev = self._event()
+                _add_event_node(s, ev, wait=False)
+                self.tail[k] = ev
+            del self.cur[k]
+            with torch.cuda.stream(s):
+                g.capture_end()
+            self.segments.append((s, g))
+        self.seg_index += 1
 
-@contextlib.contextmanager
-def side_scope(stream):
-    """Mark the kernels launched in this block (on `stream`, a low-priority side stream) as
-    side-branch work for a prioritized capture. Free outside capture."""
-    if _SIDE_NODES is None:
-        yield
-        return
-    g = _capture_graph(stream)
-    before = set(graph_nodes(g)) if g else None
-    try:
-        yield
-    finally:
-        if g:
-            _SIDE_NODES.update(set(graph_nodes(g)) - before)
+    def _event(self):
+        if self.n_ev == len(self.events):
+            self.events.append(_ev_create())
+        e = self.events[self.n_ev]
+        self.n_ev += 1
+        return e
 
+    # -- the engine's synchronisation points
+    def fork(self, src, dst):
+        if dst.cuda_stream not in self.cur:
+            self._begin(dst)  # the side stream's next segment starts with this wait
+        ev = self._event()
+        _add_event_node(src, ev, wait=False)
+        _add_event_node(dst, ev, wait=True)
 
-class PrioritizedStep:
-    """A captured step replayed from an executable instantiated with per-node priorities."""
+    def join(self, dst, src):
+        if dst.cuda_stream != self.main.cuda_stream:
+            raise RuntimeError("segmented capture: joins must target the main stream")
+        if src.cuda_stream not in self.cur:
+            ev = self.tail.pop(src.cuda_stream, None)
+            if ev is not None:  # src's work sits in closed (already launched) segments
+                _add_event_node(dst, ev, wait=True)
+            return
+        self.wait_mark(dst, self.mark(src))
 
-    def __init__(self, graph, outputs, prio_exec, info):
-        self.graph = graph          # torch CUDAGraph (keeps the memory pool alive)
-        self.outputs = outputs
-        self.prio_exec = prio_exec  # hipGraphExec_t (None: node priorities unsupported)
-        self.info = info
+    def mark(self, src):
+        """Record a point of src's captured work (a record node)."""
+        if src.cuda_stream not in self.cur:
+            raise RuntimeError("segmented capture: mark on a stream that is not capturing")
+        ev = self._event()
+        _add_event_node(src, ev, wait=False)
+        return (ev, self.seg_index)
+
+    def wait_mark(self, dst, m):
+        if dst.cuda_stream != self.main.cuda_stream:
+            raise RuntimeError("segmented capture: joins must target the main stream")
+        ev, seg = m
+        if seg == self.seg_index:
+            # the record sits in a segment still being captured: cut, so that it is launched
+            # before the segment holding the wait
+            self._end_all()
+            self._begin(self.main)
+        _add_event_node(dst, ev, wait=True)
+
+    # -- run / replay
+    def capture(self, fn):
+        global _SEG
+        if _SEG is not None:
+            raise RuntimeError("nested segmented capture")
+        _SEG = self
+        try:
+            self._begin(self.main)
+            with torch.cuda.stream(self.main):
+                out = fn()
+            self._end_all()
+        finally:
+            _SEG = None
+        return out
 
     def replay(self):
-        if self.prio_exec is None:
-            return self.replay_plain()
-        rc = _hip().hipGraphLaunch(_P(self.prio_exec), _P(torch.cuda.current_stream().cuda_stream))
-        if rc != 0:
-            raise RuntimeError("hipGraphLaunch failed (%d)" % rc)
-        return self.outputs
+        for s, g in self.segments:
+            with torch.cuda.stream(s):
+                g.replay()
 
-    def replay_plain(self):
-        self.graph.replay()
+
+class SegmentedStep:
+    def __init__(self, cap: SegmentedCapture, outputs):
+        self.cap = cap
+        self.outputs = outputs
+        self.info = {"segments": len(cap.segments), "events": cap.n_ev,
+                     "streams": len({s.cuda_stream for s, _ in cap.segments})}
+
+    def replay(self):
+        self.cap.replay()
         return self.outputs
 
     __call__ = replay
 
-    def __del__(self):
-        try:
-            if self.prio_exec is not None:
-                _hip().hipGraphExecDestroy(_P(self.prio_exec))
-        except Exception:  # noqa: BLE001 - interpreter shutdown
-            pass
 
-
-def capture_prioritized(fn: Callable[[], Any], warmup: int = 1, stream: Optional[torch.cuda.Stream] = None,
-                        pool=None) -> PrioritizedStep:
-    """capture() with the eager step's stream priorities kept as node priorities (see above)."""
-    global _SIDE_NODES
+def capture_segmented(fn: Callable[[], Any], main: torch.cuda.Stream, warmup: int = 1) -> SegmentedStep:
+    """Run `fn` `warmup` times eagerly on `main`, then record it as per-stream graph segments
+    (the streams it forks through fork() / join() keep their identity and priority at replay).
+    Replay with .replay() from any current stream (the segments launch on their own streams)."""
     if not torch.cuda.is_available():
         raise RuntimeError("hipGraph capture needs a GPU")
-    s = stream or torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
+    main.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(main):
         for _ in range(warmup):
             fn()
-    torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph(keep_graph=True)
-    _SIDE_NODES = set()
-    try:
-        with torch.cuda.graph(g, pool=pool, stream=s):
-            out = fn()
-        side = _SIDE_NODES
-    finally:
-        _SIDE_NODES = None
+    cap = SegmentedCapture(main)
+    out = cap.capture(fn)
     torch.cuda.synchronize()
-    g.instantiate()
-    hip = _hip()
-    lo, hi = torch.cuda.Stream.priority_range()
-    raw = g.raw_cuda_graph()
-    info = {"kernel_nodes": 0, "side_kernel_nodes": 0, "set_rc": {}}
-    ok = True
-    for nd in graph_nodes(raw):
-        t = ctypes.c_int(-1)
-        hip.hipGraphNodeGetType(_P(nd), ctypes.byref(t))
-        if t.value != _KERNEL_NODE:
-            continue
-        info["kernel_nodes"] += 1
-        is_side = nd in side
-        info["side_kernel_nodes"] += int(is_side)
-        v = (ctypes.c_char * 64)()
-        ctypes.cast(v, ctypes.POINTER(ctypes.c_int))[0] = lo if is_side else hi
-        rc = hip.hipGraphKernelNodeSetAttribute(_P(nd), _ATTR_PRIORITY, v)
-        info["set_rc"][rc] = info["set_rc"].get(rc, 0) + 1
-        ok = ok and rc == 0
-    ex = None
-    if ok and info["kernel_nodes"]:
-        e = _P(0)
-        rc = hip.hipGraphInstantiateWithFlags(ctypes.byref(e), _P(raw), ctypes.c_ulonglong(_FLAG_USE_NODE_PRIORITY))
-        info["instantiate_rc"] = rc
-        if rc == 0:
-            ex = e.value
-    info["set_rc"] = {str(k): v for k, v in info["set_rc"].items()}
-    return PrioritizedStep(g, out, ex, info)
+    return SegmentedStep(cap, out)
+
+
+def fork(src, dst):
+    """dst orders after the work already queued on src (a torch event outside segmented capture)."""
+    if _SEG is not None:
+        _SEG.fork(src, dst)
+        return
+    ev = torch.cuda.Event()
+    ev.record(src)
+    dst.wait_event(ev)
+
+
+def join(dst, src):
+    """dst (the main stream) orders after everything queued on src."""
+    if _SEG is not None:
+        _SEG.join(dst, src)
+        return
+    dst.wait_stream(src)
+
+
+def mark(src):
+    """A point of src's queued work that join_mark() can wait for later."""
+    if _SEG is not None:
+        return _SEG.mark(src)
+    ev = torch.cuda.Event()
+    ev.record(src)
+    return ev
+
+
+def join_mark(dst, m):
+    if _SEG is not None:
+        _SEG.wait_mark(dst, m)
+        return
+    dst.wait_event(m)
+
+
+def capturing_segmented() -> bool:
+    return _SEG is not None

@@ -148,6 +148,45 @@ def test_resnet_step_hipgraph_replay_matches_eager():
 
 
 @pytest.mark.gpu
+def test_resnet_step_segmented_capture_matches_eager():
+    """The bench's capture: the two-stream step recorded as per-stream linear graph segments
+    (event record / wait nodes at every fork and join) and replayed on the eager streams must
+    reproduce the eager steps."""
+    from tensorflow_train_distributed_amd.train.flat import FlatSGD, Schedule
+    from tensorflow_train_distributed_amd.utils import graphs
+
+    def make():
+        m = ResNet(((64, 1, 1), (128, 2, 2)), num_classes=10, device="cuda", seed=5)
+        o = FlatSGD(m.params, Schedule(kind=2, base_lr=0.1, warmup_steps=2, end_lr=0.0, power=2.0,
+                                       total_steps=100), momentum=0.9, weight_decay=5e-5)
+        return m, o
+
+    torch.manual_seed(0)
+    x = torch.randn(16, 32, 32, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (16,), device="cuda", dtype=torch.int32)
+    m1, o1 = make()
+    m2, o2 = make()
+    assert m2.wgrad_stream and m2.cd_side
+
+    def step(m, o):
+        s = m.forward_backward(x, y)
+        o.step()
+        return s
+
+    eager = [step(m1, o1).clone() for _ in range(5)]
+    main = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
+    seg = graphs.capture_segmented(lambda: step(m2, o2), main=main, warmup=1)  # warmup = step 1
+    assert seg.info["streams"] == 2 and seg.info["segments"] >= 4, seg.info
+    replays = [seg.replay().clone() for _ in range(4)]  # steps 2..5
+    torch.cuda.synchronize()
+    for a, b in zip(eager[1:], replays):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-3)
+    d = (m1.params.master - m2.params.master).abs().max()
+    assert float(d) < 1e-3 * float(m1.params.master.abs().max()), float(d)
+    assert int(o1.step_t) == int(o2.step_t) == 5
+
+
+@pytest.mark.gpu
 def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
     """precision="fp8": the 3x3 convs with 128-multiple input channels run the fp8 block-scaled
     MFMA forward with delayed activation scaling; the step must track the bf16 engine and train
