@@ -248,9 +248,16 @@ class SegmentedCapture:
         return out
 
     def replay(self):
+        # ordered after the caller's stream and before its next work (the side streams fork from
+        # and join main inside the segments)
+        cur = torch.cuda.current_stream()
+        if cur != self.main:
+            self.main.wait_stream(cur)
         for s, g in self.segments:
             with torch.cuda.stream(s):
                 g.replay()
+        if cur != self.main:
+            cur.wait_stream(self.main)
 
 
 class SegmentedStep:
@@ -270,7 +277,8 @@ class SegmentedStep:
 def capture_segmented(fn: Callable[[], Any], main: torch.cuda.Stream, warmup: int = 1) -> SegmentedStep:
     """Run `fn` `warmup` times eagerly on `main`, then record it as per-stream graph segments
     (the streams it forks through fork() / join() keep their identity and priority at replay).
-    Replay with .replay() from any current stream (the segments launch on their own streams)."""
+    .replay() may be called from any stream: the segments launch on their own streams, ordered
+    after the caller's earlier work and before its later work."""
     if not torch.cuda.is_available():
         raise RuntimeError("hipGraph capture needs a GPU")
     main.wait_stream(torch.cuda.current_stream())
