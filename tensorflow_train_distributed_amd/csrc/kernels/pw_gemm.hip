@@ -50,7 +50,23 @@ struct Pro {
   bf16_t* side;          // transformed operand written back (slice 0), or null
   uint8_t* side_mask;    // PRO 1: ReLU bit mask of `side`, or null
   int relu;
+  const bf16_t* xw;      // WG: the conv input X [M][N] (row stride N)
+  float* wslab;          // WG: per-workgroup weight-gradient partials [gridDim.x][K][N]
 };
+
+// Transposed MFMA operand from a K-major [rows][64] tile image (kmaj_off layout): operand row =
+// image column colbase + (lane & 15), its 8 K-values = image rows ms*32 + 8*(lane >> 4) + 0..7
+// (the mn_frag pattern of gemm_conv.h on this image's swizzle; ds_read_b64_tr_b16).
+__device__ __forceinline__ bf16x8_t kmaj_tr_frag(const char* lds, int colbase, int ms, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int r = ms * 32 + 8 * g + q;
+  const int col = colbase + 4 * p;
+  const s16x4_t lo = lds_read_tr(lds + kmaj_off(r, col >> 3) + (col & 7) * 2);
+  const s16x4_t hi = lds_read_tr(lds + kmaj_off(r + 4, col >> 3) + (col & 7) * 2);
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
 
 __device__ __forceinline__ void load8f(const float* p, float (&d)[8]) {
   const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p), c = *reinterpret_cast<const f32x4_t*>(p + 4);
@@ -88,9 +104,17 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 // fly under the prologue / MFMA / staging instead of being loaded row batch by row batch in
 // registers (the register epilogue ran the short-K dgrads at ~3.5 TB/s). by2 / residual are not
 // supported there (the host picks DMA only without them).
-template <int K, int BN, int BM, int PRO, int WM, bool DMA>
+// WG = true (PRO 2, one column slice: BN == N): the same conv's WEIGHT gradient is fused in.
+// dW[K][N] = A'^T . X with A' = the dz tile already in LDS (never stored to HBM) and X the conv
+// input tile (register-staged beside A, K-major image in LDS); each workgroup keeps its dW
+// partial (32 fp32 per lane: waves in a (K/32) x (N/64) grid, 32 x 64 each) over all its tiles
+// and stores it once as slab blockIdx.x of pa.wslab; the host folds the slabs. This removes the
+// dz store and the separate weight-gradient pass's re-read of dz and X.
+template <int K, int BN, int BM, int PRO, int WM, bool DMA, bool WG = false>
 __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __restrict__ w, long long ldw, EpiParams E,
                                                    int M, int N, int tiles_m, int nslices) {
+  static_assert(!WG || (PRO == 2 && K % 32 == 0 && BN % 64 == 0 && (K / 32) * (BN / 64) == NW),
+                "fused weight gradient: BN-bwd prologue, (K/32) x (BN/64) = 8 wave tiles of 32 x 64");
   constexpr int WN = NW / WM;
   constexpr int WR = BM / WM, WC = BN / WN;  // rows / cols per wave
   constexpr int TM = WR / 16, TN = WC / 16;
@@ -107,13 +131,20 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
   constexpr int SAE = SA > SE ? SA : SE;
   constexpr int SDT = DMA ? BM * BN * 2 : 0;  // one bf16 epilogue-input tile
   constexpr int SD = DMA ? 2 * SDT + BM * BN / 8 : 0;
-  static_assert(SB + SAE + SD <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[SB + SAE + SD];
+  // WG: X tile image (BM x BN, BN/64 sub-tiles of BM x 128 B); it lives in the epilogue-staging
+  // tail of the A region when that is large enough (the staging is written only after the
+  // weight-gradient MFMAs), else after the DMA region
+  constexpr int SX = WG ? BM * BN * 2 : 0;
+  constexpr bool XALIAS = WG && SE - SA >= SX;
+  constexpr int SXE = WG && !XALIAS ? SX : 0;
+  static_assert(SB + SAE + SD + SXE <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[SB + SAE + SD + SXE];
   char* const sB = smem;
   char* const sA = smem + SB;  // A tile; the epilogue staging aliases it
   char* const sDo = smem + SB + SAE;  // DMA: old `out` (beta), `by`, ReLU bits
   char* const sDy = sDo + SDT;
   char* const sDm = sDo + 2 * SDT;
+  char* const sX = XALIAS ? sA + SA : smem + SB + SAE + SD;
 
   const int b = blockIdx.x;
   const int xcd = b & 7, rq = b >> 3;
@@ -153,8 +184,27 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
 
   uint4 ra[NA], rx[NA];
   uint32_t rm[NA];
+  constexpr int XCPR = BN / 8;                          // 16-B chunks per X row
+  constexpr int NXL = WG ? (BM * XCPR) / THR : 1;       // X chunks per thread per tile
+  static_assert(!WG || (BM * XCPR) % THR == 0, "X tile mapping");
+  uint4 rw[NXL];
+  f32x4_t wacc[WG ? 2 : 1][WG ? 4 : 1];
+  if constexpr (WG) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wacc[a][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
   auto load_tile = [&](int t) {
     const long long m0 = static_cast<long long>(t) * BM;
+    if constexpr (WG) {
+#pragma unroll
+      for (int i = 0; i < NXL; ++i) {
+        const int q = tid + THR * i;
+        const long long row = m0 + q / XCPR;
+        rw[i] = row < M ? ldg16(pa.xw + row * BN + (q % XCPR) * 8) : make_uint4(0, 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const long long row = m0 + ar + APASS * i;
@@ -171,6 +221,14 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
   };
   auto stage_tile = [&](int t) {
     const long long m0 = static_cast<long long>(t) * BM;
+    if constexpr (WG) {
+#pragma unroll
+      for (int i = 0; i < NXL; ++i) {
+        const int q = tid + THR * i;
+        const int row = q / XCPR, cc = q % XCPR;
+        *reinterpret_cast<uint4*>(sX + (cc >> 3) * (BM * 128) + kmaj_off(row, cc & 7)) = rw[i];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int lrow = ar + APASS * i;
@@ -292,6 +350,30 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
           for (int c = 0; c < TN; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[c], af[a], acc[a][c], 0, 0, 0);
       }
     }
+    if constexpr (WG) {
+      // dW[k][n] += sum over this tile's rows of dz[m][k] * X[m][n]: lane holds n = 4g + i of
+      // each 16-block, k = lane & 15 (rows past M are zero in both images)
+      constexpr int WGN = BN / 64;
+      const int wk = wave / WGN, wx = wave % WGN;
+#pragma unroll
+      for (int ms = 0; ms < BM / 32; ++ms) {
+        bf16x8_t kf[2], nf[4];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int kc = wk * 32 + a * 16;
+          kf[a] = kmaj_tr_frag(sA + (kc >> 6) * (BM * 128), kc & 63, ms, lane);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int nc = wx * 64 + c * 16;
+          nf[c] = kmaj_tr_frag(sX + (nc >> 6) * (BM * 128), nc & 63, ms, lane);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) wacc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[c], kf[a], wacc[a][c], 0, 0, 0);
+      }
+    }
     __syncthreads();  // every wave is done reading sA: stage the tile over it
     const int m0 = t * BM;
     const int gq4 = lane >> 4, i16 = lane & 15;
@@ -405,6 +487,18 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
     }
     __syncthreads();  // staging / statistics reads done before the next tile overwrites sA
   }
+  if constexpr (WG) {
+    constexpr int WGN = BN / 64;
+    const int wk = wave / WGN, wx = wave % WGN;
+    float* slab = pa.wslab + static_cast<long long>(blockIdx.x) * K * BN;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = wk * 32 + a * 16 + (lane & 15), n = wx * 64 + c * 16 + 4 * (lane >> 4);
+        *reinterpret_cast<f32x4_t*>(slab + k * BN + n) = wacc[a][c];
+      }
+  }
 }
 
 // (K, N) -> tile: BN (column slice kept in LDS), BM (rows per tile), DMA epilogue; 0 = not
@@ -439,16 +533,40 @@ inline Cfg pick(int N, int K, bool dma) {
   }
 }
 
-template <int K, int BN, int BM, int PRO, int WM, bool DMA>
-hipError_t launch(const Pro& pa, const bf16_t* w, long long ldw, const EpiParams& E, int M, int N, hipStream_t st) {
+inline int grid_for(int M, int N, int BN, int BM) {
   const int nsl = ceil_div(N, BN), tiles = ceil_div(M, BM);
   int gq = big::device_cus() / (8 * nsl);  // one persistent workgroup per (free) CU in all
   if (gq < 1) gq = 1;
   const int need = ceil_div(tiles, 8);
   if (gq > need) gq = need;
-  hipLaunchKernelGGL((pw_kernel<K, BN, BM, PRO, WM, DMA>), dim3(8 * nsl * gq), dim3(THR), 0, st, pa, w, ldw, E, M, N,
+  return 8 * nsl * gq;
+}
+
+template <int K, int BN, int BM, int PRO, int WM, bool DMA, bool WG = false>
+hipError_t launch(const Pro& pa, const bf16_t* w, long long ldw, const EpiParams& E, int M, int N, hipStream_t st,
+                  int grid = 0) {
+  const int nsl = ceil_div(N, BN), tiles = ceil_div(M, BM);
+  if (grid <= 0) grid = grid_for(M, N, BN, BM);
+  hipLaunchKernelGGL((pw_kernel<K, BN, BM, PRO, WM, DMA, WG>), dim3(grid), dim3(THR), 0, st, pa, w, ldw, E, M, N,
                      tiles, nsl);
   return hipGetLastError();
+}
+
+// The fused data + weight gradient (WG) instantiations: the (K, N) = (256, 64) and (64, 256)
+// stage-2 shapes (one column slice, K * N = 16384).
+inline hipError_t dispatch_wg(const Pro& pa, const bf16_t* w, long long ldw, const EpiParams& E, int M, int N, int K,
+                              bool dma, int grid, hipStream_t st) {
+  const Cfg c = pick(N, K, dma);
+  if (c.bn != N) return hipErrorInvalidValue;
+#define PW_WG_CASE(K_, BN_, BM_, WM_, D_)                     \
+  if (K == K_ && c.bn == BN_ && c.bm == BM_ && c.dma == D_) \
+    return launch<K_, BN_, BM_, 2, WM_, D_, true>(pa, w, ldw, E, M, N, st, grid);
+  PW_WG_CASE(64, 256, 128, 2, false)
+  PW_WG_CASE(256, 64, 128, 4, false)
+  PW_WG_CASE(64, 256, 64, 2, true)
+  PW_WG_CASE(256, 64, 128, 4, true)
+#undef PW_WG_CASE
+  return hipErrorInvalidValue;
 }
 
 template <int PRO>
@@ -487,6 +605,13 @@ using namespace ttdk;
 // for an N x K pointwise conv, or 0 when the shape is not handled by the streaming kernel.
 TTDK_EXPORT int ttdk_pw_rows(int N, int K, int dma) { return pw::pick(N, K, dma != 0).bm; }
 
+// Workgroups (= weight-gradient slabs) of ttdk_pw_conv_wgrad for this shape; 0 = not fusable.
+TTDK_EXPORT int ttdk_pw_wgrad_slabs(int M, int N, int K, int dma) {
+  const pw::Cfg c = pw::pick(N, K, dma != 0);
+  if (c.bm == 0 || c.bn != N || K * N != 16384 || K % 32 || N % 64) return 0;
+  return pw::grid_for(M, N, c.bn, c.bm);
+}
+
 // out[M, N] = epilogue( A'[M, K] . w[N, K]^T ) with A' from the prologue `pro` (see above).
 // x, x2: [M][K] bf16 (row stride K); mask_in: bits of x (pro 2); s/b/rs/rb: BN coefficients
 // (pro 1: scale, shift, residual scale/shift; pro 2: s = coef[3][K]); side/side_mask: where the
@@ -504,7 +629,7 @@ TTDK_EXPORT int ttdk_pw_conv(const bf16_t* x, const bf16_t* x2, const uint8_t* m
   if (pro == 1 && (!s || !b || (rs && (!rb || !x2)))) return hipErrorInvalidValue;
   if (pro == 2 && (!s || !x2)) return hipErrorInvalidValue;
   if (side_mask && pro != 1) return hipErrorInvalidValue;
-  const pw::Pro pa{x, x2, mask_in, s, b, rs, rb, side, side_mask, relu};
+  const pw::Pro pa{x, x2, mask_in, s, b, rs, rb, side, side_mask, relu, nullptr, nullptr};
   switch (pro) {
     case 0:
       return pw::dispatch<0>(pa, w, ldw, e, M, N, K, dma, st);
@@ -513,4 +638,22 @@ TTDK_EXPORT int ttdk_pw_conv(const bf16_t* x, const bf16_t* x2, const uint8_t* m
     default:
       return pw::dispatch<2>(pa, w, ldw, e, M, N, K, dma, st);
   }
+}
+
+// ttdk_pw_conv with pro = 2 (BN backward as the operand prologue) and the conv's weight gradient
+// fused in (see pw_kernel WG): dx = epilogue(dz . w^T) as ttdk_pw_conv, dw[K][N] (fp32, += when
+// beta_w) = dz^T . xw with dz never stored; ws: ttdk_pw_wgrad_slabs(M, N, K, dma) * K * N floats.
+TTDK_EXPORT int ttdk_pw_conv_wgrad(const bf16_t* g, const bf16_t* y, const uint8_t* mask_in, const float* coef,
+                                   const bf16_t* xw, const bf16_t* w, long long ldw, int M, int N, int K,
+                                   const TtdkEpilogue* epi, float* dw, float* ws, int beta_w, hipStream_t st) {
+  const EpiParams e = to_epi(epi);
+  const bool dma = (e.beta || e.by) && !e.residual && !e.by2 && e.act == 0 && !e.bias;
+  const int slabs = ttdk_pw_wgrad_slabs(M, N, K, dma);
+  if (!slabs || !g || !y || !coef || !xw || !dw || !ws || ldw % 8 || (reinterpret_cast<uintptr_t>(g) & 15) ||
+      (reinterpret_cast<uintptr_t>(xw) & 15) || e.mode != 0 || e.remap || e.ldo % 8 || (e.residual && e.ldr % 8))
+    return hipErrorInvalidValue;
+  const pw::Pro pa{g, y, mask_in, coef, nullptr, nullptr, nullptr, nullptr, nullptr, 1, xw, ws};
+  hipError_t r = pw::dispatch_wg(pa, w, ldw, e, M, N, K, dma, slabs, st);
+  if (r != hipSuccess) return r;
+  return splitk_reduce(ws, slabs, static_cast<long long>(K) * N, dw, beta_w, st);
 }

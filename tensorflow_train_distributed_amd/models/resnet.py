@@ -122,6 +122,10 @@ class ResNet:
         # (256-row kernel operand prologue, stores h + ReLU bits): no BN apply pass for the
         # stage-3/4 blocks the streaming pointwise kernel does not take; TTD_FWD_BNPRO=0: off
         self.fwd_pro = os.environ.get("TTD_FWD_BNPRO", "1") != "0"
+        # the streaming-kernel data gradients with the BN-backward prologue (stage-2 c1 / c3) also
+        # form their conv's weight gradient from the dz tile in LDS (pw_gemm.hip WG); 0: separate
+        # side-stream weight-gradient pass over a stored dz
+        self.pw_wgrad = os.environ.get("TTD_PW_WGRAD", "1") != "0"
         # stem weight gradient on its dedicated kernel (3 real input channels, BN backward on the fly)
         self.stem_kernel = os.environ.get("TTD_STEM_WGRAD", "1") != "0"
         # dedicated stem forward kernel (stem_fwd.hip: K = 7 x 32 over the 3 real channels)
@@ -443,10 +447,18 @@ class ResNet:
             # kernel): dz is written once there for the weight gradient, never re-read by the dgrad
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
-            dz = torch.empty_like(y)
             wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
             _, fy, fmask, _ = feeds
             bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
+            if self.pw_wgrad and G.pw_wgrad_fusable(M, c.cin_store, Kc):
+                # ... and the weight gradient in the same kernel, from the dz tile in LDS: dz is
+                # never stored, the side-stream pass re-reading dz and x disappears
+                out, partial, T = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None), bn_stat=(fy, fmask),
+                                            out=dx, beta=dx_beta if dx is not None else 0, beta_s2=bs2,
+                                            wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
+                self._ready_main(c.name + "_bn/moving_variance")
+                return out, (partial, T)
+            dz = torch.empty_like(y)
             out, partial, T = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, dz), bn_stat=(fy, fmask),
                                         out=dx, beta=dx_beta if dx is not None else 0, beta_s2=bs2)
             self._wgrad(c, x, dz, wname)
@@ -555,6 +567,20 @@ class ResNet:
 
     def _ready(self, name):
         if self._grad_hook is not None:
+            self._grad_hook(name)
+
+    def _ready_main(self, name):
+        """Gradient-ready hook for a gradient produced on the main stream: issued from the side
+        stream after a fork, so the bucket it completes also orders after the side-stream
+        weight gradients queued before it (flat-layout order)."""
+        side = self._wgrad_stream
+        if self._grad_hook is None:
+            return
+        if side is None:
+            self._grad_hook(name)
+            return
+        graphs.fork(torch.cuda.current_stream(), side)
+        with torch.cuda.stream(side):
             self._grad_hook(name)
 
     def forward_backward(self, images, labels, grad_scale: Optional[float] = None, grad_hook=None):

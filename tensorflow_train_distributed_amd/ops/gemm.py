@@ -286,8 +286,13 @@ def pw_ok(M, N, K):
     return _PW and pw_rows(N, K) > 0 and N * K <= 65536
 
 
+def pw_wgrad_fusable(M, N, K, dma=True):
+    """ops.gemm.pw_conv(..., wgrad=...) takes this (dz channels K, dx channels N) shape."""
+    return _PW and int(_lib.query("ttdk_pw_wgrad_slabs", int(M), int(N), int(K), int(bool(dma)))) > 0
+
+
 def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None, bn_stat=None, bn_stat2=None,
-            beta_s2=None):
+            beta_s2=None, wgrad=None):
     """Unit-stride 1x1 conv / dense GEMM out[M, N] = A'[M, K] . w[N, K]^T on the persistent
     streaming kernel (pw_gemm.hip), A' = prologue(x):
 
@@ -301,7 +306,10 @@ def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None,
     stat=True: also per-tile BN partial sums of the stored output -> returns (out, partial, T).
     bn_stat=(y, mask) [+ bn_stat2=y2]: dgrad-style ReLU-masked gradient + BN-backward sums of the
     consuming unit (see conv_dgrad) -> returns (out, partial, T[, partial2]).
-    beta / residual / beta_s2: as conv_dgrad / gemm."""
+    beta / residual / beta_s2: as conv_dgrad / gemm.
+    wgrad=(xw, dw[, beta_w]) with the "bn_bwd" prologue (its side None): the same conv's weight
+    gradient dw[K, N] (fp32; += when beta_w) = dz^T . xw is formed in the kernel from the dz tile
+    in LDS (dz is never stored); xw: the conv input, bf16 [..., N] (pw_gemm.hip pw_kernel WG)."""
     _check(x, torch.bfloat16, "x")
     _check(w, torch.bfloat16, "w")
     K = x.shape[-1]
@@ -340,6 +348,26 @@ def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None,
         else:
             raise ValueError("pw_conv: unknown prologue %r" % (prologue[0],))
     _log("pw_%s" % ("fwd" if pro != 2 else "dgrad"), M, N, K)
+    if wgrad is not None:
+        xw, dw = wgrad[0], wgrad[1]
+        beta_w = int(wgrad[2]) if len(wgrad) > 2 else 0
+        if pro != 2 or side is not None:
+            raise ValueError("pw_conv: wgrad= needs the bn_bwd prologue without a dz store")
+        _check(xw, torch.bfloat16, "wgrad x")
+        if xw.numel() != M * N or dw.dtype != torch.float32 or dw.numel() != K * N or not dw.is_contiguous():
+            raise ValueError("pw_conv: wgrad x must be [M, N] = [%d, %d] bf16 and dw [K, N] fp32" % (M, N))
+        slabs = int(_lib.query("ttdk_pw_wgrad_slabs", M, N, K, int(dma)))
+        if slabs <= 0:
+            raise ValueError("pw_conv: N=%d K=%d has no fused weight-gradient kernel" % (N, K))
+        _log("pw_wgrad", K, N, M)
+        ws = torch.empty(slabs * K * N, dtype=torch.float32, device=x.device)
+        _lib.call("ttdk_pw_conv_wgrad", x.data_ptr(), P(x2), P(mask_in), P(s), xw.data_ptr(), w.data_ptr(), K, M, N,
+                  K, ctypes.byref(e), dw.data_ptr(), ws.data_ptr(), beta_w, _lib.stream())
+        if partial is None:
+            return out
+        if partial2 is not None:
+            return out, partial, T, partial2
+        return out, partial, T
     _lib.call("ttdk_pw_conv", x.data_ptr(), P(x2), P(mask_in), P(s), P(b), P(rs), P(rb), P(side), P(side_mask), 1, pro,
               w.data_ptr(), K, M, N, K, ctypes.byref(e), _lib.stream())
     if partial is None:

@@ -105,3 +105,41 @@ def test_pw_bn_backward_prologue_matches_dgrad_path(K, N, second):
     assert rel < 2e-2, rel
     for a, b in zip((got[1],) + ((got[3],) if second else ()), (r[1],) + ((r[3],) if second else ())):
         torch.testing.assert_close(a.sum(0), b.sum(0), rtol=2e-2, atol=2.0)
+
+
+@pytest.mark.parametrize("K,N,dgrad_epi", [(256, 64, True), (64, 256, True), (256, 64, False), (64, 256, False)])
+def test_pw_bn_backward_prologue_fused_weight_gradient(K, N, dgrad_epi):
+    """wgrad=(x, dw): the weight gradient formed from the dz tile in LDS (dz never stored) equals
+    the fp32 dz^T . x of the dz the unfused kernel stores, and the data gradient / statistics
+    are the unfused kernel's, bit for bit (same kernel body)."""
+    G, _ = _ops()
+    Nimg, H, W = 6, 28, 28
+    M = Nimg * H * W - 37  # ragged last tile
+    g = _rand((M, K), seed=12)
+    y = _rand((M, K), seed=13)
+    bits = torch.randint(0, 256, (M * K // 8,), dtype=torch.uint8, device="cuda")
+    coef = torch.randn(3, K, device="cuda") * torch.tensor([[1.0], [0.1], [0.05]], device="cuda")
+    wt = _rand((N, K), scale=K ** -0.5, seed=14)  # dgrad B operand [C=N][K]
+    x = _rand((M, N), seed=15)                   # the conv input
+    assert G.pw_wgrad_fusable(M, N, K, dgrad_epi)
+    kw = {}
+    if dgrad_epi:
+        kw = dict(beta=1, bn_stat=(_rand((M, N), seed=16), torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8,
+                                                                          device="cuda")))
+    acc0 = _rand((M, N), seed=17)
+    side = torch.empty_like(g)
+    out_a = acc0.clone()
+    ra = G.pw_conv(g, wt, prologue=("bn_bwd", y, bits, coef, side), out=out_a, **kw)
+    out_b = acc0.clone()
+    dw = torch.full((K, N), float("nan"), device="cuda")
+    rb = G.pw_conv(g, wt, prologue=("bn_bwd", y, bits, coef, None), out=out_b, wgrad=(x, dw), **kw)
+    dw2 = torch.ones((K, N), device="cuda")
+    G.pw_conv(g, wt, prologue=("bn_bwd", y, bits, coef, None), out=acc0.clone(), wgrad=(x, dw2, 1), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(out_a, out_b)
+    if dgrad_epi:
+        assert torch.equal(ra[1], rb[1])
+    ref = side.float().t() @ x.float()
+    rel = (dw - ref).abs().max() / ref.abs().max()
+    assert rel < 1e-3, rel
+    torch.testing.assert_close(dw2, ref + 1.0, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Time the GEMM kernels on the shapes that matter (random bf16 operands):
 4-wave 128x128 kernel (tile=(128,128)) vs the 256x256 LDS-DMA kernel (tile=(256,256)),
-plus torch.matmul (hipBLASLt) as a yardstick. Prints TF/s."""
+plus torch.matmul (hipBLASLt) as a yardstick. Prints TF/s.
+usage: gemm_bench.py [--tokens T (BERT rows, default 16384)] [--only SUBSTR]"""
 import sys
 
 import torch
@@ -9,7 +10,8 @@ import torch
 sys.path.insert(0, ".")
 from tensorflow_train_distributed_amd.ops import gemm as G  # noqa: E402
 
-T = 16384
+T = int(sys.argv[sys.argv.index("--tokens") + 1]) if "--tokens" in sys.argv else 16384
+ONLY = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
 SHAPES = [  # (name, M, N, K, trans_a, trans_b)
     ("sq4096_nt", 4096, 4096, 4096, False, True),
     ("sq8192_nt", 8192, 8192, 8192, False, True),
@@ -48,6 +50,8 @@ def timeit(fn, iters=20):
 
 def main():
     for name, M, N, K, ta, tb in SHAPES:
+        if ONLY and ONLY not in name:
+            continue
         a = (torch.rand((K, M) if ta else (M, K), device="cuda") * 2 - 1).bfloat16()
         b = (torch.rand((N, K) if tb else (K, N), device="cuda") * 2 - 1).bfloat16()
         fl = 2.0 * M * N * K
