@@ -441,6 +441,18 @@ class ResNet:
                 graphs.join(torch.cuda.current_stream(), self._wgrad_stream)
             self._ready(c.name + "_bn/moving_variance")
             return None, None
+        if (need_dx and wgrad_last and dstat is not None and feeds is None and dx is None and not sampled_only
+                and self.fuse_bn_bwd and self.pw_wgrad and self._pw_part("dgrad") and self._pw_dgrad_ok(c)
+                and G.pw_wgrad_fusable(M, c.cin_store, Kc, False)):
+            # the unit-stride projection shortcut (stage 2): BN backward, data and weight gradient
+            # in one streaming kernel (no dz pass, no dz store, no weight-gradient re-read)
+            coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
+                                      dstat[0], dstat[1])
+            wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
+            out = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None),
+                            wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
+            self._cd_done = graphs.mark(torch.cuda.current_stream())
+            return out, None
         if (need_dx and dstat is not None and feeds is not None and feeds2 is None
                 and self.fuse_bn_bwd and self._pw_part("dgrad") and self._pw_dgrad_ok(c)):
             # BN backward applied inside the data gradient's operand load (streaming pointwise
