@@ -107,14 +107,18 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 // WG = true (PRO 2, one column slice: BN == N): the same conv's WEIGHT gradient is fused in.
 // dW[K][N] = A'^T . X with A' = the dz tile already in LDS (never stored to HBM) and X the conv
 // input tile (register-staged beside A, K-major image in LDS); each workgroup keeps its dW
-// partial (32 fp32 per lane: waves in a (K/32) x (N/64) grid, 32 x 64 each) over all its tiles
+// partial (waves in a (K/32) x (N/(16*WNB)) grid, 32 x 16*WNB each; 32 fp32 per lane at
+// K * N = 16384) over all its tiles
 // and stores it once as slab blockIdx.x of pa.wslab; the host folds the slabs. This removes the
 // dz store and the separate weight-gradient pass's re-read of dz and X.
 template <int K, int BN, int BM, int PRO, int WM, bool DMA, bool WG = false>
 __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __restrict__ w, long long ldw, EpiParams E,
                                                    int M, int N, int tiles_m, int nslices) {
-  static_assert(!WG || (PRO == 2 && K % 32 == 0 && BN % 64 == 0 && (K / 32) * (BN / 64) == NW),
-                "fused weight gradient: BN-bwd prologue, (K/32) x (BN/64) = 8 wave tiles of 32 x 64");
+  // weight-gradient wave tiles: 32 k x (16 * WNB) n, 8 of them covering K x BN
+  constexpr int WNB = WG ? (K * BN) / (NW * 32 * 16) : 1;
+  constexpr int WGN = BN / (16 * WNB);
+  static_assert(!WG || (PRO == 2 && K % 32 == 0 && WNB >= 1 && BN % (16 * WNB) == 0 && (K / 32) * WGN == NW),
+                "fused weight gradient: BN-bwd prologue, (K/32) x (BN/(16*WNB)) = 8 wave tiles");
   constexpr int WN = NW / WM;
   constexpr int WR = BM / WM, WC = BN / WN;  // rows / cols per wave
   constexpr int TM = WR / 16, TN = WC / 16;
@@ -188,12 +192,12 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
   constexpr int NXL = WG ? (BM * XCPR) / THR : 1;       // X chunks per thread per tile
   static_assert(!WG || (BM * XCPR) % THR == 0, "X tile mapping");
   uint4 rw[NXL];
-  f32x4_t wacc[WG ? 2 : 1][WG ? 4 : 1];
+  f32x4_t wacc[WG ? 2 : 1][WNB];
   if constexpr (WG) {
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) wacc[a][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < WNB; ++c) wacc[a][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
   auto load_tile = [&](int t) {
     const long long m0 = static_cast<long long>(t) * BM;
@@ -353,25 +357,24 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
     if constexpr (WG) {
       // dW[k][n] += sum over this tile's rows of dz[m][k] * X[m][n]: lane holds n = 4g + i of
       // each 16-block, k = lane & 15 (rows past M are zero in both images)
-      constexpr int WGN = BN / 64;
       const int wk = wave / WGN, wx = wave % WGN;
 #pragma unroll
       for (int ms = 0; ms < BM / 32; ++ms) {
-        bf16x8_t kf[2], nf[4];
+        bf16x8_t kf[2], nf[WNB];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           const int kc = wk * 32 + a * 16;
           kf[a] = kmaj_tr_frag(sA + (kc >> 6) * (BM * 128), kc & 63, ms, lane);
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int nc = wx * 64 + c * 16;
+        for (int c = 0; c < WNB; ++c) {
+          const int nc = wx * (16 * WNB) + c * 16;
           nf[c] = kmaj_tr_frag(sX + (nc >> 6) * (BM * 128), nc & 63, ms, lane);
         }
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) wacc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[c], kf[a], wacc[a][c], 0, 0, 0);
+          for (int c = 0; c < WNB; ++c) wacc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[c], kf[a], wacc[a][c], 0, 0, 0);
       }
     }
     __syncthreads();  // every wave is done reading sA: stage the tile over it
@@ -488,14 +491,13 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
     __syncthreads();  // staging / statistics reads done before the next tile overwrites sA
   }
   if constexpr (WG) {
-    constexpr int WGN = BN / 64;
     const int wk = wave / WGN, wx = wave % WGN;
     float* slab = pa.wslab + static_cast<long long>(blockIdx.x) * K * BN;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int k = wk * 32 + a * 16 + (lane & 15), n = wx * 64 + c * 16 + 4 * (lane >> 4);
+      for (int c = 0; c < WNB; ++c) {
+        const int k = wk * 32 + a * 16 + (lane & 15), n = wx * (16 * WNB) + c * 16 + 4 * (lane >> 4);
         *reinterpret_cast<f32x4_t*>(slab + k * BN + n) = wacc[a][c];
       }
   }
@@ -553,7 +555,7 @@ hipError_t launch(const Pro& pa, const bf16_t* w, long long ldw, const EpiParams
 }
 
 // The fused data + weight gradient (WG) instantiations: the (K, N) = (256, 64) and (64, 256)
-// stage-2 shapes (one column slice, K * N = 16384).
+// stage-2 shapes (one column slice, K * N = 16384) and the first block's (64, 64) c1.
 inline hipError_t dispatch_wg(const Pro& pa, const bf16_t* w, long long ldw, const EpiParams& E, int M, int N, int K,
                               bool dma, int grid, hipStream_t st) {
   const Cfg c = pick(N, K, dma);
@@ -565,6 +567,8 @@ inline hipError_t dispatch_wg(const Pro& pa, const bf16_t* w, long long ldw, con
   PW_WG_CASE(256, 64, 128, 4, false)
   PW_WG_CASE(64, 256, 64, 2, true)
   PW_WG_CASE(256, 64, 128, 4, true)
+  PW_WG_CASE(64, 64, 128, 4, false)
+  PW_WG_CASE(64, 64, 64, 4, true)
 #undef PW_WG_CASE
   return hipErrorInvalidValue;
 }
@@ -608,7 +612,8 @@ TTDK_EXPORT int ttdk_pw_rows(int N, int K, int dma) { return pw::pick(N, K, dma 
 // Workgroups (= weight-gradient slabs) of ttdk_pw_conv_wgrad for this shape; 0 = not fusable.
 TTDK_EXPORT int ttdk_pw_wgrad_slabs(int M, int N, int K, int dma) {
   const pw::Cfg c = pw::pick(N, K, dma != 0);
-  if (c.bm == 0 || c.bn != N || K * N != 16384 || K % 32 || N % 64) return 0;
+  const bool shape = (K * N == 16384 && N % 64 == 0) || (K == 64 && N == 64);
+  if (c.bm == 0 || c.bn != N || K % 32 || !shape) return 0;
   return pw::grid_for(M, N, c.bn, c.bm);
 }
 

@@ -453,6 +453,20 @@ class ResNet:
                             wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
             self._cd_done = graphs.mark(torch.cuda.current_stream())
             return out, None
+        if (need_dx and dstat is not None and feeds is None and not wgrad_last and not sampled_only and not dx_sampled
+                and self.fuse_bn_bwd and self.pw_wgrad and self._pw_part("dgrad") and self.device.type == "cuda"
+                and c.k == 1 and c.stride == 1 and c.pad == 0
+                and G.pw_wgrad_fusable(M, c.cin_store, Kc, bool(dx is not None and dx_beta))):
+            # a 1x1 unit whose input is not a BN unit's output (stage 2's first c1, fed by the max
+            # pool; accumulating into the projection's gradient): BN backward, data and weight
+            # gradient in one streaming kernel
+            coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
+                                      dstat[0], dstat[1])
+            wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
+            out = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None), out=dx,
+                            beta=dx_beta if dx is not None else 0, wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
+            self._ready_main(c.name + "_bn/moving_variance")
+            return out, None
         if (need_dx and dstat is not None and feeds is not None and feeds2 is None
                 and self.fuse_bn_bwd and self._pw_part("dgrad") and self._pw_dgrad_ok(c)):
             # BN backward applied inside the data gradient's operand load (streaming pointwise

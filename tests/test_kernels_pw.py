@@ -107,7 +107,8 @@ def test_pw_bn_backward_prologue_matches_dgrad_path(K, N, second):
         torch.testing.assert_close(a.sum(0), b.sum(0), rtol=2e-2, atol=2.0)
 
 
-@pytest.mark.parametrize("K,N,dgrad_epi", [(256, 64, True), (64, 256, True), (256, 64, False), (64, 256, False)])
+@pytest.mark.parametrize("K,N,dgrad_epi", [(256, 64, True), (64, 256, True), (256, 64, False), (64, 256, False),
+                                            (64, 64, False), (64, 64, True)])
 def test_pw_bn_backward_prologue_fused_weight_gradient(K, N, dgrad_epi):
     """wgrad=(x, dw): the weight gradient formed from the dz tile in LDS (dz never stored) equals
     the fp32 dz^T . x of the dz the unfused kernel stores, and the data gradient / statistics

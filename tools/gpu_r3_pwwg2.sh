@@ -1,6 +1,6 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_resnet_engine.py > gpurun_out/t_pwwg2.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_pw.py::test_pw_bn_backward_prologue_fused_weight_gradient tests/test_resnet_engine.py > gpurun_out/t_pwwg2.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "PASS|FAIL|Error|error" gpurun_out/t_pwwg2.log | tail -20; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/grad_path_check.py --attr pw_wgrad > gpurun_out/pwwg_check2.json 2>/dev/null || exit 1
 python -c "import json; d=json.load(open('gpurun_out/pwwg_check2.json')); print(d['rel_grad_on_vs_off'], d['cos_on_vs_off'], d['worst_vars'][:6])"
