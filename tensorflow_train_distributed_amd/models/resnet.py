@@ -626,7 +626,10 @@ class ResNet:
         self._side_keep = []
         if self.wgrad_stream:
             if getattr(self, "_side", None) is None:
-                self._side = torch.cuda.Stream(device=self.device)
+                side_cus = int(os.environ.get("TTD_SIDE_CUS", "0"))
+                # TTD_SIDE_CUS > 0: the side stream may only occupy that many CUs (utils.graphs)
+                self._side = (graphs.cu_masked_stream(self.device, side_cus) if side_cus > 0
+                              else torch.cuda.Stream(device=self.device))
             self._wgrad_stream = self._side
         if grad_scale is None:
             grad_scale = 1.0 / N
