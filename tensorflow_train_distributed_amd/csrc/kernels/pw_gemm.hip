@@ -535,9 +535,11 @@ inline Cfg pick(int N, int K, bool dma) {
   }
 }
 
-inline int grid_for(int M, int N, int BN, int BM) {
+inline int grid_for(int M, int N, int BN, int BM, int max_wgs = 0) {
   const int nsl = ceil_div(N, BN), tiles = ceil_div(M, BM);
-  int gq = big::device_cus() / (8 * nsl);  // one persistent workgroup per (free) CU in all
+  int cus = big::device_cus();
+  if (max_wgs > 0 && max_wgs < cus) cus = max_wgs;  // a side-stream launch leaves CUs to the main chain
+  int gq = cus / (8 * nsl);  // one persistent workgroup per (free) CU in all
   if (gq < 1) gq = 1;
   const int need = ceil_div(tiles, 8);
   if (gq > need) gq = need;
@@ -610,11 +612,12 @@ using namespace ttdk;
 TTDK_EXPORT int ttdk_pw_rows(int N, int K, int dma) { return pw::pick(N, K, dma != 0).bm; }
 
 // Workgroups (= weight-gradient slabs) of ttdk_pw_conv_wgrad for this shape; 0 = not fusable.
-TTDK_EXPORT int ttdk_pw_wgrad_slabs(int M, int N, int K, int dma) {
+// max_wgs > 0 caps the persistent grid (a launch on the side stream must not hold every CU).
+TTDK_EXPORT int ttdk_pw_wgrad_slabs(int M, int N, int K, int dma, int max_wgs) {
   const pw::Cfg c = pw::pick(N, K, dma != 0);
   const bool shape = (K * N == 16384 && N % 64 == 0) || (K == 64 && N == 64);
   if (c.bm == 0 || c.bn != N || K % 32 || !shape) return 0;
-  return pw::grid_for(M, N, c.bn, c.bm);
+  return pw::grid_for(M, N, c.bn, c.bm, max_wgs);
 }
 
 // out[M, N] = epilogue( A'[M, K] . w[N, K]^T ) with A' from the prologue `pro` (see above).
@@ -647,13 +650,15 @@ TTDK_EXPORT int ttdk_pw_conv(const bf16_t* x, const bf16_t* x2, const uint8_t* m
 
 // ttdk_pw_conv with pro = 2 (BN backward as the operand prologue) and the conv's weight gradient
 // fused in (see pw_kernel WG): dx = epilogue(dz . w^T) as ttdk_pw_conv, dw[K][N] (fp32, += when
-// beta_w) = dz^T . xw with dz never stored; ws: ttdk_pw_wgrad_slabs(M, N, K, dma) * K * N floats.
+// beta_w) = dz^T . xw with dz never stored; ws: ttdk_pw_wgrad_slabs(M, N, K, dma, max_wgs) * K * N
+// floats.
 TTDK_EXPORT int ttdk_pw_conv_wgrad(const bf16_t* g, const bf16_t* y, const uint8_t* mask_in, const float* coef,
                                    const bf16_t* xw, const bf16_t* w, long long ldw, int M, int N, int K,
-                                   const TtdkEpilogue* epi, float* dw, float* ws, int beta_w, hipStream_t st) {
+                                   const TtdkEpilogue* epi, float* dw, float* ws, int beta_w, int max_wgs,
+                                   hipStream_t st) {
   const EpiParams e = to_epi(epi);
   const bool dma = (e.beta || e.by) && !e.residual && !e.by2 && e.act == 0 && !e.bias;
-  const int slabs = ttdk_pw_wgrad_slabs(M, N, K, dma);
+  const int slabs = ttdk_pw_wgrad_slabs(M, N, K, dma, max_wgs);
   if (!slabs || !g || !y || !coef || !xw || !dw || !ws || ldw % 8 || (reinterpret_cast<uintptr_t>(g) & 15) ||
       (reinterpret_cast<uintptr_t>(xw) & 15) || e.mode != 0 || e.remap || e.ldo % 8 || (e.residual && e.ldr % 8))
     return hipErrorInvalidValue;

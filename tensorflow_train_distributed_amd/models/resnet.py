@@ -126,6 +126,10 @@ class ResNet:
         # form their conv's weight gradient from the dz tile in LDS (pw_gemm.hip WG); 0: separate
         # side-stream weight-gradient pass over a stored dz
         self.pw_wgrad = os.environ.get("TTD_PW_WGRAD", "1") != "0"
+        # cap on the persistent workgroups of that kernel when it runs on the side stream (the
+        # stage-2 projection; 0 = one per CU). It holds every CU while it runs, but the main chain
+        # joins on it right after: 128 / 64 measured 0.3 / 2.1 ms slower per step than the full grid
+        self.side_pw_wgs = int(os.environ.get("TTD_SIDE_PW_WGS", "0"))
         # stem weight gradient on its dedicated kernel (3 real input channels, BN backward on the fly)
         self.stem_kernel = os.environ.get("TTD_STEM_WGRAD", "1") != "0"
         # dedicated stem forward kernel (stem_fwd.hip: K = 7 x 32 over the 3 real channels)
@@ -450,7 +454,7 @@ class ResNet:
                                       dstat[0], dstat[1])
             wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
             out = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None),
-                            wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
+                            wgrad=(x, P.g[wname].view(c.cout, c.cin_store)), max_wgs=self.side_pw_wgs)
             self._cd_done = graphs.mark(torch.cuda.current_stream())
             return out, None
         if (need_dx and dstat is not None and feeds is None and not wgrad_last and not sampled_only and not dx_sampled

@@ -76,8 +76,8 @@ _SIGS = {
     # pw_gemm.hip
     "ttdk_pw_rows": [I, I, I],
     "ttdk_pw_conv": [P, P, P, P, P, P, P, P, P, I, I, P, L, I, I, I, E, P],
-    "ttdk_pw_wgrad_slabs": [I, I, I, I],
-    "ttdk_pw_conv_wgrad": [P, P, P, P, P, P, L, I, I, I, E, P, P, I, P],
+    "ttdk_pw_wgrad_slabs": [I, I, I, I, I],
+    "ttdk_pw_conv_wgrad": [P, P, P, P, P, P, L, I, I, I, E, P, P, I, I, P],
     # batchnorm.hip
     "ttdk_bn_num_partials": [L, I],
     "ttdk_bn_stats_partial": [P, L, I, P, I, P],

@@ -289,11 +289,11 @@ def pw_ok(M, N, K):
 
 def pw_wgrad_fusable(M, N, K, dma=True):
     """ops.gemm.pw_conv(..., wgrad=...) takes this (dz channels K, dx channels N) shape."""
-    return _PW and int(_lib.query("ttdk_pw_wgrad_slabs", int(M), int(N), int(K), int(bool(dma)))) > 0
+    return _PW and int(_lib.query("ttdk_pw_wgrad_slabs", int(M), int(N), int(K), int(bool(dma)), 0)) > 0
 
 
 def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None, bn_stat=None, bn_stat2=None,
-            beta_s2=None, wgrad=None):
+            beta_s2=None, wgrad=None, max_wgs=0):
     """Unit-stride 1x1 conv / dense GEMM out[M, N] = A'[M, K] . w[N, K]^T on the persistent
     streaming kernel (pw_gemm.hip), A' = prologue(x):
 
@@ -310,7 +310,8 @@ def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None,
     beta / residual / beta_s2: as conv_dgrad / gemm.
     wgrad=(xw, dw[, beta_w]) with the "bn_bwd" prologue (its side None): the same conv's weight
     gradient dw[K, N] (fp32; += when beta_w) = dz^T . xw is formed in the kernel from the dz tile
-    in LDS (dz is never stored); xw: the conv input, bf16 [..., N] (pw_gemm.hip pw_kernel WG)."""
+    in LDS (dz is never stored); xw: the conv input, bf16 [..., N] (pw_gemm.hip pw_kernel WG).
+    max_wgs > 0 caps its persistent grid (launches on a side stream next to the main chain)."""
     _check(x, torch.bfloat16, "x")
     _check(w, torch.bfloat16, "w")
     K = x.shape[-1]
@@ -357,13 +358,13 @@ def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None,
         _check(xw, torch.bfloat16, "wgrad x")
         if xw.numel() != M * N or dw.dtype != torch.float32 or dw.numel() != K * N or not dw.is_contiguous():
             raise ValueError("pw_conv: wgrad x must be [M, N] = [%d, %d] bf16 and dw [K, N] fp32" % (M, N))
-        slabs = int(_lib.query("ttdk_pw_wgrad_slabs", M, N, K, int(dma)))
+        slabs = int(_lib.query("ttdk_pw_wgrad_slabs", M, N, K, int(dma), int(max_wgs)))
         if slabs <= 0:
             raise ValueError("pw_conv: N=%d K=%d has no fused weight-gradient kernel" % (N, K))
         _log("pw_wgrad", K, N, M)
         ws = torch.empty(slabs * K * N, dtype=torch.float32, device=x.device)
         _lib.call("ttdk_pw_conv_wgrad", x.data_ptr(), P(x2), P(mask_in), P(s), xw.data_ptr(), w.data_ptr(), K, M, N,
-                  K, ctypes.byref(e), dw.data_ptr(), ws.data_ptr(), beta_w, _lib.stream())
+                  K, ctypes.byref(e), dw.data_ptr(), ws.data_ptr(), beta_w, int(max_wgs), _lib.stream())
         if partial is None:
             return out
         if partial2 is not None:

@@ -136,8 +136,12 @@ def test_pw_bn_backward_prologue_fused_weight_gradient(K, N, dgrad_epi):
     rb = G.pw_conv(g, wt, prologue=("bn_bwd", y, bits, coef, None), out=out_b, wgrad=(x, dw), **kw)
     dw2 = torch.ones((K, N), device="cuda")
     G.pw_conv(g, wt, prologue=("bn_bwd", y, bits, coef, None), out=acc0.clone(), wgrad=(x, dw2, 1), **kw)
+    dw3 = torch.empty((K, N), device="cuda")  # capped persistent grid (side-stream launches)
+    out_c = acc0.clone()
+    G.pw_conv(g, wt, prologue=("bn_bwd", y, bits, coef, None), out=out_c, wgrad=(x, dw3), max_wgs=64, **kw)
     torch.cuda.synchronize()
-    assert torch.equal(out_a, out_b)
+    assert torch.equal(out_a, out_b) and torch.equal(out_a, out_c)
+    torch.testing.assert_close(dw3, dw, rtol=1e-4, atol=1e-4 * float(dw.abs().max()))
     if dgrad_epi:
         assert torch.equal(ra[1], rb[1])
     ref = side.float().t() @ x.float()
