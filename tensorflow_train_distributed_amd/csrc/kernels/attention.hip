@@ -25,6 +25,9 @@
 //             bwd_kv, which runs after it; then recomputes S, dP per key tile; dQ in registers
 //             (deterministic, no float atomics). (A separate delta pass re-read O and dO:
 //             227 us per BERT-Large b128 layer, 5.5 ms per step.)
+//   bwd_fused (opt-in): all of dQ, dK, dV of one (batch, head) in one workgroup — five MFMA
+//             products instead of seven, one dropout hash per element instead of two; slower
+//             at BERT-Large's S = 512 (occupancy: see ttdk_attn_set_fused_bwd).
 #include "tile_common.h"
 
 namespace ttdk {
@@ -49,8 +52,9 @@ struct AttnParams {
   const bf16_t* dout;
   long long ldq, ldk, ldv, ldo, lddo;
   bf16_t* out;   // fwd: O ; bwd_q: dQ ; bwd_kv: dK
-  bf16_t* out2;  // bwd_kv: dV
-  long long ld_out, ld_out2;
+  bf16_t* out2;  // bwd_kv: dV ; fused bwd: dK
+  bf16_t* out3;  // fused bwd: dV
+  long long ld_out, ld_out2, ld_out3;
   float* lse;          // [B*H][S] log2 domain
   float* delta;        // [B*H][S]: written by bwd_q, read by bwd_kv
   const int* seqlen;   // [B] or null
@@ -536,6 +540,228 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
   }
 }
 
+// ------------------------------------------------------------------------------ fused bwd
+// dQ, dK and dV of one (batch, head) in ONE workgroup (S = 64 * NKB <= 512 keys): five MFMA
+// products per (query slice, key tile) instead of the split kernels' seven (both recompute S and
+// dP), every dropout hash computed once instead of twice, delta = rowsum(dO . O) formed while the
+// query slice is staged, and no cross-workgroup sum for dQ (deterministic, no atomics).
+//   * 4 waves, one per SIMD (launch_bounds(256, 1): 512 registers per lane); wave w owns keys
+//     [w*16*NKB, (w+1)*16*NKB): its dK^T and dV^T live in accumulators for the whole sweep (key
+//     on the MFMA lane, so the S / dP accumulators are already the B operands of dV^T += dO^T P
+//     and dK^T += Q^T dS), its V fragments in registers;
+//   * LDS: K of all S keys (S rows for the Q.K^T B operand, K^T column reads for dQ), dS^T of
+//     the slice for all keys (two 32-column halves, alternating per slice), and the 32-query
+//     slice of Q / dO / lse / delta double-buffered (register-staged one slice ahead);
+//   * per slice: S, dP -> P, dS for each pair of 16-key tiles; dV^T, dK^T accumulate; dS^T to
+//     LDS; one barrier; dQ[32 x 64] = dS . K split over the 4 waves (16 columns each), stored.
+template <int NKB, int NW, bool DROP>
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P) {
+  constexpr int NT = NW * 64;
+  constexpr int SK = 16 * NKB * NW;      // keys = queries of one (b, h)
+  constexpr int QS = 32;                 // queries per slice
+  constexpr int IMG = SK * 128;          // [SK][64] bf16 image
+  constexpr int QT = QS * 128;           // [32][64] bf16 slice image
+  constexpr int STAGE = 2 * QT + 2 * QS * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 2 * STAGE];
+  char* const sK = smem;
+  char* const sDS = smem + IMG;
+  char* const sStage = smem + 2 * IMG;
+  const int bh = tile::xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bh / P.H, h = bh - b * P.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int key0 = wave * 16 * NKB;
+  const int len = P.seqlen ? min(P.seqlen[b], SK) : SK;
+  const long long tok0 = static_cast<long long>(b) * SK;
+  const uint32_t key = DROP ? drop_key(P.rng, P.site) : 0u;
+
+  // K image of all keys (keys >= len zeroed: their dS is 0, keep 0 * K finite)
+  for (int c = tid; c < SK * 8; c += NT) {
+    const int row = c >> 3, ch = c & 7;
+    const uint4 v = row < len ? ldg16(P.k + (tok0 + row) * P.ldk + h * D + ch * 8) : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(sK + tile::off64(row, ch * 8)) = v;
+  }
+  bf16x8_t vf[NKB][2];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      vf[kb][ks] = ldg_frag(P.v + (tok0 + key0 + kb * 16 + i16) * P.ldv + h * D + ks * 32 + g * 8);
+  f32x4_t dk[NKB][4], dv[NKB][4];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) dk[kb][db] = dv[kb][db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // slice staging: thread t moves row (t & 255) >> 3, 16-B chunk t & 7 of Q, dO and O (delta
+  // partial); with 512 threads the first 256 take Q, the others dO and O
+  constexpr bool SPLIT_STAGE = NT >= 512;
+  const int srow = (tid & 255) >> 3, sch = tid & 7;
+  const bool do_q = !SPLIT_STAGE || tid < 256, do_d = !SPLIT_STAGE || (tid >= 256 && tid < 512);
+  uint4 rq = make_uint4(0, 0, 0, 0), rd = rq, ro = rq;
+  float rl = 0.f;
+  auto stage_load = [&](int s) {
+    const long long row = tok0 + s * QS + srow;
+    if (do_q) rq = ldg16(P.q + row * P.ldq + h * D + sch * 8);
+    if (do_d) {
+      rd = ldg16(P.dout + row * P.lddo + h * D + sch * 8);
+      ro = ldg16(P.o + row * P.ldo + h * D + sch * 8);
+    }
+    if (tid < QS) rl = P.lse[static_cast<long long>(bh) * SK + s * QS + tid];
+  };
+  auto stage_store = [&](int buf) {
+    char* st = sStage + buf * STAGE;
+    if (do_q) *reinterpret_cast<uint4*>(st + tile::off64(srow, sch * 8)) = rq;
+    float* stats = reinterpret_cast<float*>(st + 2 * QT);
+    if (tid < QS) stats[tid] = rl;
+    if (!do_d) return;
+    *reinterpret_cast<uint4*>(st + QT + tile::off64(srow, sch * 8)) = rd;
+    float a[8], d[8];
+    unpack8(ro, a);
+    unpack8(rd, d);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * d[j];
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (sch == 0) stats[QS + srow] = acc;
+  };
+  constexpr int NSL = SK / QS;
+  stage_load(0);
+  stage_store(0);
+  __syncthreads();
+
+  for (int s = 0; s < NSL; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < NSL) stage_load(s + 1);
+    const char* sQ = sStage + cur * STAGE;
+    const char* sD = sQ + QT;
+    const float* sL = reinterpret_cast<const float*>(sQ + 2 * QT);
+    const int dcol = cur * 32;  // dS^T columns of this slice
+#pragma unroll
+    for (int pp = 0; pp < NKB / 2; ++pp) {
+      const int k0 = key0 + pp * 32;
+      // Q / dO row fragments (re-read from LDS per key pair: registers go to dK^T, dV^T, V)
+      bf16x8_t qf[2][2], df[2][2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          qf[qb][ks] = rd_row(sQ, qb * 16 + i16, ks * 4 + g);
+          df[qb][ks] = rd_row(sD, qb * 16 + i16, ks * 4 + g);
+        }
+      // S[q][key], dP[q][key]: lane holds q = qb*16 + 4g + i, key = k0 + j*16 + i16
+      f32x4_t sc[2][2], dp[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8_t k0f = rd_row(sK, k0 + j * 16 + i16, g), k1f = rd_row(sK, k0 + j * 16 + i16, 4 + g);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          sc[qb][j] = mfma(qf[qb][0], k0f, f32x4_t{0.f, 0.f, 0.f, 0.f});
+          sc[qb][j] = mfma(qf[qb][1], k1f, sc[qb][j]);
+          dp[qb][j] = mfma(df[qb][0], vf[2 * pp + j][0], f32x4_t{0.f, 0.f, 0.f, 0.f});
+          dp[qb][j] = mfma(df[qb][1], vf[2 * pp + j][1], dp[qb][j]);
+        }
+      }
+      // P, dS in place (sc <- P * keep * scale, dp <- dS). Dropout: lanes i16, i16 ^ 1 hold the
+      // two keys of one pair for j = 0 and j = 1; the even lane hashes the j = 0 pair, the odd
+      // lane the j = 1 pair, and they swap (one hash per lane per (query, pair of tiles))
+      const bool odd = (i16 & 1) != 0;
+      const uint32_t pair = static_cast<uint32_t>(k0 + (odd ? 16 : 0) + i16) >> 1;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        // this lane's query rows qb*16 + 4g + i: lse2 and delta
+        const f32x4_t ls = *reinterpret_cast<const f32x4_t*>(sL + qb * 16 + 4 * g);
+        const f32x4_t dl = *reinterpret_cast<const f32x4_t*>(sL + QS + qb * 16 + 4 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint32_t hk[2] = {0u, 0u};
+          if constexpr (DROP) {
+            const int qg = s * QS + qb * 16 + 4 * g + i;
+            const uint32_t mine = attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * SK + qg)), pair);
+            const uint32_t other = __shfl_xor(mine, 1, 64);
+            hk[0] = odd ? other : mine;
+            hk[1] = odd ? mine : other;
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int kcol = k0 + j * 16 + i16;
+            const float p = kcol < len ? fast_exp2(sc[qb][j][i] * P.scale_log2 - ls[i]) : 0.f;
+            float dpv = dp[qb][j][i];
+            float pd = p;
+            if constexpr (DROP) {
+              const bool kp = attn_keep(hk[j], static_cast<uint32_t>(kcol), P.drop_thr);
+              pd = kp ? p * P.drop_scale : 0.f;
+              dpv = kp ? dpv * P.drop_scale : 0.f;
+            }
+            sc[qb][j][i] = pd;
+            dp[qb][j][i] = p * (dpv - dl[i]);
+          }
+        }
+      }
+      bf16x8_t pfr[2], sfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        pfr[j] = pack_frag(sc[0][j], sc[1][j]);
+        sfr[j] = pack_frag(dp[0][j], dp[1][j]);
+        // dS^T rows (keys) x this slice's 32 query columns, for dQ
+        const uint4 w = __builtin_bit_cast(uint4, sfr[j]);
+        *reinterpret_cast<uint2*>(sDS + tile::off64(k0 + j * 16 + i16, dcol + 4 * g)) = make_uint2(w.x, w.y);
+        *reinterpret_cast<uint2*>(sDS + tile::off64(k0 + j * 16 + i16, dcol + 16 + 4 * g)) = make_uint2(w.z, w.w);
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS (contraction over the slice's 32 queries)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8_t dof = rd_col(sD, 0, 16, db * 16, lane);
+        const bf16x8_t qcf = rd_col(sQ, 0, 16, db * 16, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          dv[2 * pp + j][db] = mfma(dof, pfr[j], dv[2 * pp + j][db]);
+          dk[2 * pp + j][db] = mfma(qcf, sfr[j], dk[2 * pp + j][db]);
+        }
+      }
+    }
+    if (s + 1 < NSL) stage_store(cur ^ 1);
+    __syncthreads();
+    // dQ^T[d][q] of the slice: 8 tiles of 16 d x 16 q, tile t = (qb = t >> 2, db = t & 3);
+    // wave w takes tiles w, w + NW, ...
+    constexpr int TPW = 8 / NW;
+    f32x4_t dq[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) dq[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int ks = 0; ks < SK / 32; ++ks) {
+#pragma unroll
+      for (int u = 0; u < TPW; ++u) {
+        const int t = wave + u * NW, qb = t >> 2, db = t & 3;
+        dq[u] = mfma(rd_col(sK, ks * 32, ks * 32 + 16, db * 16, lane),
+                     rd_col(sDS, ks * 32, ks * 32 + 16, dcol + qb * 16, lane), dq[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+      const int t = wave + u * NW, qb = t >> 2, db = t & 3;
+      const f32x4_t v = dq[u] * P.scale;
+      bf16_t* op = P.out + (tok0 + s * QS + qb * 16 + i16) * P.ld_out + h * D + db * 16 + 4 * g;
+      *reinterpret_cast<uint2*>(op) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+  }
+  // dK (scaled by 1/sqrt(D)) and dV: lane holds key key0 + kb*16 + i16, d = db*16 + 4g + i
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    const long long row = tok0 + key0 + kb * 16 + i16;
+    bf16_t* pk = P.out2 + row * P.ld_out2 + h * D + 4 * g;
+    bf16_t* pv = P.out3 + row * P.ld_out3 + h * D + 4 * g;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const f32x4_t a = dk[kb][db] * P.scale, c = dv[kb][db];
+      *reinterpret_cast<uint2*>(pk + db * 16) = make_uint2(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]));
+      *reinterpret_cast<uint2*>(pv + db * 16) = make_uint2(pack_bf16x2(c[0], c[1]), pack_bf16x2(c[2], c[3]));
+    }
+  }
+}
+
 AttnParams make_params(int B, int H, int S, const int* seqlen, float p_drop, const long long* rng, uint32_t site) {
   AttnParams P{};
   P.B = B;
@@ -576,6 +802,25 @@ TTDK_EXPORT int ttdk_attn_fwd(const bf16_t* q, long long ldq, const bf16_t* k, l
   return hipGetLastError();
 }
 
+// Single-kernel backward (attn_bwd_fused_kernel) for S in {128, 256, 512}: opt-in
+// (TTD_ATTN_FUSED_BWD=1 or ttdk_attn_set_fused_bwd(1)). Measured at BERT-Large b128 (S = 512,
+// p = 0.1): 1190 us standalone vs 980 us for the split dQ / dK-dV kernels, BERT step 185.2 vs
+// 177.2 ms — one workgroup per (b, h) holds 4 waves (the S = 512 dK^T / dV^T accumulators need
+// 256 AGPRs per lane: one wave per SIMD, LDS 145 KB: one workgroup per CU), too little
+// occupancy to hide the MFMA -> softmax dependencies; the 8-wave form spills 65 VGPRs.
+static int g_attn_fused = -1;
+static bool attn_fused_bwd() {
+  if (g_attn_fused < 0) {
+    const char* e = getenv("TTD_ATTN_FUSED_BWD");
+    g_attn_fused = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return g_attn_fused != 0;
+}
+TTDK_EXPORT int ttdk_attn_set_fused_bwd(int on) {
+  g_attn_fused = on ? 1 : 0;
+  return 0;
+}
+
 // dq/dk/dv may alias one fused [tokens, 3*H*64] buffer (different column offsets).
 TTDK_EXPORT int ttdk_attn_bwd(const bf16_t* q, long long ldq, const bf16_t* k, long long ldk, const bf16_t* v,
                               long long ldv, const bf16_t* o, long long ldo, const bf16_t* dout, long long lddo,
@@ -590,6 +835,24 @@ TTDK_EXPORT int ttdk_attn_bwd(const bf16_t* q, long long ldq, const bf16_t* k, l
   P.ldq = ldq; P.ldk = ldk; P.ldv = ldv; P.ldo = ldo; P.lddo = lddo;
   P.lse = const_cast<float*>(lse);
   P.delta = delta;
+  if (attn_fused_bwd() && (S == 128 || S == 256 || S == 512)) {
+    // one workgroup per (batch, head): dQ, dK, dV in one pass (attn_bwd_fused_kernel)
+    P.out = dq; P.ld_out = lddq; P.out2 = dk; P.ld_out2 = lddk; P.out3 = dv; P.ld_out3 = lddv;
+    const dim3 g1(B * H);
+    const bool d = p_drop > 0.f;
+    // S = 512: 8 waves x 64 keys (two waves per SIMD); S = 256 / 128: 4 waves x 64 / 32 keys
+    if (S == 512) {
+      if (d) hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 8, true>), g1, dim3(512), 0, st, P);
+      else hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 8, false>), g1, dim3(512), 0, st, P);
+    } else if (S == 256) {
+      if (d) hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 4, true>), g1, dim3(256), 0, st, P);
+      else hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 4, false>), g1, dim3(256), 0, st, P);
+    } else {
+      if (d) hipLaunchKernelGGL((attn_bwd_fused_kernel<2, 4, true>), g1, dim3(256), 0, st, P);
+      else hipLaunchKernelGGL((attn_bwd_fused_kernel<2, 4, false>), g1, dim3(256), 0, st, P);
+    }
+    return hipGetLastError();
+  }
   dim3 grid(B * H * (S / QBLK)), block(256);
   // dQ first: it computes delta (rowsum dO . O) on the way and stores it for dK / dV
   P.out = dq; P.ld_out = lddq; P.out2 = nullptr;

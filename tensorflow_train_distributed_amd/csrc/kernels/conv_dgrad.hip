@@ -140,9 +140,11 @@ static Phase phase_of(int a, int s, int pad, int R, int H) {
 }
 
 // dx[N,H,W,C] of a strided conv (dilation 1, every phase has >= 1 tap) by phases. `ws`:
-// scratch for the phase sub-kernels, C*R*S*Kout bf16 (the size of wt).
+// scratch for the phase sub-kernels, C*R*S*Kout bf16 (the size of wt); ws_ready != 0: ws
+// already holds the phase filters in this launcher's phase order (ttdk_wprep, once per step),
+// wt is not read.
 TTDK_EXPORT int ttdk_conv_dgrad_subpixel(const bf16_t* dy, const bf16_t* wt, const TtdkConv* g, bf16_t* ws,
-                                         const TtdkEpilogue* epi, hipStream_t st) {
+                                         int ws_ready, const TtdkEpilogue* epi, hipStream_t st) {
   const int s = g->sh;
   if (g->sw != s || s < 2 || g->dh != 1 || g->dw != 1 || g->R < s || g->S < s || g->K % 8 || g->C % 8)
     return hipErrorInvalidValue;
@@ -162,8 +164,9 @@ TTDK_EXPORT int ttdk_conv_dgrad_subpixel(const bf16_t* dy, const bf16_t* wt, con
       const int M = g->N * pr.n * pc.n, K = pr.T * pc.T * Kc;
       const long long wn = static_cast<long long>(N) * K;
       int grid = static_cast<int>(std::min<long long>((wn / 8 + 255) / 256, 4096));
-      hipLaunchKernelGGL(subpixel_weights_kernel, dim3(grid), dim3(256), 0, st, wt, wsp, N, g->R, g->S, Kc, s, pr.r0,
-                         pr.T, pc.r0, pc.T);
+      if (!ws_ready)
+        hipLaunchKernelGGL(subpixel_weights_kernel, dim3(grid), dim3(256), 0, st, wt, wsp, N, g->R, g->S, Kc, s,
+                           pr.r0, pr.T, pc.r0, pc.T);
       EpiParams e = pe;
       e.remap = 1;
       e.rP = pr.n;

@@ -364,6 +364,53 @@ TTDK_EXPORT int ttdk_transpose_aca_bf16(const bf16_t* src, bf16_t* dst, int A, i
   return hipGetLastError();
 }
 
+// Every data-gradient filter operand of a network in ONE launch (instead of one transpose per
+// conv on the backward's critical chain, plus s*s sub-pixel gathers per strided conv): entry e
+// turns the bf16 filter [K][R][S][C] at src + src_off into [C][Tr][Ts][K] at dst + dst_off,
+// taking taps r = r0 + tr*s, q = s0 + ts*s (s = 1, full R x S: the plain [C,R,S,K] transpose;
+// s > 1: one sub-pixel phase of a strided dgrad, see conv_dgrad.hip). Blocks walk the
+// concatenated 32x32 (K, C) tiles of all entries' taps; tile_begin is each entry's first tile.
+struct WPrepEntry {
+  long long src_off, dst_off;
+  int K, R, S, C, s, r0, Tr, s0, Ts, tile_begin;
+};
+
+__global__ __launch_bounds__(256) void wprep_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                    const WPrepEntry* __restrict__ tab, int n) {
+  __shared__ bf16_t tile[32][33];
+  const int bid = blockIdx.x;
+  int e = 0;
+  while (e + 1 < n && tab[e + 1].tile_begin <= bid) ++e;
+  const WPrepEntry t = tab[e];
+  const int kt = (t.K + 31) / 32, ct = (t.C + 31) / 32;
+  int rel = bid - t.tile_begin;
+  const int tap = rel / (kt * ct);
+  rel -= tap * kt * ct;
+  const int k0 = (rel / ct) * 32, c0 = (rel % ct) * 32;
+  const int tr = tap / t.Ts, ts = tap % t.Ts;
+  const int r = t.r0 + tr * t.s, q = t.s0 + ts * t.s;
+  const bf16_t* s_ = src + t.src_off + (static_cast<long long>(r) * t.S + q) * t.C;
+  bf16_t* d_ = dst + t.dst_off + static_cast<long long>(tap) * t.K;
+  const long long sld = static_cast<long long>(t.R) * t.S * t.C;  // src stride between k rows
+  const long long dld = static_cast<long long>(t.Tr) * t.Ts * t.K;  // dst stride between c rows
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int k = k0 + i, c = c0 + tx;
+    tile[i][tx] = (k < t.K && c < t.C) ? s_[k * sld + c] : static_cast<bf16_t>(0);
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, k = k0 + tx;
+    if (k < t.K && c < t.C) d_[c * dld + k] = tile[tx][i];
+  }
+}
+
+TTDK_EXPORT int ttdk_wprep(const bf16_t* src, bf16_t* dst, const void* tab, int n, int tiles, hipStream_t st) {
+  if (n <= 0 || tiles <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wprep_kernel, dim3(tiles), dim3(256), 0, st, src, dst, static_cast<const WPrepEntry*>(tab), n);
+  return hipGetLastError();
+}
+
 TTDK_EXPORT int ttdk_transpose2d_f32(const float* src, float* dst, int R, int C, hipStream_t st) {
   dim3 grid((C + 31) / 32, (R + 31) / 32);
   hipLaunchKernelGGL(transpose2d_f32_kernel, grid, dim3(256), 0, st, src, dst, R, C);

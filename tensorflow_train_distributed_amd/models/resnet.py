@@ -135,6 +135,9 @@ class ResNet:
         # dedicated stem forward kernel (stem_fwd.hip: K = 7 x 32 over the 3 real channels)
         self.stem_fwd_kernel = os.environ.get("TTD_STEM_FWD", "1") != "0"
         self._wgrad_stream = None
+        # every data-gradient filter operand prepared in one launch per step (TTD_WPREP=0: per conv)
+        self.wprep = os.environ.get("TTD_WPREP", "1") != "0"
+        self._wp_cur = None
         self.num_classes = num_classes
         self.in_channels = in_channels
         self.in_store = 8 if in_channels <= 8 else (in_channels + 7) // 8 * 8
@@ -452,7 +455,7 @@ class ResNet:
             # in one streaming kernel (no dz pass, no dz store, no weight-gradient re-read)
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
-            wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
+            wt2 = self._crsk(wname).view(c.cin_store, c.cout)
             out = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None),
                             wgrad=(x, P.g[wname].view(c.cout, c.cin_store)), max_wgs=self.side_pw_wgs)
             self._cd_done = graphs.mark(torch.cuda.current_stream())
@@ -466,7 +469,7 @@ class ResNet:
             # gradient in one streaming kernel
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
-            wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
+            wt2 = self._crsk(wname).view(c.cin_store, c.cout)
             out = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None), out=dx,
                             beta=dx_beta if dx is not None else 0, wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
             self._ready_main(c.name + "_bn/moving_variance")
@@ -477,7 +480,7 @@ class ResNet:
             # kernel): dz is written once there for the weight gradient, never re-read by the dgrad
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
-            wt2 = K.krsc_to_crsk(P.c[wname]).view(c.cin_store, c.cout)
+            wt2 = self._crsk(wname).view(c.cin_store, c.cout)
             _, fy, fmask, _ = feeds
             bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
             if self.pw_wgrad and G.pw_wgrad_fusable(M, c.cin_store, Kc):
@@ -501,7 +504,7 @@ class ResNet:
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
             dz = torch.empty_like(y)
-            wt = K.krsc_to_crsk(P.c[wname])
+            wt = self._crsk(wname)
             _, fy, fmask, _ = feeds
             out, partial, T = G.conv3_halo(dout, wt, flip=True, prologue=("bn_bwd", y, None, coef, dz),
                                            bn_stat=(fy, fmask))
@@ -516,7 +519,7 @@ class ResNet:
             coef = K.bn_backward_coef(M, Kc, P.var[pre + "gamma"], st, P.g[pre + "gamma"], P.g[pre + "beta"],
                                       dstat[0], dstat[1])
             dz = torch.empty_like(y)
-            wt = K.krsc_to_crsk(P.c[wname])
+            wt = self._crsk(wname)
             bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
             pro = (y, coef, dz)
             if feeds is not None and G.dgrad_stat_rows(tuple(x.shape), tuple(wt.shape), stride, pad) is not None:
@@ -545,7 +548,7 @@ class ResNet:
             self._wgrad(c, x, dz, wname)
         if not need_dx:
             return None, None
-        wt = K.krsc_to_crsk(P.c[wname])
+        wt = self._crsk(wname)
         bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
         if (feeds is not None and feeds2 is None and dx is None and self.fuse_bn_bwd and self.c3_dgrad == 2
                 and self._c3_ok(c, x.shape[1], x.shape[2])):
@@ -561,9 +564,10 @@ class ResNet:
                                                          bn_stat=(fy, fmask), bn_stat2=feeds2[1], beta_s2=bs2)
                 return out, (partial, T, partial2)
             out, partial, T = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, bn_stat=(fy, fmask),
-                                           beta_s2=bs2)
+                                           beta_s2=bs2, ws=self._phase_ws(wname))
             return out, (partial, T)
-        out = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, sampled_only=sampled_only, beta_s2=bs2)
+        out = G.conv_dgrad(dz, wt, x.shape, stride, pad, out=dx, beta=dx_beta, sampled_only=sampled_only, beta_s2=bs2,
+                           ws=self._phase_ws(wname))
         if wgrad_last:
             # data gradient first (its consumer waits on this event), then the weight gradient
             self._cd_done = graphs.mark(torch.cuda.current_stream())
@@ -571,6 +575,49 @@ class ResNet:
             # layout (the block's c3 and c2) are not final yet
             self._wgrad(c, x, dz, wname, ready=False)
         return out, None
+
+    def _weight_prep(self, image_shape):
+        """Data-gradient filter operands of every conv, prepared in one launch at the start of the
+        step (ops.kernels.WeightPrep): [C,R,S,K] transposes, plus the sub-pixel phase filters of
+        the strided 3x3 convs (their geometry depends on the image size). TTD_WPREP=0: per-conv
+        transposes / phase gathers inside the backward, as before."""
+        from ..ops import kernels as K
+        key = tuple(image_shape[1:3])
+        if getattr(self, "_wp_key", None) == key:
+            return self._wp
+        P = self.params
+        wp = K.WeightPrep(P.compute)
+        H = (image_shape[1] + 2 * self.stem.pad - self.stem.k) // self.stem.stride + 1
+        W = (image_shape[2] + 2 * self.stem.pad - self.stem.k) // self.stem.stride + 1
+        H, W = K.pool_out(H, 3, 2, 1), K.pool_out(W, 3, 2, 1)
+        for blk in self.blocks:
+            for key_ in ("c1", "c2", "c3", "cd"):
+                c = blk[key_]
+                if c is None:
+                    continue
+                name = c.name + "_conv/kernel"
+                shape = tuple(P.var[name].shape)
+                wp.add(name, P.offsets[name], shape)
+                if c.k > 1 and c.stride > 1:
+                    wp.add(name + "/phases", P.offsets[name], shape, sub=(c.stride, c.pad, c.pad, H, W))
+            s = blk["c2"].stride
+            H, W = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+        self._wp = wp.build()
+        self._wp_key = key
+        return self._wp
+
+    def _crsk(self, wname):
+        from ..ops import kernels as K
+        wp = self._wp_cur
+        if wp is not None and wp.has(wname):
+            return wp.crsk(wname)
+        return K.krsc_to_crsk(self.params.c[wname])
+
+    def _phase_ws(self, wname):
+        wp = self._wp_cur
+        if wp is not None and wp.has(wname + "/phases"):
+            return wp.phases(wname + "/phases")
+        return None
 
     def _wgrad(self, c: ConvSpec, x, dz, wname, ready=True):
         """Weight gradient of conv c into its flat gradient slice; on the side stream when enabled,
@@ -644,6 +691,11 @@ class ResNet:
             x = K.pad_channels(images.contiguous(), self.in_store)
         if fp8:
             self._fp8_step_begin()
+        self._wp_cur = None
+        if self.wprep and self.device.type == "cuda":
+            # this step's data-gradient filters (the weights are final until the optimizer runs)
+            self._wp_cur = self._weight_prep(tuple(images.shape))
+            self._wp_cur.run()
 
         def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None, pro=None,
                  pro_big=False):

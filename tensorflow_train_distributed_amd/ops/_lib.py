@@ -57,7 +57,7 @@ _SIGS = {
     "ttdk_conv_dgrad_bnpro_ok": [G],
     "ttdk_set_inkernel_fold": [I],
     "ttdk_conv_fwd_bnpro": [P, P, G, P, P, I, P, P, E, P],
-    "ttdk_conv_dgrad_subpixel": [P, P, G, P, E, P],
+    "ttdk_conv_dgrad_subpixel": [P, P, G, P, I, E, P],
     "ttdk_conv_dgrad_subpixel_stat_rows": [G],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_conv_wgrad_bn": [P, P, P, P, G, P, P, I, I, I, I, P],
@@ -111,6 +111,7 @@ _SIGS = {
     "ttdk_pad_channels": [P, P, L, I, I, P],
     "ttdk_unpad_channels": [P, P, L, I, I, P],
     "ttdk_transpose_aca_bf16": [P, P, I, I, I, P],
+    "ttdk_wprep": [P, P, P, I, I, P],
     "ttdk_transpose2d_f32": [P, P, I, I, P],
     "ttdk_bias_act_dropout_fwd": [P, P, P, L, I, I, F, U64, U64, I, P],
     "ttdk_bias_act_dropout_bwd": [P, P, P, P, L, I, I, F, U64, U64, I, P],

@@ -524,7 +524,7 @@ def dgrad_bnpro_ok(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
 
 
 def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, residual=None,
-               tile=(0, 0), bn_stat=None, bn_stat2=None, sampled_only=False, beta_s2=None, bn_pro=None):
+               tile=(0, 0), bn_stat=None, bn_stat2=None, sampled_only=False, beta_s2=None, bn_pro=None, ws=None):
     """dx[N,H,W,C] from dy[N,P,Q,K] and wt = w transposed to [C,R,S,K].
 
     For strided 1x1 convs only the sampled pixels are written: pass a zero-initialised `out`
@@ -540,6 +540,9 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
     stores g = dx * mask and per-tile BN-backward partial sums (sum g, sum g*y); returns
     (out, partial [T, 2, C], T). bn_stat2=y2: a second BN fed by the same g (projection
     shortcut); returns (out, partial, T, partial2). Requires dgrad_stat_rows(...) not None.
+
+    ws: for a strided (sub-pixel) dgrad, the phase filters already gathered in the launcher's
+    phase order (ops.kernels.WeightPrep, once per step): wt is then not read.
     """
     _check(dy, torch.bfloat16, "dy")
     _check(wt, torch.bfloat16, "wt")
@@ -574,9 +577,10 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
                     for pb in _phases(g.sw, g.pw, S, g.W):
                         _log("dgrad_%dx%d_s%d_phase%dx%d" % (R, S, g.sh, pa[0], pb[0]), g.N * pa[1] * pb[1], C,
                              pa[0] * pb[0] * K)
-            ws = torch.empty_like(wt)
+            ready = ws is not None
+            ws = torch.empty_like(wt) if ws is None else ws
             _lib.call("ttdk_conv_dgrad_subpixel", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), ws.data_ptr(),
-                      ctypes.byref(e), _lib.stream())
+                      int(ready), ctypes.byref(e), _lib.stream())
         elif bn_pro is not None:
             _bnpro_call(dy, wt, g, bn_pro, e)
         else:
@@ -596,9 +600,10 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
                 for pb in _phases(g.sw, g.pw, S, g.W):
                     _log("dgrad_%dx%d_s%d_phase%dx%d" % (R, S, g.sh, pa[0], pb[0]), g.N * pa[1] * pb[1], C,
                          pa[0] * pb[0] * K)
-        ws = torch.empty_like(wt)
+        ready = ws is not None
+        ws = torch.empty_like(wt) if ws is None else ws
         _lib.call("ttdk_conv_dgrad_subpixel", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), ws.data_ptr(),
-                  ctypes.byref(e), _lib.stream())
+                  int(ready), ctypes.byref(e), _lib.stream())
         return out
     _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * (g.P * g.Q if strided_pw else g.H * g.W), C, R * S * K)
     _lib.call("ttdk_conv_dgrad", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), tile[0], tile[1], ctypes.byref(e),

@@ -3,6 +3,7 @@ cross-entropy, element-wise/layout, optimizers, fp8). All tensors are CUDA tenso
 launch goes to PyTorch's current stream. See the .hip files for the math."""
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -268,6 +269,89 @@ def krsc_to_crsk(w, out=None):
         out = torch.empty((C, R, S, K), dtype=w.dtype, device=w.device)
     _lib.call("ttdk_transpose_aca_bf16", w.data_ptr(), out.data_ptr(), K, R * S, C, _s())
     return out
+
+
+def subpixel_phases(s, pad, R, H):
+    """(first tap, tap count) of each non-empty sub-pixel phase along one axis of a stride-s
+    data gradient, in ttdk_conv_dgrad_subpixel's order (mirror of conv_dgrad.hip phase_of)."""
+    out = []
+    for a in range(s):
+        r0 = (a + pad) % s
+        T = (R - r0 + s - 1) // s if r0 < R else 0
+        n = (H - a + s - 1) // s if a < H else 0
+        if n:
+            out.append((r0, T))
+    return out
+
+
+class WeightPrep:
+    """Every data-gradient filter operand of a network in one launch per step (ttdk_wprep):
+    [C,R,S,K] transposes of the [K,R,S,C] filters, and for strided 3x3 dgrads the sub-pixel
+    phase filters in ttdk_conv_dgrad_subpixel's order — instead of one transpose launch per conv
+    (and s*s gathers per strided conv) on the backward's critical chain.
+
+    src: the flat bf16 compute copy that holds every filter; add(name, offset, shape) registers a
+    [K,R,S,C] filter at that element offset, add(..., sub=(s, pad_h, pad_w, H, W)) its phase
+    filters (the dgrad input is H x W); build() packs the table; run() launches on the current
+    stream; crsk(name) / phases(name) return views of the output buffer."""
+
+    _DT = np.dtype([("src_off", "<i8"), ("dst_off", "<i8"), ("K", "<i4"), ("R", "<i4"), ("S", "<i4"),
+                    ("C", "<i4"), ("s", "<i4"), ("r0", "<i4"), ("Tr", "<i4"), ("s0", "<i4"), ("Ts", "<i4"),
+                    ("tile_begin", "<i4")])
+
+    def __init__(self, src):
+        self.src = src
+        self._rows = []
+        self._views = {}
+        self._dst_n = 0
+        self._tiles = 0
+        self.buf = None
+
+    def _entry(self, off, shape, s, r0, Tr, s0, Ts):
+        K, R, S, C = shape
+        dst = self._dst_n
+        self._rows.append((off, dst, K, R, S, C, s, r0, Tr, s0, Ts, self._tiles))
+        self._tiles += Tr * Ts * (-(-K // 32)) * (-(-C // 32))
+        self._dst_n += C * Tr * Ts * K
+        return dst
+
+    def add(self, name, offset, shape, sub=None):
+        K, R, S, C = shape
+        if sub is None:
+            self._views[name] = ("crsk", self._entry(offset, shape, 1, 0, R, 0, S), (C, R, S, K))
+            return
+        s, ph, pw, H, W = sub
+        start = self._dst_n
+        for r0, Tr in subpixel_phases(s, ph, R, H):
+            for s0, Ts in subpixel_phases(s, pw, S, W):
+                self._entry(offset, shape, s, r0, Tr, s0, Ts)
+        self._views[name] = ("phases", start, self._dst_n - start)
+
+    def build(self):
+        arr = np.zeros(len(self._rows), dtype=self._DT)
+        for i, r in enumerate(self._rows):
+            arr[i] = r
+        self._tab = torch.from_numpy(arr.view(np.uint8).copy()).to(self.src.device)
+        self.buf = torch.empty(max(self._dst_n, 1), dtype=torch.bfloat16, device=self.src.device)
+        return self
+
+    def run(self):
+        if self._rows:
+            _lib.call("ttdk_wprep", self.src.data_ptr(), self.buf.data_ptr(), self._tab.data_ptr(), len(self._rows),
+                      self._tiles, _s())
+
+    def has(self, name):
+        return name in self._views
+
+    def crsk(self, name):
+        kind, off, shape = self._views[name]
+        assert kind == "crsk"
+        return self.buf[off:off + int(np.prod(shape))].view(shape)
+
+    def phases(self, name):
+        kind, off, n = self._views[name]
+        assert kind == "phases"
+        return self.buf[off:off + n]
 
 
 def bias_act_dropout(x, bias, act=ACT_NONE, rate=0.0, seed=0, offset=0, out=None):

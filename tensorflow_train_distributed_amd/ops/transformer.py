@@ -14,6 +14,7 @@ from ._lib import F, I, L, P
 _lib.register({
     "ttdk_attn_fwd": [P, L, P, L, P, L, P, L, P, P, I, I, I, F, P, I, P],
     "ttdk_attn_bwd": [P, L, P, L, P, L, P, L, P, L, P, P, P, L, P, L, P, L, P, I, I, I, F, P, I, P],
+    "ttdk_attn_set_fused_bwd": [I],
     "ttdk_ln_fwd": [P, P, P, P, P, P, P, P, I, I, F, F, I, F, I, P, P],
     "ttdk_ln_bwd_num_blocks": [I],
     "ttdk_ln_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, F, I, F, I, P, P],
@@ -59,6 +60,13 @@ def attention_fwd(q, k, v, out, lse, B, H, S, *, seqlen=None, p_drop=0.0, rng=No
               out.data_ptr(), out.stride(0), lse.data_ptr(), _p(seqlen), B, H, S, float(p_drop),
               _p(rng.t if rng is not None else None), int(site), _s())
     return out, lse
+
+
+def set_fused_attention_bwd(on: bool):
+    """Select the single-kernel attention backward (S in {128, 256, 512}; opt-in, measured slower
+    at BERT-Large: attention.hip) or the split dQ / dK-dV kernels (default;
+    TTD_ATTN_FUSED_BWD=1 at start-up selects the fused one)."""
+    _lib.call("ttdk_attn_set_fused_bwd", int(bool(on)))
 
 
 def attention_bwd(q, k, v, o, dout, lse, dq, dk, dv, B, H, S, *, delta=None, seqlen=None, p_drop=0.0, rng=None,

@@ -624,3 +624,37 @@ def test_conv_fwd_with_bn_apply_operand_prologue(cfg):
     torch.testing.assert_close(sums[0], yf.sum(0), rtol=2e-3, atol=5e-2)
     torch.testing.assert_close(sums[1], (yf * yf).sum(0), rtol=2e-3, atol=5e-1)
     assert T == -(-M // 256)
+
+
+@pytest.mark.gpu
+def test_weight_prep_matches_per_conv_transposes_and_phase_filters():
+    """ttdk_wprep (one launch for every filter of a network) vs the per-conv transpose and the
+    sub-pixel dgrad's own phase gathers: bitwise equal filters, and a strided dgrad fed the
+    prepared phase filters (ws=...) equals the one that gathers them itself."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(3)
+    shapes = [(64, 1, 1, 256), (128, 3, 3, 128), (256, 3, 3, 64), (40, 5, 5, 24), (2048, 1, 1, 512)]
+    sizes = [int(torch.tensor(s).prod()) for s in shapes]
+    flat = torch.randn(sum(sizes) + 3, device="cuda").bfloat16()
+    wp = K.WeightPrep(flat)
+    offs, o = [], 3  # unaligned start on purpose
+    for i, (s, n) in enumerate(zip(shapes, sizes)):
+        offs.append(o)
+        wp.add("w%d" % i, o, s)
+        if s[1] > 1:
+            wp.add("w%d/phases" % i, o, s, sub=(2, s[1] // 2, s[2] // 2, 15, 13))
+        o += n
+    wp.build().run()
+    for i, (s, n) in enumerate(zip(shapes, sizes)):
+        w = flat[offs[i]:offs[i] + n].view(s)
+        assert torch.equal(wp.crsk("w%d" % i), K.krsc_to_crsk(w))
+    # strided dgrad with the prepared phase filters
+    Kc, R, _, C = shapes[1]
+    w = flat[offs[1]:offs[1] + sizes[1]].view(shapes[1])
+    wt = K.krsc_to_crsk(w)
+    x_shape = (2, 15, 13, C)
+    dy = torch.randn(2, 8, 7, Kc, device="cuda").bfloat16()
+    a = G.conv_dgrad(dy, wt, x_shape, (2, 2), (1, 1))
+    b = G.conv_dgrad(dy, torch.zeros_like(wt), x_shape, (2, 2), (1, 1), ws=wp.phases("w1/phases"))
+    assert torch.equal(a, b)

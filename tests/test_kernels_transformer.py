@@ -52,15 +52,19 @@ def test_attention_dropout_pair_hash_statistics():
 
 
 @gpu
-@pytest.mark.parametrize("masked,p", [(False, 0.0), (True, 0.0), (False, 0.1)])
-def test_attention_fwd_bwd_matches_reference(masked, p):
+@pytest.mark.parametrize("S,masked,p,fused", [(256, False, 0.0, True), (256, True, 0.0, True), (256, False, 0.1, True),
+                                             (512, True, 0.1, True), (128, False, 0.1, True), (512, False, 0.0, True),
+                                             (256, True, 0.1, False), (512, False, 0.1, False)])
+def test_attention_fwd_bwd_matches_reference(S, masked, p, fused):
+    """fp32 autograd oracle; the backward on the single-kernel path (fused, S in {128, 256, 512})
+    and on the split dQ / dK-dV kernels."""
     torch.manual_seed(0)
-    B, H, S = 2, 3, 256
+    B, H = 2, 3
     D = H * 64
     dev = "cuda"
     qkv = (torch.randn(B * S, 3 * D, device=dev) * 1.5).bfloat16()
     q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-    seqlen = torch.tensor([S, 150], dtype=torch.int32, device=dev) if masked else None
+    seqlen = torch.tensor([S, S // 2 + 22], dtype=torch.int32, device=dev) if masked else None
     rng = T.RngState(99, dev) if p > 0 else None
     if rng is not None:
         rng.advance()
@@ -82,8 +86,12 @@ def test_attention_fwd_bwd_matches_reference(masked, p):
     do = torch.randn(B * S, D, device=dev).bfloat16()
     ref.backward(do.float())
     dqkv = torch.empty_like(qkv)
-    T.attention_bwd(q, k, v, o, do, lse, dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], B, H, S, seqlen=seqlen,
-                    p_drop=p, rng=rng, site=5)
+    T.set_fused_attention_bwd(fused)
+    try:
+        T.attention_bwd(q, k, v, o, do, lse, dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], B, H, S, seqlen=seqlen,
+                        p_drop=p, rng=rng, site=5)
+    finally:
+        T.set_fused_attention_bwd(False)
     for name, got, want in (("dq", dqkv[:, :D], qf.grad), ("dk", dqkv[:, D:2 * D], kf.grad),
                             ("dv", dqkv[:, 2 * D:], vf.grad)):
         rel = float((got.float() - want).norm() / want.norm())
