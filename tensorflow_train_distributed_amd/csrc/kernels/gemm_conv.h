@@ -1979,7 +1979,7 @@ __device__ __forceinline__ void pers_epi(const f32x4_t (&acc)[2][2][4][2], const
 template <int BN, class OA, class OB, int EK>
 __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::Params pa, typename OB::Params pb,
                                                                 EpiParams E, int M, int N, int K, int tiles_m,
-                                                                int tiles_n, int ovl) {
+                                                                int tiles_n, int ovl, int fullwait) {
   using Gm = Geo<BN>;
   constexpr int T = OA::THREADS, NW = T / 64, WN = NW / 2;
   static_assert(OB::THREADS == T && NW == 8, "8-wave operand policies");
@@ -2049,6 +2049,13 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
   int t = xcd_remap(vt, nblk);
   prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
   const float alpha_e = epi_alpha(E);
+  // store instructions per thread of a whole-tile (unchecked) epilogue: 8 row blocks x 2 column
+  // halves, twice with the aux copy
+  constexpr int EPI_ST = 16 * (((EK & kEkAux) != 0) ? 2 : 1);
+  // how the previous tile ended: 0 = nothing issued after this tile's prologue DMA (first tile,
+  // or no overlap), 1 = a whole-tile epilogue's EPI_ST stores issued after it, 2 = a checked
+  // (edge) epilogue, whose store count is data-dependent
+  int prev = 0;
 
   for (;;) {
     const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
@@ -2061,10 +2068,20 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
         for (int a = 0; a < 4; ++a)
 #pragma unroll
           for (int b = 0; b < NB; ++b) acc[ha][hb][a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // K-tile 0 landed (every store of the previous epilogue retired too: vmcnt counts both,
-    // in issue order, and the epilogue's count is not a compile-time constant)
-    if (ktiles > 1 && vt == static_cast<int>(blockIdx.x)) wait_vm<GA + 2 * GB>();
-    else wait_vm<0>();
+    // K-tile 0 landed. vmcnt retires in issue order: prologue (K-tile 0: 2 GA + 2 GB
+    // instructions, K-tile 1: GA + 2 GB), then the previous tile's epilogue stores; the count
+    // leaves K-tile 1 and those stores in flight (a wait for every store of the previous
+    // epilogue left 128 KB of stores per CU exposed between two tiles: ~6 us per tile at a
+    // K = 1024 BERT GEMM's ~14 us of MFMA work). Edge epilogues issue a data-dependent number
+    // of stores: wait for all.
+    if (prev == 2) wait_vm<0>();
+    else if (ktiles > 1) {
+      if (prev == 1) wait_vm<GA + 2 * GB + EPI_ST>();
+      else wait_vm<GA + 2 * GB>();
+    } else {
+      if (prev == 1) wait_vm<EPI_ST>();
+      else wait_vm<0>();
+    }
     barrier();
     if (lag) barrier();
     for (int kt = 0; kt < ktiles; ++kt) {
@@ -2103,9 +2120,11 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
       prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
     }
     // ------------------------------------------------------------ register epilogue
-    if (m0 + BM <= M && n0 + BN <= N) pers_epi<EK, false, BNH, WC>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
+    const bool whole = m0 + BM <= M && n0 + BN <= N;
+    if (whole) pers_epi<EK, false, BNH, WC>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
     else pers_epi<EK, true, BNH, WC>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
     if (nvt >= nblk) break;
+    prev = !ovl ? 0 : (whole && !fullwait ? 1 : 2);
     if (!ovl) {
       t = xcd_remap(nvt, nblk);
       prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
@@ -2202,9 +2221,12 @@ hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, 
         N % 8 == 0 && pe.ldo % 8 == 0 && (!pe.residual || pe.ldr % 4 == 0) && (!pe.bias || al16(pe.bias)) &&
         al16(pe.out) && (!pe.aux || al16(pe.aux)) && (!pe.residual || (reinterpret_cast<uintptr_t>(pe.residual) & 7) == 0)) {
       const int ovl = ::ttdk_rt::pers_flag() == 1;
+      // TTD_PERS_STORE_WAIT=1: wait for every store of the previous epilogue (A/B)
+      static const int fullwait = getenv_int("TTD_PERS_STORE_WAIT", 0);
 #define TTDK_PERS(EKV)                                                                                                \
   case EKV:                                                                                                           \
-    hipLaunchKernelGGL((gemm256p_kernel<BN, OA, OB, EKV>), dim3(cus), dim3(THR), 0, st, pa, pb, pe, M, N, K, tm, tn, ovl); \
+    hipLaunchKernelGGL((gemm256p_kernel<BN, OA, OB, EKV>), dim3(cus), dim3(THR), 0, st, pa, pb, pe, M, N, K, tm, tn, ovl, \
+                       fullwait);                                                                                     \
     return hipGetLastError();
       switch (ek) {
         TTDK_PERS(0)

@@ -95,6 +95,9 @@ class ResNet:
         # projection-shortcut backward (BN backward + strided dgrad) on the side stream, concurrent
         # with the block's c3 -> c2 data-gradient chain (joins before c1's dgrad accumulates into it)
         self.cd_side = os.environ.get("TTD_CD_SIDE", "1") != "0"
+        # forward projection shortcut on the side stream, concurrent with the block's c1 -> c2
+        # (TTD_FWD_PROJ_SIDE=0: inline on the main stream — no fork / join, fewer graph segments)
+        self.fwd_proj_side = os.environ.get("TTD_FWD_PROJ_SIDE", "1") != "0"
         # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
         # never stored: two HBM passes of the stage's largest tensor saved; TTD_FUSE_PROJ=0: off)
         self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
@@ -736,7 +739,8 @@ class ResNet:
                 o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm), defer=c3ok,
                                     want8=fp8 and not c3ok and self._fp8_conv(blk["c2"]), pro_big=pbig)
                 pend = None
-            if blk["cd"] is not None and side is not None:
+            proj_side = blk["cd"] is not None and side is not None and self.fwd_proj_side
+            if proj_side:
                 # projection shortcut on the side stream, concurrent with the c1 -> c2 chain
                 main = torch.cuda.current_stream()
                 graphs.fork(main, side)
@@ -764,7 +768,7 @@ class ResNet:
                 o2_8 = None
             else:
                 o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]), pro=pro2)
-            if blk["cd"] is not None and side is not None:
+            if proj_side:
                 graphs.join(main, side)
             elif blk["cd"] is not None:
                 sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
