@@ -1979,7 +1979,7 @@ __device__ __forceinline__ void pers_epi(const f32x4_t (&acc)[2][2][4][2], const
 template <int BN, class OA, class OB, int EK>
 __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::Params pa, typename OB::Params pb,
                                                                 EpiParams E, int M, int N, int K, int tiles_m,
-                                                                int tiles_n, int ovl, int fullwait, int prio) {
+                                                                int tiles_n, int ovl, int fullwait) {
   using Gm = Geo<BN>;
   constexpr int T = OA::THREADS, NW = T / 64, WN = NW / 2;
   static_assert(OB::THREADS == T && NW == 8, "8-wave operand policies");
@@ -2016,17 +2016,15 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
         else f[ks][b] = frag_mn<BNH>(sB, wn * WC + b * 16, ks, lane);
       }
   };
-  // prio 0: s_setprio(1) brackets every MFMA cluster; 1: static priority 1 for the lagging
-  // (younger, wm = 1) half, no per-cluster flips (MI355X_MICROARCH item 4); 2: no priorities
   auto mma = [&](const bf16x8_t (&x)[2][4], const bf16x8_t (&y)[2][NB], f32x4_t (&c)[4][NB]) {
-    if (prio == 0) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b) c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y[ks][b], x[ks][a], c[a][b], 0, 0, 0);
-    if (prio == 0) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   };
   // first two K-tiles of a tile: all four halves of K-tile 0, then A0 / B0 / B1 of K-tile 1
   // (its A1 is issued in the first phase of the main loop, as in gemm256_kernel)
@@ -2048,7 +2046,6 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
 
   int vt = blockIdx.x;
   if (vt >= nblk) return;
-  if (prio == 1 && lag) __builtin_amdgcn_s_setprio(1);
   int t = xcd_remap(vt, nblk);
   prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
   const float alpha_e = epi_alpha(E);
@@ -2132,229 +2129,6 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
       t = xcd_remap(nvt, nblk);
       prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
     }
-    vt = nvt;
-  }
-}
-
-// ---- 4-wave persistent GEMM: 256 x 256 tile, each wave a 128 x 128 quadrant (1 wave per SIMD)
-// hipBLASLt's kernel at the BERT shapes (MT256x256x64, PMC: profiles/r3_gemm_pmc_ours_vs_hipblaslt.txt)
-// runs half the waves of gemm256p_kernel: every A fragment feeds 8 MFMAs instead of 2-4, and the
-// 8-wave ping-pong's SQ_WAIT_ANY (34 % of wave cycles vs 10.6 %) disappears. Here:
-//   * 4 waves (wm, wn) = quadrant rows wm*128.., cols wn*128..; acc[8][8] f32x4 = 256 AGPRs;
-//   * K-tile 64, two LDS stages of A0 A1 B0 B1 halves (128 rows x 128 B each, the OpDenseK
-//     image: 16 LDS-DMA instructions per thread per K-tile); a wave reads only its own A and B
-//     halves (16 + 16 ds_read_b128 per K-tile);
-//   * fragments pipelined by K-half (ks): the ks = 1 reads are in flight under the ks = 0 MFMAs,
-//     the next K-tile's ks = 0 reads under the ks = 1 MFMAs; two barriers per K-tile (stage
-//     free -> DMA of K-tile + 2; K-tile + 1 landed -> its reads), both between MFMA blocks;
-//   * persistent over tiles like gemm256p_kernel (next tile's first two K-tiles in flight under
-//     the register epilogue, which stores 16 B per lane via lane-pair exchange).
-template <int EK, bool CHECK>
-__device__ __forceinline__ void pers_epi4(const f32x4_t (&acc)[8][8], const EpiParams& E, int m0, int n0, int M, int N,
-                                          float alpha, int lane, int wm, int wn) {
-  const int g = lane >> 4, i16 = lane & 15;
-  const bool odd = g & 1;
-  bf16_t* const out = static_cast<bf16_t*>(E.out);
-  constexpr bool LD = (EK & (kEkDGelu | kEkBeta)) != 0;
-  uint2 rvb[2][4][2], ovb[2][4][2];  // [slot][pair][b]
-  auto load_row = [&](int a, uint2 (&rv)[4][2], uint2 (&ov)[4][2]) {
-    const int m = m0 + wm * 128 + a * 16 + i16;
-    if (CHECK && m >= M) return;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int nb = n0 + wn * 128 + p * 32 + 4 * g;
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if constexpr ((EK & kEkDGelu) != 0)
-          if (!CHECK || nb + 16 * b < N)
-            rv[p][b] = *reinterpret_cast<const uint2*>(E.residual + static_cast<long long>(m) * E.ldr + nb + 16 * b);
-        if constexpr ((EK & kEkBeta) != 0)
-          if (!CHECK || nb + 16 * b < N)
-            ov[p][b] = *reinterpret_cast<const uint2*>(out + static_cast<long long>(m) * E.ldo + nb + 16 * b);
-      }
-    }
-  };
-  if constexpr (LD) load_row(0, rvb[0], ovb[0]);
-#pragma unroll
-  for (int a = 0; a < 8; ++a) {
-    if constexpr (LD)
-      if (a + 1 < 8) load_row(a + 1, rvb[(a + 1) & 1], ovb[(a + 1) & 1]);
-    const int m = m0 + wm * 128 + a * 16 + i16;
-    if (CHECK && m >= M) continue;
-    const long long row = static_cast<long long>(m) * E.ldo;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int nb = n0 + wn * 128 + p * 32 + 4 * g;  // block b: nb + 16 b
-      const uint2(&rv)[2] = rvb[a & 1][p];
-      const uint2(&ov)[2] = ovb[a & 1][p];
-      uint2 po[2], pa[2];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        f32x4_t v = acc[a][2 * p + b] * alpha;
-        if constexpr ((EK & kEkBias) != 0)
-          if (!CHECK || nb + 16 * b < N) v += *reinterpret_cast<const f32x4_t*>(E.bias + nb + 16 * b);
-        if constexpr ((EK & kEkDGelu) != 0) {
-          v[0] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].x & 0xffff)));
-          v[1] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].x >> 16)));
-          v[2] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].y & 0xffff)));
-          v[3] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv[b].y >> 16)));
-        }
-        if constexpr ((EK & kEkBeta) != 0) {
-          v[0] += bf2f(static_cast<bf16_t>(ov[b].x & 0xffff));
-          v[1] += bf2f(static_cast<bf16_t>(ov[b].x >> 16));
-          v[2] += bf2f(static_cast<bf16_t>(ov[b].y & 0xffff));
-          v[3] += bf2f(static_cast<bf16_t>(ov[b].y >> 16));
-        }
-        if constexpr ((EK & kEkAux) != 0) pa[b] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        if constexpr ((EK & kEkGelu) != 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
-        }
-        po[b] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      }
-      const int nst = odd ? nb + 12 : nb;  // odd lane: columns 4(g-1)+16.. of the pair
-      {
-        const uint2 snd = odd ? po[0] : po[1];
-        const uint2 rcv = make_uint2(__shfl_xor(snd.x, 16, 64), __shfl_xor(snd.y, 16, 64));
-        const uint4 w = odd ? make_uint4(rcv.x, rcv.y, po[1].x, po[1].y) : make_uint4(po[0].x, po[0].y, rcv.x, rcv.y);
-        if (!CHECK || nst < N) *reinterpret_cast<uint4*>(out + row + nst) = w;
-      }
-      if constexpr ((EK & kEkAux) != 0) {
-        const uint2 snd = odd ? pa[0] : pa[1];
-        const uint2 rcv = make_uint2(__shfl_xor(snd.x, 16, 64), __shfl_xor(snd.y, 16, 64));
-        const uint4 w = odd ? make_uint4(rcv.x, rcv.y, pa[1].x, pa[1].y) : make_uint4(pa[0].x, pa[0].y, rcv.x, rcv.y);
-        if (!CHECK || nst < N) *reinterpret_cast<uint4*>(E.aux + row + nst) = w;
-      }
-    }
-  }
-}
-
-// Dense K-major operand of gemm4w_kernel (256 threads, whole tiles only: no row clamp): the 4
-// DMA instructions of a thread per 128-row half are 32 rows apart and share the XOR chunk
-// (it depends on (row >> 1) & 7 = (tid >> 4) & 7 only), so one pointer per half and a uniform
-// 32-row stride replace OpDenseK's eight 64-bit pointers (VGPRs the 256-AGPR kernel needs).
-struct OpDenseK4 {
-  using Params = DenseP;
-  static constexpr int THREADS = 256;
-  static constexpr int G = 4;
-  const char* p0[2];
-  long long step;  // bytes between the 4 DMA rows of a thread (32 rows)
-  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
-    const int row = tid >> 3, slot = tid & 7;
-    const int chunk = slot ^ ((row >> 1) & 7);
-    step = 32LL * P.ld * 2;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      p0[h] = static_cast<const char*>(P.p) + static_cast<long long>(row0 + h * 128 + row) * P.ld * 2 + chunk * 16;
-  }
-  template <int H>
-  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
-    const char* b = p0[H] + static_cast<long long>(kt) * 128;
-#pragma unroll
-    for (int i = 0; i < G; ++i) glds(b + i * step, lds + (i * 256 + wave * 64) * 16);
-  }
-};
-
-template <class OA, class OB, int EK>
-__global__ __launch_bounds__(256, 1) void gemm4w_kernel(typename OA::Params pa, typename OB::Params pb, EpiParams E,
-                                                        int M, int N, int K, int tiles_m, int tiles_n) {
-  constexpr int T = 256;
-  static_assert(OA::THREADS == T && OB::THREADS == T, "4-wave operand policies");
-  constexpr int HALF = 128 * 128;  // 128 rows x 128 B
-  constexpr int STAGE = 4 * HALF;  // A0 A1 B0 B1
-  constexpr int KT_OPS = 2 * OA::G + 2 * OB::G;  // DMA instructions per thread per K-tile
-  constexpr int EPI_ST = 32 * (((EK & kEkAux) != 0) ? 2 : 1);  // stores per thread, whole tile
-  constexpr int W1 = (KT_OPS + EPI_ST) < 63 ? KT_OPS + EPI_ST : 63;
-  constexpr int W0 = EPI_ST < 63 ? EPI_ST : 63;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  const int nblk = tiles_m * tiles_n;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int ktiles = K / 64;
-  auto stage = [&](int kt) { return smem + (kt & 1) * STAGE; };
-  OA la;
-  OB lb;
-  auto issue_kt = [&](int kt) {
-    char* st = stage(kt);
-    la.template issue<0>(st, kt, wave);
-    la.template issue<1>(st + HALF, kt, wave);
-    lb.template issue<0>(st + 2 * HALF, kt, wave);
-    lb.template issue<1>(st + 3 * HALF, kt, wave);
-  };
-  auto prologue = [&](int m0, int n0) {
-    la.init(pa, m0, tid);
-    lb.init(pb, n0, tid);
-    issue_kt(0);
-    if (ktiles > 1) issue_kt(1);
-  };
-  bf16x8_t fa[2][8], fb[2][8];
-  auto read_ks = [&](int kt, int ks) {
-    const char* sa = stage(kt) + wm * HALF;
-    const char* sb = stage(kt) + 2 * HALF + wn * HALF;
-#pragma unroll
-    for (int a = 0; a < 8; ++a) fa[ks][a] = frag_k(sa, a * 16, ks, lane);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) fb[ks][b] = frag_k(sb, b * 16, ks, lane);
-  };
-  f32x4_t acc[8][8];
-  auto mma_ks = [&](int ks) {
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][b], fa[ks][a], acc[a][b], 0, 0, 0);
-  };
-
-  int vt = blockIdx.x;
-  if (vt >= nblk) return;
-  int t = xcd_remap(vt, nblk);
-  prologue((t / tiles_n) * BM, (t % tiles_n) * 256);
-  const float alpha_e = epi_alpha(E);
-  int prev = 0;  // 0: nothing after this tile's prologue DMA; 1: a whole-tile epilogue's stores; 2: an edge epilogue
-  for (;;) {
-    const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * 256;
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // K-tile 0 landed (K-tile 1 and the previous epilogue's stores may stay in flight)
-    if (prev == 2) wait_vm<0>();
-    else if (ktiles > 1) {
-      if (prev == 1) wait_vm<W1>();
-      else wait_vm<KT_OPS>();
-    } else {
-      if (prev == 1) wait_vm<W0>();
-      else wait_vm<0>();
-    }
-    barrier();
-    read_ks(0, 0);
-    const int nvt = vt + gridDim.x;
-    for (int kt = 0; kt < ktiles; ++kt) {
-      read_ks(kt, 1);
-      mma_ks(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      barrier();  // every wave's reads of stage kt are done
-      if (kt + 2 < ktiles) {
-        issue_kt(kt + 2);
-        wait_vm<KT_OPS>();  // K-tile kt + 1 landed
-      } else if (kt + 1 < ktiles) {
-        wait_vm<0>();
-      } else if (nvt < nblk) {
-        // both stages free: the next tile's first two K-tiles go in flight under the epilogue
-        t = xcd_remap(nvt, nblk);
-        prologue((t / tiles_n) * BM, (t % tiles_n) * 256);
-      }
-      if (kt + 1 < ktiles) {
-        barrier();  // publish K-tile kt + 1
-        read_ks(kt + 1, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      mma_ks(1);
-    }
-    // (whole tiles only: the launcher requires M % 256 == 0 and N % 256 == 0)
-    pers_epi4<EK, false>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
-    if (nvt >= nblk) break;
-    prev = 1;
     vt = nvt;
   }
 }
@@ -2449,32 +2223,11 @@ hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, 
       const int ovl = ::ttdk_rt::pers_flag() == 1;
       // TTD_PERS_STORE_WAIT=1: wait for every store of the previous epilogue (A/B)
       static const int fullwait = getenv_int("TTD_PERS_STORE_WAIT", 0);
-      static const int prio = getenv_int("TTD_PERS_PRIO", 0);
 #define TTDK_PERS(EKV)                                                                                                \
   case EKV:                                                                                                           \
     hipLaunchKernelGGL((gemm256p_kernel<BN, OA, OB, EKV>), dim3(cus), dim3(THR), 0, st, pa, pb, pe, M, N, K, tm, tn, ovl, \
-                       fullwait, prio);                                                                               \
+                       fullwait);                                                                                     \
     return hipGetLastError();
-      // TTD_GEMM4W=1: the 4-wave 128x128-per-wave persistent kernel for dense K-major operands
-      static const int w4 = getenv_int("TTD_GEMM4W", 0);
-      if constexpr (std::is_same<OA, OpDenseK<128, 2, THR>>::value && std::is_same<OB, OpDenseK<128, 2, THR>>::value) {
-        if (w4 && K % 64 == 0 && M % 256 == 0 && N % 256 == 0) {
-          using A4 = OpDenseK4;
-#define TTDK_P4(EKV)                                                                                                 \
-  case EKV:                                                                                                          \
-    hipLaunchKernelGGL((gemm4w_kernel<A4, A4, EKV>), dim3(cus), dim3(256), 0, st, pa, pb, pe, M, N, K, tm, tn);      \
-    return hipGetLastError();
-          switch (ek) {
-            TTDK_P4(0)
-            TTDK_P4(kEkBias)
-            TTDK_P4(kEkBias | kEkAux | kEkGelu)
-            TTDK_P4(kEkDGelu)
-            TTDK_P4(kEkBeta)
-            default: break;
-          }
-#undef TTDK_P4
-        }
-      }
       switch (ek) {
         TTDK_PERS(0)
         TTDK_PERS(kEkBias)
