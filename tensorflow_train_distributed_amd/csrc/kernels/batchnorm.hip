@@ -435,14 +435,19 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
 }
 
 // dz = a*g + b*y + c, g = dy * [out > 0] (ReLU mask bit, or `out` > 0, or no mask).
+// q8: optional OCP e5m2 copy of dz (fp8 data gradients, ResNet config 5) quantised with the
+// slot's delayed scale; this step's amax goes to the slot's 64 amax lanes (fp8.hip).
 template <bool FIXED>
 __global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ out,
                                                              const uint8_t* __restrict__ mask,
                                                              const bf16_t* __restrict__ y,
                                                              const float* __restrict__ coef, bf16_t* __restrict__ dz,
+                                                             uint8_t* __restrict__ q8, float* __restrict__ q8_slot,
                                                              long long n8, int C) {
   const int cg = C >> 3;
+  const float qs = q8 ? q8_slot[2] : 1.f;
+  float qmax = 0.f;
   float ca[8], cb[8], cc[8];
   auto load_coef = [&](int c0) {
 #pragma unroll
@@ -492,7 +497,33 @@ __global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __res
       unpack8(yv[u], yf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = ca[j] * g[j] + cb[j] * yf[j] + cc[j];
-      reinterpret_cast<uint4*>(dz)[i] = pack8(g);
+      const uint4 packed = pack8(g);
+      reinterpret_cast<uint4*>(dz)[i] = packed;
+      if (q8) {  // the stored bf16 values, scaled, saturated to the e5m2 range
+        float fq[8];
+        unpack8(packed, fq);
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          qmax = fmaxf(qmax, fabsf(fq[j]));
+          const float v = fminf(fmaxf(fq[j] * qs, -57344.f), 57344.f);
+          const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_cvt_pk_bf8_f32(v, v, 0, false) & 0xff);
+          if (j < 4) lo |= b << (8 * j);
+          else hi |= b << (8 * (j - 4));
+        }
+        reinterpret_cast<uint2*>(q8)[i] = make_uint2(lo, hi);
+      }
+    }
+  }
+  if (q8) {
+    __shared__ float red[kThreads / 64];
+    qmax = wave_max(qmax);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = qmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = red[0];
+      for (int w = 1; w < kThreads / 64; ++w) m = fmaxf(m, red[w]);
+      atomicMax(reinterpret_cast<unsigned int*>(q8_slot + 8 + (blockIdx.x & 63)), __float_as_uint(m));
     }
   }
 }
@@ -580,16 +611,24 @@ TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* 
   return hipGetLastError();
 }
 
-TTDK_EXPORT int ttdk_bn_bwd_apply(const bf16_t* dy, const bf16_t* out, const uint8_t* mask, const bf16_t* y,
-                                  const float* coef, bf16_t* dz, long long n, int C, hipStream_t st) {
-  if (C % 8 || n % 8) return hipErrorInvalidValue;
+TTDK_EXPORT int ttdk_bn_bwd_apply_q8(const bf16_t* dy, const bf16_t* out, const uint8_t* mask, const bf16_t* y,
+                                     const float* coef, bf16_t* dz, uint8_t* q8, float* q8_slot, long long n, int C,
+                                     hipStream_t st) {
+  if (C % 8 || n % 8 || (q8 && !q8_slot)) return hipErrorInvalidValue;
   const long long n8 = n / 8;
   const int grid = grid_for(n8, kThreads * kUnroll);
   if (kThreads % (C >> 3) == 0)
-    hipLaunchKernelGGL(bwd_apply_kernel<true>, dim3(grid), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, n8, C);
+    hipLaunchKernelGGL(bwd_apply_kernel<true>, dim3(grid), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, q8, q8_slot,
+                       n8, C);
   else
-    hipLaunchKernelGGL(bwd_apply_kernel<false>, dim3(grid), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, n8, C);
+    hipLaunchKernelGGL(bwd_apply_kernel<false>, dim3(grid), dim3(kThreads), 0, st, dy, out, mask, y, coef, dz, q8,
+                       q8_slot, n8, C);
   return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bn_bwd_apply(const bf16_t* dy, const bf16_t* out, const uint8_t* mask, const bf16_t* y,
+                                  const float* coef, bf16_t* dz, long long n, int C, hipStream_t st) {
+  return ttdk_bn_bwd_apply_q8(dy, out, mask, y, coef, dz, nullptr, nullptr, n, C, st);
 }
 
 // Slab rows (slices) ttdk_bn_reduce_finalize uses for T partial rows: the caller provides a

@@ -96,3 +96,22 @@ TTDK_EXPORT int ttdk_gemm_fp8(const uint8_t* A, long long lda, const uint8_t* B,
   TTDK_F8(128, 64, 1);
 #undef TTDK_F8
 }
+
+// fp8 data gradient of a unit-stride conv on the block-scaled MFMA: dy8 [N,P,Q,K] in OCP e5m2
+// (gradients), wt8 = the filter transposed to [C][R][S][K] in e4m3; dx = dequant (epi.ascale0 x
+// epi.ascale1) of the implicit-GEMM gather, with the bf16 path's epilogues (accumulate, next BN's
+// masked gradient + backward statistics on 256-row tiles). K % 128 == 0 (one 128-element K-tile
+// inside one tap).
+TTDK_EXPORT int ttdk_conv_dgrad_fp8(const uint8_t* dy8, const uint8_t* wt8, const TtdkConv* g, const TtdkEpilogue* epi,
+                                    hipStream_t st) {
+  if (g->sh != 1 || g->sw != 1 || g->dh != 1 || g->dw != 1 || g->K % 128 || g->C % 8) return hipErrorInvalidValue;
+  EpiParams pe = to_epi(epi);
+  if (pe.remap || pe.residual || pe.bH || pe.by2 || pe.mode != 0) return hipErrorInvalidValue;
+  if (pe.by && (pe.stat == nullptr || pe.ldo % 8 || pe.act)) return hipErrorInvalidValue;
+  const int N = g->C, K = g->R * g->S * g->K;
+  const int M = g->N * g->H * g->W;
+  const big::ConvP pa = conv_params(dy8, g->P, g->Q, g->K, g->H, g->W, g, M);
+  const big::DenseP pb{wt8, K, N};
+  if (N >= 256) return big::launch<256, big::OpConvK<128, 1, true, true>, big::OpDenseK<128, 1>, 2>(pa, pb, pe, M, N, K, 1, st);
+  return big::launch<128, big::OpConvK<128, 1, true, true>, big::OpDenseK<64, 1>, 2>(pa, pb, pe, M, N, K, 1, st);
+}

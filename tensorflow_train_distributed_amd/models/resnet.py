@@ -98,6 +98,12 @@ class ResNet:
         # forward projection shortcut on the side stream, concurrent with the block's c1 -> c2
         # (TTD_FWD_PROJ_SIDE=0: inline on the main stream — no fork / join, fewer graph segments)
         self.fwd_proj_side = os.environ.get("TTD_FWD_PROJ_SIDE", "1") != "0"
+        # ... joined after the block's c3 when c3's BN apply is deferred into the next c1
+        # (TTD_LATE_PROJ_JOIN=0: before c3, as the apply pass needs it)
+        self.late_proj_join = os.environ.get("TTD_LATE_PROJ_JOIN", "1") != "0"
+        # precision="fp8": unit-stride 3x3 data gradients on the fp8 MFMA with e5m2 gradients
+        # (TTD_FP8_DGRAD=0: bf16 data gradients)
+        self.fp8_dgrad = os.environ.get("TTD_FP8_DGRAD", "1") != "0"
         # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
         # never stored: two HBM passes of the stage's largest tensor saved; TTD_FUSE_PROJ=0: off)
         self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
@@ -202,11 +208,27 @@ class ResNet:
         self._a_slots = torch.zeros((4 * len(self.blocks) + 4, FP8_SLOT), dtype=torch.float32, device=self.device)
         self._a_slots[:, 2] = 1.0
         self._a_slots[:, 3] = 1.0
+        # fp8 data gradients (unit-stride 3x3 convs with >= 128 output channels: the stage 3-5 c2
+        # units off the halo kernel): dz in OCP e5m2 with delayed per-tensor scaling (one slot per
+        # conv; the BN backward-apply pass that produces dz writes the copy and this step's amax),
+        # the filter transposed to [C,R,S,K] in e4m3 with current scaling (from the step's
+        # WeightPrep buffer). The first step only collects the gradient amax (bf16 dgrad).
+        self._g8 = {c.name: i for i, c in enumerate(c for c in self.conv_list() if self._fp8_dgrad_conv(c))}
+        self._g_slots = torch.zeros((max(1, len(self._g8)), FP8_SLOT), dtype=torch.float32, device=self.device)
+        self._g_slots[:, 2] = 1.0
+        self._g_slots[:, 3] = 1.0
+        self._fp8_bwd_steps = 0
         self._fp8 = True
+
+    def _fp8_dgrad_conv(self, c: ConvSpec) -> bool:
+        return (self.precision == "fp8" and self.fp8_dgrad and c.k == 3 and c.stride == 1 and c.cout % 128 == 0
+                and c.cin_store % 8 == 0 and not self._c3_ok(c, 56, 56))
 
     def _fp8_step_begin(self):
         from ..ops import kernels as K
         K.fp8_rollover(self._a_slots, margin=0.9)
+        if self._g8:
+            K.fp8_rollover(self._g_slots, margin=0.5, fmax=57344.0)
         K.fp8_quant_weights(self.params.compute, self._w8_flat, self._w8_table, self._w8_n, self._w8_max,
                             self._w8_slots)
         self._a_next = 0
@@ -540,9 +562,17 @@ class ResNet:
             out = G.conv_dgrad(dout, wt, x.shape, stride, pad, out=dx, beta=dx_beta, beta_s2=bs2, bn_pro=pro)
             self._wgrad(c, x, dz, wname)
             return out, None
+        dz8 = None
         if dstat is not None:
+            g8 = (self._fp8 is not None and need_dx and c.name in self._g8 and self._wp_cur is not None
+                  and feeds is not None and feeds2 is None and dx is None)
+            q8 = torch.empty(y.numel(), dtype=torch.uint8, device=y.device) if g8 else None
             dz = K.bn_backward_from_partial(dout.view(M, Kc), y.view(M, Kc), P.var[pre + "gamma"], st,
-                                            P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1]).view(N, Pp, Q, Kc)
+                                            P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1], q8=q8,
+                                            q8_slot=self._g_slots[self._g8[c.name]] if g8 else None
+                                            ).view(N, Pp, Q, Kc)
+            if g8 and self._fp8_bwd_steps >= 1:  # (step 0 only collects the gradient amax)
+                dz8 = q8.view(N, Pp, Q, Kc)
         else:
             dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
                                P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
@@ -553,6 +583,16 @@ class ResNet:
             return None, None
         wt = self._crsk(wname)
         bs2 = (x.shape[1], x.shape[2]) if dx_sampled else None
+        if dz8 is not None:
+            # fp8 data gradient (e5m2 dz x e4m3 transposed filter) with the feeding unit's masked
+            # gradient + BN-backward sums in its epilogue
+            _, fy, fmask, _ = feeds
+            kind, off, shape = self._wp_cur._views[wname]
+            wt8 = self._wt8_buf[off:off + int(np.prod(shape))].view(shape)
+            i8 = self._g8[c.name]
+            out, partial, T = G.conv_dgrad_fp8(dz8, wt8, x.shape, stride, pad, bn_stat=(fy, fmask),
+                                               ascale=(self._g_slots[i8][3:4], self._wt8_slots[i8][3:4]))
+            return out, (partial, T)
         if (feeds is not None and feeds2 is None and dx is None and self.fuse_bn_bwd and self.c3_dgrad == 2
                 and self._c3_ok(c, x.shape[1], x.shape[2])):
             # halo 3x3 kernel (flipped filter) with the feeding unit's BN-backward sums in its epilogue
@@ -607,6 +647,21 @@ class ResNet:
             H, W = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
         self._wp = wp.build()
         self._wp_key = key
+        if self._fp8 is not None and self._g8:
+            # e4m3 copies of the fp8-dgrad convs' transposed filters, quantised from the WeightPrep
+            # buffer (same element offsets) with current per-tensor scaling
+            rows = []
+            for c in self.conv_list():
+                if c.name in self._g8:
+                    kind, off, shape = wp._views[c.name + "_conv/kernel"]
+                    rows.append((off, int(np.prod(shape)), self._g8[c.name]))
+            arr = np.zeros(len(rows), dtype=np.dtype([("off", "<i8"), ("len", "<i4"), ("slot", "<i4")]))
+            for i, r in enumerate(rows):
+                arr[i] = r
+            self._wt8_table = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
+            self._wt8_n, self._wt8_max = len(rows), max(r[1] for r in rows)
+            self._wt8_buf = torch.empty(wp.buf.numel(), dtype=torch.uint8, device=self.device)
+            self._wt8_slots = torch.zeros((len(self._g8), K.FP8_SLOT), dtype=torch.float32, device=self.device)
         return self._wp
 
     def _crsk(self, wname):
@@ -699,6 +754,9 @@ class ResNet:
             # this step's data-gradient filters (the weights are final until the optimizer runs)
             self._wp_cur = self._weight_prep(tuple(images.shape))
             self._wp_cur.run()
+            if fp8 and self._g8:
+                K.fp8_quant_weights(self._wp_cur.buf, self._wt8_buf, self._wt8_table, self._wt8_n, self._wt8_max,
+                                    self._wt8_slots)
 
         def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None, pro=None,
                  pro_big=False):
@@ -768,13 +826,6 @@ class ResNet:
                 o2_8 = None
             else:
                 o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]), pro=pro2)
-            if proj_side:
-                graphs.join(main, side)
-            elif blk["cd"] is not None:
-                sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
-            else:
-                sc, cd = h, None
-            sc_bn = (cd[3].scale, cd[3].shift) if cd is not None and self.fuse_proj else None
             defer3 = (nxt is not None and self._pw_part("c31") and self._pw_fwd_ok(nxt["c1"], True)
                       and not self._fp8_conv(nxt["c1"]))
             c3_in = y2 if fuse23 else o2
@@ -782,9 +833,22 @@ class ResNet:
             if not defer3 and nxt is not None:
                 # or on the 256-row kernel's operand prologue (stage-3/4 widths)
                 defer3 = defer_big = self._fwd_pro_ok(nxt["c1"], tuple(c3_in.shape[:3]) + (blk["c3"].cout,))
+            # the shortcut is first read by c3's apply pass, or — when c3's BN apply is deferred into
+            # the next block's c1 — only there: the join then waits until after c3 (the side-stream
+            # projection gets c3's duration too; it measured 0.2-0.3 ms exposed before c3)
+            late_join = proj_side and defer3 and self.late_proj_join
+            if proj_side and not late_join:
+                graphs.join(main, side)
+            elif blk["cd"] is not None and not proj_side:
+                sc, cd, _ = unit(blk["cd"], h, False, inp8=h8, defer=self.fuse_proj)
+            elif blk["cd"] is None:
+                sc, cd = h, None
+            sc_bn = (cd[3].scale, cd[3].shift) if cd is not None and self.fuse_proj else None
             c3_pro = (c2[3].scale, c2[3].shift, None, None, o2, c2[2]) if fuse23 else None
             if defer3:
                 y3, c3, _ = unit(blk["c3"], c3_in, True, defer=True, pro=c3_pro)
+                if late_join:
+                    graphs.join(main, side)
                 pend = (y3, c3[3], sc, sc_bn, c3, defer_big)
                 o3, h8 = None, None
             else:
@@ -859,6 +923,8 @@ class ResNet:
             graphs.join(torch.cuda.current_stream(), self._wgrad_stream)
             self._wgrad_stream = None
         self._side_keep = []
+        if fp8:
+            self._fp8_bwd_steps += 1
         bwd_range.__exit__(None, None, None)
         self._grad_hook = None
         return sums

@@ -89,6 +89,7 @@ _SIGS = {
     "ttdk_bn_bwd_finalize": [P, F, I, P, P, P, P, P, P, I, P],
     "ttdk_bn_apply": [P, P, P, P, P, P, P, P, P, P, L, I, I, P],
     "ttdk_bn_bwd_apply": [P, P, P, P, P, P, L, I, P],
+    "ttdk_bn_bwd_apply_q8": [P, P, P, P, P, P, P, P, L, I, P],
     # pool.hip
     "ttdk_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "ttdk_maxpool_bwd": [P, P, P] + [I] * 12 + [P],

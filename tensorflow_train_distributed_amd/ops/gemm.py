@@ -737,6 +737,7 @@ def stem_wgrad(x, g_out, y, coef, *, out=None, beta=0):
 _lib.register({
     "ttdk_conv_fwd_fp8": [_lib.P, _lib.P, _lib.G, _lib.I, _lib.E, _lib.P],
     "ttdk_gemm_fp8": [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.I, _lib.I, _lib.E, _lib.P],
+    "ttdk_conv_dgrad_fp8": [_lib.P, _lib.P, _lib.G, _lib.E, _lib.P],
 })
 
 
@@ -779,4 +780,41 @@ def conv_fwd_fp8(x8, w8, stride=(1, 1), padding=(0, 0), *, alpha=1.0, out=None, 
     _log("fwd8_%dx%d_s%d" % (g.R, g.S, g.sh), M, N, K)
     e = _epi(out, ldo=g.K, residual=residual, act=act, stat=stat, alpha=alpha, ascale=ascale)
     _lib.call("ttdk_conv_fwd_fp8", x8.data_ptr(), w8.data_ptr(), ctypes.byref(g), bn, ctypes.byref(e), _lib.stream())
+    return out
+
+
+def conv_dgrad_fp8_ok(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
+    """Whether conv_dgrad_fp8 takes this data gradient: unit stride, the output gradient's
+    channels (wt_shape[-1]) a multiple of 128, wt_shape = [C, R, S, K]."""
+    C, R, S, K = wt_shape
+    return tuple(stride) == (1, 1) and K % 128 == 0 and C % 8 == 0
+
+
+def conv_dgrad_fp8(dy8, wt8, x_shape, stride=(1, 1), padding=(0, 0), *, ascale, out=None, beta=0, bn_stat=None,
+                   beta_s2=None):
+    """fp8 data gradient: dy8 [N,P,Q,K] OCP e5m2 (uint8), wt8 [C,R,S,K] e4m3 (uint8), unit
+    stride; ascale = (inv scale of dy8, inv scale of wt8) as device fp32 scalars. Epilogues as
+    conv_dgrad: beta accumulate (beta_s2 sampled rows), bn_stat=(y, mask) -> (out, partial, T)
+    with 256-row statistics tiles."""
+    if dy8.dtype != torch.uint8 or wt8.dtype != torch.uint8:
+        raise ValueError("conv_dgrad_fp8 wants uint8 operands")
+    C, R, S, K = wt8.shape
+    if not conv_dgrad_fp8_ok(x_shape, wt8.shape, stride, padding):
+        raise ValueError("conv_dgrad_fp8: unit stride and K % 128 == 0 required")
+    g = conv_geom(tuple(x_shape), (K, R, S, C), stride, padding)
+    if out is None:
+        out = torch.empty(tuple(x_shape), dtype=torch.bfloat16, device=dy8.device)
+    M = g.N * g.H * g.W
+    _log("dgrad8_%dx%d_s%d" % (R, S, stride[0]), M, C, R * S * K)
+    if bn_stat is not None:
+        y, mask = bn_stat
+        T = -(-M // 256)
+        partial = torch.empty((T, 2, C), dtype=torch.float32, device=dy8.device)
+        e = _epi(out, ldo=C, beta=beta, stat=partial, by=y, bmask=mask, beta_s2=beta_s2 if beta else None,
+                 ascale=ascale)
+        _lib.call("ttdk_conv_dgrad_fp8", dy8.data_ptr(), wt8.data_ptr(), ctypes.byref(g), ctypes.byref(e),
+                  _lib.stream())
+        return out, partial, T
+    e = _epi(out, ldo=C, beta=beta, beta_s2=beta_s2 if beta else None, ascale=ascale)
+    _lib.call("ttdk_conv_dgrad_fp8", dy8.data_ptr(), wt8.data_ptr(), ctypes.byref(g), ctypes.byref(e), _lib.stream())
     return out

@@ -97,9 +97,10 @@ def bn_apply(y2d, scale, shift, *, residual=None, residual_bn=None, relu=False, 
 FP8_SLOT = 72  # floats per fp8 scaling slot (see fp8.hip)
 
 
-def fp8_rollover(slots, margin=1.0):
-    """Delayed scaling step for fp8 activation slots [n, FP8_SLOT] (see fp8.hip)."""
-    _lib.call("ttdk_fp8_rollover", slots.data_ptr(), slots.shape[0], 448.0, float(margin), _s())
+def fp8_rollover(slots, margin=1.0, fmax=448.0):
+    """Delayed scaling step for fp8 slots [n, FP8_SLOT] (see fp8.hip): e4m3 activations (fmax
+    448), e5m2 gradients (fmax 57344)."""
+    _lib.call("ttdk_fp8_rollover", slots.data_ptr(), slots.shape[0], float(fmax), float(margin), _s())
 
 
 def fp8_quant_weights(src, dst, table, n_tensors, max_len, slots):
@@ -136,16 +137,19 @@ def bn_backward_coef(M, C, gamma, state, dgamma, dbeta, partial, T, *, accumulat
     return coef
 
 
-def bn_backward_from_partial(g, y, gamma, state, dgamma, dbeta, partial, T, *, dz=None, accumulate=False):
+def bn_backward_from_partial(g, y, gamma, state, dgamma, dbeta, partial, T, *, dz=None, accumulate=False, q8=None,
+                             q8_slot=None):
     """BN backward when the producer of the (already ReLU-masked) gradient g also emitted the
     per-tile sums (sum g, sum g*y) — ops.gemm.conv_dgrad(bn_stat=...): finalize + one apply
-    pass, no separate statistics pass over g and y."""
+    pass, no separate statistics pass over g and y. q8 (uint8 like dz): an OCP e5m2 copy of dz
+    quantised with the delayed scale of q8_slot (fp32[FP8_SLOT]; its amax lanes collect this
+    step's amax)."""
     M, C = y.shape
     coef = bn_backward_coef(M, C, gamma, state, dgamma, dbeta, partial, T, accumulate=accumulate, device=y.device)
     if dz is None:
         dz = torch.empty_like(y)
-    _lib.call("ttdk_bn_bwd_apply", g.data_ptr(), None, None, y.data_ptr(), coef.data_ptr(), dz.data_ptr(), M * C, C,
-              _s())
+    _lib.call("ttdk_bn_bwd_apply_q8", g.data_ptr(), None, None, y.data_ptr(), coef.data_ptr(), dz.data_ptr(),
+              _p(q8), _p(q8_slot), M * C, C, _s())
     return dz
 
 

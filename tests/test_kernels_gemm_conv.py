@@ -658,3 +658,68 @@ def test_weight_prep_matches_per_conv_transposes_and_phase_filters():
     a = G.conv_dgrad(dy, wt, x_shape, (2, 2), (1, 1))
     b = G.conv_dgrad(dy, torch.zeros_like(wt), x_shape, (2, 2), (1, 1), ws=wp.phases("w1/phases"))
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(8, 14, 14, 256, 256), (4, 28, 28, 128, 128), (2, 7, 7, 512, 512)])
+def test_conv_dgrad_fp8_e5m2_vs_fp32_oracle(cfg):
+    """fp8 data gradient (e5m2 dy x e4m3 transposed filter, block-scaled MFMA) of a 3x3/s1 conv vs
+    F.conv2d's fp32 input gradient on the DEQUANTISED operands (tight), vs the bf16 operands
+    (fp8 rounding: loose), and with the feeding-BN statistics epilogue vs the bf16 dgrad's."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    N, H, W, C, Kc = cfg
+    torch.manual_seed(11)
+    w = (torch.randn(Kc, 3, 3, C, device="cuda") / (9 * C) ** 0.5).bfloat16()
+    dy = (torch.randn(N, H, W, Kc, device="cuda") * 3e-4).bfloat16()
+    s_dy = torch.tensor([57344.0 * 0.5 / float(dy.float().abs().max())], device="cuda")
+    s_w = torch.tensor([448.0 / float(w.float().abs().max())], device="cuda")
+    dy8 = K.quant_fp8(dy, s_dy, e5m2=True)
+    wt = K.krsc_to_crsk(w)
+    wt8 = K.quant_fp8(wt, s_w)
+    inv = (1.0 / s_dy, 1.0 / s_w)
+    dx = G.conv_dgrad_fp8(dy8, wt8, (N, H, W, C), (1, 1), (1, 1), ascale=inv)
+    dyq = K.dequant_fp8(dy8, s_dy, e5m2=True).float()
+    wq = K.dequant_fp8(wt8, s_w).float()  # [C,3,3,K]
+    x = torch.zeros(N, C, H, W, device="cuda", requires_grad=True)
+    y = F.conv2d(x, wq.permute(3, 0, 1, 2), padding=1)  # w [K,C,3,3] from the transposed copy
+    y.backward(dyq.permute(0, 3, 1, 2))
+    ref = x.grad.permute(0, 2, 3, 1)
+    assert _rel(dx, ref) < 1e-2
+    ref_bf = G.conv_dgrad(dy, wt, (N, H, W, C), (1, 1), (1, 1)).float()
+    assert _rel(dx, ref_bf) < 0.12
+    # feeding-BN epilogue: masked gradient + (sum g, sum g*y) partial sums
+    yb = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    mask = torch.randint(0, 256, (N * H * W * C // 8,), dtype=torch.uint8, device="cuda")
+    out8, part8, T8 = G.conv_dgrad_fp8(dy8, wt8, (N, H, W, C), (1, 1), (1, 1), ascale=inv, bn_stat=(yb, mask))
+    bits = ((mask.view(-1, 1) >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1).view(N, H, W, C).float()
+    g_ref = (dx.float() * bits)
+    assert _rel(out8, g_ref) < 1e-2
+    sums = part8[:T8].sum(0)
+    assert torch.allclose(sums[0], out8.float().view(-1, C).sum(0), rtol=2e-2, atol=1e-6)
+    assert torch.allclose(sums[1], (out8.float() * yb.float()).view(-1, C).sum(0), rtol=2e-2, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_bn_backward_apply_e5m2_copy_and_amax():
+    """The BN backward-apply pass's OCP e5m2 copy of dz (delayed scale from the slot) dequantises
+    to dz within e5m2 rounding, and the slot's amax lanes receive max |dz|."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(5)
+    M, C = 4096, 256
+    g = (torch.randn(M, C, device="cuda") * 1e-3).bfloat16()
+    y = torch.randn(M, C, device="cuda").bfloat16()
+    st = K.BNState(C, "cuda")
+    st.mean.copy_(y.float().mean(0))
+    st.rstd.copy_(torch.rsqrt(y.float().var(0, unbiased=False) + 1e-5))
+    gamma = torch.rand(C, device="cuda") + 0.5
+    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    part = torch.stack([g.float().sum(0), (g.float() * y.float()).sum(0)]).unsqueeze(0).contiguous()
+    slot = torch.zeros(K.FP8_SLOT, device="cuda")
+    slot[2] = 2.0 ** 16
+    slot[3] = 2.0 ** -16
+    q8 = torch.empty(M * C, dtype=torch.uint8, device="cuda")
+    dz = K.bn_backward_from_partial(g, y, gamma, st, dg, db, part, 1, q8=q8, q8_slot=slot)
+    back = K.dequant_fp8(q8, slot[2:3], e5m2=True).float().view(M, C)
+    assert _rel(back, dz.float()) < 0.08
+    assert abs(float(slot[8:72].max()) - float(dz.float().abs().max())) <= 1e-6 + 1e-2 * float(dz.float().abs().max())

@@ -189,8 +189,9 @@ def test_resnet_step_segmented_capture_matches_eager():
 @pytest.mark.gpu
 def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
     """precision="fp8": the 3x3 convs with 128-multiple input channels run the fp8 block-scaled
-    MFMA forward with delayed activation scaling; the step must track the bf16 engine and train
-    with LAMB."""
+    MFMA forward with delayed activation scaling, and the unit-stride 3x3 data gradients the fp8
+    MFMA with e5m2 gradients (delayed scaling; step 1 calibrates both); the step must track the
+    bf16 engine and train with LAMB."""
     from tensorflow_train_distributed_amd.train.flat import FlatLAMB, Schedule
     torch.manual_seed(0)
     stages = ((64, 2, 1), (128, 2, 2), (256, 1, 2))
@@ -199,6 +200,7 @@ def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
     ref = ResNet(stages, num_classes=10, device="cuda", seed=7)
     f8 = ResNet(stages, num_classes=10, device="cuda", seed=7, precision="fp8")
     assert sum(f8._fp8_conv(c) for c in f8.conv_list()) >= 3
+    assert len(f8._g8) >= 1  # a unit-stride 3x3 data gradient on the fp8 MFMA (e5m2 gradients) from step 2
     s_ref = ref.forward_backward(x, y).clone()
     f8.forward_backward(x, y)  # step 1 calibrates the delayed activation scales
     s8 = f8.forward_backward(x, y).clone()
