@@ -195,3 +195,41 @@ def test_gpu_sequential_training_with_flat_adam():
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < losses[0] * 0.5, losses
+
+
+def test_weight_prep_table_layout_cpu():
+    """WeightPrep (one launch for every data-gradient filter operand): the sub-pixel phase
+    entries follow ops.gemm's phase order and partition the taps, the output views tile the
+    buffer without overlap, and tile_begin is the running tile count (checked without a GPU)."""
+    import numpy as np
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    src = torch.zeros(10_000_000, dtype=torch.bfloat16)
+    wp = K.WeightPrep(src)
+    shapes = {"a": (256, 1, 1, 64), "b": (128, 3, 3, 128), "c": (512, 3, 3, 256)}
+    off = 0
+    for n, s in shapes.items():
+        wp.add(n, off, s)
+        if s[1] == 3:
+            wp.add(n + "/phases", off, s, sub=(2, 1, 1, 28, 28))
+        off += int(np.prod(s))
+    wp.build()
+    rows = wp._tab.numpy().view(K.WeightPrep._DT)
+    tiles = 0
+    for r in rows:
+        assert r["tile_begin"] == tiles
+        tiles += r["Tr"] * r["Ts"] * (-(-r["K"] // 32)) * (-(-r["C"] // 32))
+    assert tiles == wp._tiles
+    for n, s in shapes.items():
+        Kc, R, S, C = s
+        assert tuple(wp.crsk(n).shape) == (C, R, S, Kc)
+        if R == 3:
+            ph = wp.phases(n + "/phases")
+            assert ph.numel() == C * R * S * Kc  # the phases partition the 9 taps
+            want = [(T1, T2) for (T1, _) in G._phases(2, 1, 3, 28) for (T2, _) in G._phases(2, 1, 3, 28)]
+            got = [(int(r["Tr"]), int(r["Ts"])) for r in rows if r["s"] == 2 and r["K"] == Kc and r["C"] == C]
+            assert got == want
+    ends = sorted((v[1], v[1] + (int(np.prod(v[2])) if v[0] == "crsk" else v[2])) for v in wp._views.values())
+    for (a0, a1), (b0, b1) in zip(ends, ends[1:]):
+        assert a1 <= b0
+    assert ends[-1][1] == wp.buf.numel()
