@@ -30,6 +30,8 @@
 //             at BERT-Large's S = 512 (occupancy: see ttdk_attn_set_fused_bwd).
 #include "tile_common.h"
 
+#include <type_traits>
+
 namespace ttdk {
 namespace {
 
@@ -163,7 +165,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       }
     }
     const int kbase = kt * KT;
-    const bool full = kbase + KT <= len;
+    if (kbase + KT > len) {
+      // (block-uniform: only the last key tile of a padded sequence; the full tiles run no
+      // per-element compare / select — the kernel is VALU-bound, profiles/r3_bert_*_pmc_*)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (kbase + kb * 16 + 4 * g + i >= len) s[qb][kb][i] = -INFINITY;
+    }
     bf16x8_t pf[2][2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
@@ -172,10 +184,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (!full && kbase + kb * 16 + 4 * g + i >= len) s[qb][kb][i] = -INFINITY;
-          mx = fmaxf(mx, s[qb][kb][i]);
-        }
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[qb][kb][i]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m[qb], mx * P.scale_log2);
@@ -341,7 +350,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
             hk[qb][i][1] = odd ? mine : other;
           }
       }
-      // P, dS (in place: sc <- P*keep*scale, dp <- dS)
+      // P, dS (in place: sc <- P*keep*scale, dp <- dS). (Specialising the loop on the wave's key
+      // mask, as bwd_q and fwd do, made this kernel spill 63 VGPRs.)
 #pragma unroll
       for (int qb = 0; qb < 4; ++qb)
 #pragma unroll
@@ -489,6 +499,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
     }
     const int kbase = kt * KT;
     bf16x8_t sfr[2][2];
+    // key mask only on a tile that reaches past len (block-uniform)
+    auto pds = [&](auto maskc) {
+      constexpr bool MASK = decltype(maskc)::value;
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const int qrow = q0 + qb * 16 + i16;
@@ -505,7 +518,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int kcol = kbase + kb * 16 + 4 * g + i;
-          const float p = kcol < len ? fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2[qb]) : 0.f;
+          float p = fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2[qb]);
+          if constexpr (MASK) p = kcol < len ? p : 0.f;
           float dpv = dp[qb][kb][i];
           if constexpr (DROP) dpv = attn_keep(hp[i >> 1], static_cast<uint32_t>(i), P.drop_thr) ? dpv * P.drop_scale : 0.f;
           sc[qb][kb][i] = p * (dpv - del[qb]);
@@ -514,6 +528,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
       sfr[qb][0] = pack_frag(sc[qb][0], sc[qb][1]);
       sfr[qb][1] = pack_frag(sc[qb][2], sc[qb][3]);
     }
+    };
+    if (kbase + KT <= len) pds(std::false_type{});
+    else pds(std::true_type{});
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
