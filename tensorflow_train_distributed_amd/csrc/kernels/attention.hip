@@ -88,6 +88,11 @@ struct TileLoader {
     c = tid & 7;
   }
   __device__ __forceinline__ void load(int row0, int nrows) {
+    if (row0 + 64 <= nrows) {  // block-uniform: whole tile in range, no per-dword selects
+#pragma unroll
+      for (int j = 0; j < 2; ++j) v[j] = ldg16(base + static_cast<long long>(row0 + r + 32 * j) * ld + c * 8);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int row = row0 + r + 32 * j;
@@ -364,11 +369,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
             float p = kcol < len ? fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2) : 0.f;
             float dpv = dp[qb][kb][i];
             float pd = p;
-            if constexpr (DROP) {
+            if constexpr (DROP) {  // one select for both: keep factor 1/(1-p) or 0
               const uint32_t h = hk[qb][i][kb];
-              const bool kp = attn_keep(h, static_cast<uint32_t>(kcol), P.drop_thr);
-              pd = kp ? p * P.drop_scale : 0.f;
-              dpv = kp ? dpv * P.drop_scale : 0.f;
+              const float kf = attn_keep(h, static_cast<uint32_t>(kcol), P.drop_thr) ? P.drop_scale : 0.f;
+              pd = p * kf;
+              dpv = dpv * kf;
             }
             sc[qb][kb][i] = pd;
             dp[qb][kb][i] = p * (dpv - del);
