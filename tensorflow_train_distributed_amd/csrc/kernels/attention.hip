@@ -76,27 +76,31 @@ __device__ __forceinline__ bf16x8_t ldg_frag(const bf16_t* p) {
 }
 
 // 64 rows x 64 cols tile loader: thread t moves rows (t >> 3) and (t >> 3) + 32, chunk t & 7.
+// The lane's row / chunk offset is folded into its pointer once; per tile only the block-uniform
+// row0 * ld is formed (scalar), not a 64-bit vector multiply per row (v_mul_lo_u32 is a
+// quarter-rate instruction in these VALU-bound loops).
 struct TileLoader {
-  const bf16_t* base;
+  const bf16_t* lanep;
   long long ld;
   int r, c;
   uint4 v[2];
   __device__ __forceinline__ void init(const bf16_t* b, long long l, int tid) {
-    base = b;
     ld = l;
     r = tid >> 3;
     c = tid & 7;
+    lanep = b + static_cast<long long>(r) * l + c * 8;
   }
   __device__ __forceinline__ void load(int row0, int nrows) {
+    const bf16_t* p = lanep + static_cast<long long>(row0) * ld;
     if (row0 + 64 <= nrows) {  // block-uniform: whole tile in range, no per-dword selects
 #pragma unroll
-      for (int j = 0; j < 2; ++j) v[j] = ldg16(base + static_cast<long long>(row0 + r + 32 * j) * ld + c * 8);
+      for (int j = 0; j < 2; ++j) v[j] = ldg16(p + 32 * j * ld);
       return;
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int row = row0 + r + 32 * j;
-      v[j] = row < nrows ? ldg16(base + static_cast<long long>(row) * ld + c * 8) : make_uint4(0, 0, 0, 0);
+      v[j] = row < nrows ? ldg16(p + 32 * j * ld) : make_uint4(0, 0, 0, 0);
     }
   }
   __device__ __forceinline__ void store(char* lds) const {
@@ -108,6 +112,8 @@ struct TileLoader {
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // ------------------------------------------------------------------------------ forward
+// (launch_bounds(256, 4) — 128 VGPRs, 4 waves / SIMD instead of 3, 10-12 spilled — measured
+// 10-18 % slower at BERT-Large b128: the spills land in the loop)
 template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
@@ -190,8 +196,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[qb][kb][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = tile::rows4_max(mx);
       const float mnew = fmaxf(m[qb], mx * P.scale_log2);
       const float msub = mnew == -INFINITY ? 0.f : mnew;
       const float alpha = fast_exp2(m[qb] - msub);
@@ -218,8 +223,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
           s[qb][kb][i] = pd;
         }
       }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = tile::rows4_sum(rs);
       l[qb] = l[qb] * alpha + rs;
 #pragma unroll
       for (int db = 0; db < 4; ++db) o[qb][db] *= alpha;
@@ -350,7 +354,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
             const int ql = qb * 16 + 4 * g + i;
             const uint32_t mine =
                 attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * P.S + qt * KT + ql)), pair);
-            const uint32_t other = __shfl_xor(mine, 1, 64);
+            // lane ^ 1 on the VALU (DPP quad_perm [1,0,3,2]), not an LDS bpermute round trip
+            const uint32_t other = __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);
             hk[qb][i][0] = odd ? other : mine;
             hk[qb][i][1] = odd ? mine : other;
           }
@@ -455,8 +460,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
       for (int j = 0; j < 8; ++j) acc += a[j] * d[j];
     }
     // the 4 lane groups g hold the row's 4 slices
-    acc += __shfl_xor(acc, 16, 64);
-    acc += __shfl_xor(acc, 32, 64);
+    acc = tile::rows4_sum(acc);
     del[qb] = acc;
     const long long srow = static_cast<long long>(bh) * P.S + q0 + qb * 16 + i16;
     lse2[qb] = P.lse[srow];
@@ -702,7 +706,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P
           if constexpr (DROP) {
             const int qg = s * QS + qb * 16 + 4 * g + i;
             const uint32_t mine = attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * SK + qg)), pair);
-            const uint32_t other = __shfl_xor(mine, 1, 64);
+            // lane ^ 1 on the VALU (DPP quad_perm [1,0,3,2]), not an LDS bpermute round trip
+            const uint32_t other = __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);
             hk[0] = odd ? other : mine;
             hk[1] = odd ? mine : other;
           }

@@ -49,6 +49,22 @@ __device__ __forceinline__ bf16x8_t pack_frag(const f32x4_t& a, const f32x4_t& b
   return __builtin_bit_cast(bf16x8_t, w);
 }
 
+// Max / sum over the four lanes {l, l^16, l^32, l^48} (one MFMA result row spread over the 4 lane
+// groups) on the VALU with the gfx950 permlane swaps instead of two ds_bpermute round trips
+// through LDS (each followed by an lgkmcnt(0) wait in the softmax's serial chain).
+__device__ __forceinline__ float rows4_max(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rows4_sum(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // Bijective blockIdx -> work-item map that keeps consecutive work items on one XCD
 // (hardware dispatches blockIdx round-robin over the 8 XCDs).
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
