@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
       }
       if (relu) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+        for (int j = 0; j < 8; ++j) f[j] = ttdk::relu(f[j]);
       }
       const uint4 packed = pack8(f);
       reinterpret_cast<uint4*>(out)[i] = packed;

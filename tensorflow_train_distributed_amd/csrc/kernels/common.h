@@ -40,6 +40,11 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
+// ReLU as ONE v_maximum3_f32 (gfx950; NaN-propagating like torch.relu / tf.nn.relu). fmaxf(x, 0)
+// on a value the compiler cannot prove canonical (a bf16 load, an MFMA accumulator) costs a
+// canonicalising v_max_f32 x, x, x first: two VALU per element in the GEMM / BN epilogues.
+__device__ __forceinline__ float relu(float x) { return __builtin_elementwise_maximum(x, 0.f); }
+
 __device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(THR, 1) void conv3_kernel(Pro pa, const bf16_t* __r
         float f[8];
         unpack8(ra[i], f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * k0[j] + k1[j], 0.f);
+        for (int j = 0; j < 8; ++j) f[j] = relu(f[j] * k0[j] + k1[j]);
         v = ok ? pack8(f) : make_uint4(0, 0, 0, 0);
         if (write_side && interior) {
           *reinterpret_cast<uint4*>(pa.side + off) = v;

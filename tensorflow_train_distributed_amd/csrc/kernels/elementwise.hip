@@ -117,7 +117,7 @@ enum Act : int { kNone = 0, kRelu = 1, kGelu = 2, kElu = 3 };
 
 __device__ __forceinline__ float act_fwd(float x, int act) {
   switch (act) {
-    case kRelu: return fmaxf(x, 0.f);
+    case kRelu: return relu(x);
     case kGelu: return 0.5f * x * (1.f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
     case kElu: return x > 0.f ? x : expm1f(x);
     default: return x;

@@ -685,7 +685,7 @@ __device__ __forceinline__ void epi_rows(const EpiParams& E, const char* smem, i
       }
       if (E.act == kActRelu) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+        for (int j = 0; j < 8; ++j) f[j] = relu(f[j]);
       } else if (E.act == kActGelu) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = gelu_tanh(f[j]);
@@ -1631,7 +1631,7 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
               for (int j = 0; j < 8; ++j) gv[j] += yf[j];
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gv[j] = fmaxf(gv[j], 0.f);
+            for (int j = 0; j < 8; ++j) gv[j] = relu(gv[j]);
           }
           const uint4 o = pack8(gv);
           *q = o;

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const bf16_t* __re
         float f[8];
         unpack8(v[r][s], f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * sc[j] + sh[j], 0.f);
+        for (int j = 0; j < 8; ++j) f[j] = relu(f[j] * sc[j] + sh[j]);
         const uint4 pk = pack8(f);  // the bf16 activation the unfused path would have stored
         float o[8];
         unpack8(pk, o);

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
         }
         if (pa.relu) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+          for (int j = 0; j < 8; ++j) f[j] = relu(f[j]);
         }
         v = ok ? pack8(f) : make_uint4(0, 0, 0, 0);
         if (write_side && ok) {
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(THR, 1) void pw_kernel(Pro pa, const bf16_t* __rest
         }
         if (E.act == kActRelu) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+          for (int j = 0; j < 8; ++j) f[j] = relu(f[j]);
         }
         if (E.by) {
           const uint32_t mb = E.bmask ? static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(sDm + r * (BN / 8) + c))
