@@ -343,9 +343,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
       // dropout hashes: lanes i16 and i16 ^ 1 hold keys 2j and 2j + 1 (one pair, one hash) of
       // the same query rows, for kb = 0 and kb = 1: the even lane hashes the kb = 0 pairs, the
       // odd lane the kb = 1 pairs, and they swap (16 hashes per lane instead of 32)
-      uint32_t hk[4][4][2];
+      uint32_t hk[4][4][2];  // the 16-bit hash half of (query row, key kb) in the low bits
       if constexpr (DROP) {
         const bool odd = (i16 & 1) != 0;
+        // v_perm_b32 selectors (bytes of {other, mine}; 0x0c = zero byte): key parity = lane
+        // parity, so the even lane takes low halves, the odd lane high halves — one perm per
+        // element instead of a swap select, a shift / mask and a half select
+        const uint32_t sel0 = odd ? 0x0c0c0706u : 0x0c0c0100u, sel1 = odd ? 0x0c0c0302u : 0x0c0c0504u;
         const uint32_t pair = static_cast<uint32_t>(k0 + (odd ? 16 : 0) + i16) >> 1;
 #pragma unroll
         for (int qb = 0; qb < 4; ++qb)
@@ -356,8 +360,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
                 attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * P.S + qt * KT + ql)), pair);
             // lane ^ 1 on the VALU (DPP quad_perm [1,0,3,2]), not an LDS bpermute round trip
             const uint32_t other = __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);
-            hk[qb][i][0] = odd ? other : mine;
-            hk[qb][i][1] = odd ? mine : other;
+            hk[qb][i][0] = __builtin_amdgcn_perm(other, mine, sel0);
+            hk[qb][i][1] = __builtin_amdgcn_perm(other, mine, sel1);
           }
       }
       // P, dS (in place: sc <- P*keep*scale, dp <- dS). (Specialising the loop on the wave's key
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
             float pd = p;
             if constexpr (DROP) {  // one select for both: keep factor 1/(1-p) or 0
               const uint32_t h = hk[qb][i][kb];
-              const float kf = attn_keep(h, static_cast<uint32_t>(kcol), P.drop_thr) ? P.drop_scale : 0.f;
+              const float kf = h >= P.drop_thr ? P.drop_scale : 0.f;
               pd = p * kf;
               dpv = dpv * kf;
             }
@@ -694,6 +698,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P
       // two keys of one pair for j = 0 and j = 1; the even lane hashes the j = 0 pair, the odd
       // lane the j = 1 pair, and they swap (one hash per lane per (query, pair of tiles))
       const bool odd = (i16 & 1) != 0;
+      const uint32_t sel0 = odd ? 0x0c0c0706u : 0x0c0c0100u, sel1 = odd ? 0x0c0c0302u : 0x0c0c0504u;
       const uint32_t pair = static_cast<uint32_t>(k0 + (odd ? 16 : 0) + i16) >> 1;
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
@@ -708,8 +713,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P
             const uint32_t mine = attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * SK + qg)), pair);
             // lane ^ 1 on the VALU (DPP quad_perm [1,0,3,2]), not an LDS bpermute round trip
             const uint32_t other = __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);
-            hk[0] = odd ? other : mine;
-            hk[1] = odd ? mine : other;
+            hk[0] = __builtin_amdgcn_perm(other, mine, sel0);  // 16-bit halves, as in bwd_kv
+            hk[1] = __builtin_amdgcn_perm(other, mine, sel1);
           }
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
@@ -718,7 +723,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P
             float dpv = dp[qb][j][i];
             float pd = p;
             if constexpr (DROP) {
-              const bool kp = attn_keep(hk[j], static_cast<uint32_t>(kcol), P.drop_thr);
+              const bool kp = hk[j] >= P.drop_thr;
               pd = kp ? p * P.drop_scale : 0.f;
               dpv = kp ? dpv * P.drop_scale : 0.f;
             }
