@@ -54,9 +54,9 @@ __device__ __forceinline__ bf16x8_t pack_frag(const f32x4_t& a, const f32x4_t& b
 // through LDS (each followed by an lgkmcnt(0) wait in the softmax's serial chain).
 __device__ __forceinline__ float rows4_max(float x) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  x = __builtin_elementwise_maximum(__uint_as_float(a[0]), __uint_as_float(a[1]));  // no canonicalising max
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+  return __builtin_elementwise_maximum(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 __device__ __forceinline__ float rows4_sum(float x) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
