@@ -53,7 +53,10 @@ def build_resnet(args, dev, rank, world):
     else:
         opt = FlatSGD(model.params, Schedule(kind=2, base_lr=0.1 * B * world / 256, warmup_steps=5, end_lr=0.0,
                                              power=2.0, total_steps=10000), momentum=0.9, weight_decay=5e-5)
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
+    # the collectives hide under the backward: ~44 ms at 1024 images on one MI355X,
+    # the CTA-budget probe of the native engine weighs the gradient bytes against it
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16,
+                                 overlap_ms=44.0 * B / 1024 * (args.image_size / 224) ** 2)
     g = torch.Generator(device=dev)
     g.manual_seed(rank)
     S = args.image_size
@@ -100,7 +103,9 @@ def build_bert(args, dev, rank, world):
     broadcast_flat_(model.params)
     opt = FlatLAMB(model.params, Schedule(kind=2, base_lr=4e-3, warmup_steps=100, end_lr=0.0, power=1.0,
                                           total_steps=10000), weight_decay=0.01, max_grad_norm=1.0)
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
+    # backward ~120 ms at 128 sequences of 512
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16,
+                                 overlap_ms=120.0 * B / 128 * S / 512)
     batch = synthetic_batch(cfg, B, S, max_predictions=80 if S >= 512 else 20, device=dev, seed=rank)
 
     def step():
@@ -290,12 +295,12 @@ def main():
     graph_info = None
     if use_graph:
         from tensorflow_train_distributed_amd.utils import graphs
-        mode = os.environ.get("TTD_GRAPH_MODE", "segmented" if world == 1 else "single")
+        mode = os.environ.get("TTD_GRAPH_MODE", "segmented")
         if mode == "segmented":
             # per-stream linear graph segments replayed on the eager step's own streams (main
-            # high priority, weight gradients normal priority); cross-stream edges are event nodes
-            # (utils/graphs.py). The native RCCL engine's comm stream forks and joins inside its own
-            # library, so N>1 captures the step as one graph instead.
+            # high priority, weight gradients normal priority, the native RCCL engine's
+            # communicator stream); cross-stream edges — bucket forks and the final join
+            # included — are event nodes (utils/graphs.py, parallel/collective.py)
             main_s = prio if prio is not None else torch.cuda.Stream(device=dev)
             graph = graphs.capture_segmented(step, main=main_s, warmup=2)
             out = graph.outputs
@@ -307,6 +312,16 @@ def main():
             graph, out = graphs.capture(step, stream=prio)
             graph_info = {"mode": "single"}
         run = graph.replay
+        comm0 = getattr(red0, "comm", None)
+        if comm0 is not None:
+            # a captured join arms no watchdog marker: arm it after every replay, so a replayed
+            # step whose collectives never finish still trips the no-progress deadline
+            replay = run
+
+            def run():
+                out_ = replay()
+                comm0.arm()
+                return out_
     else:
         run = step
     if prio is not None:
@@ -339,10 +354,16 @@ def main():
     elapsed = max(per_rank)
     red = getattr(step, "reducer", None)
     comm_stats = None
-    if graph is None and red is not None and world > 1 and red.time_next_step():
-        # one extra (untimed) step with the collectives instrumented: busy time on the
+    if red is not None and world > 1 and red.time_next_step():
+        # one extra (untimed, eager) step with the collectives instrumented: busy time on the
         # communicator stream and the part of it the backward did not hide
-        run()
+        if graph is None:
+            run()
+        elif prio is not None:
+            with torch.cuda.stream(prio):
+                step()
+        else:
+            step()
         sync()
         comm_stats = red.comm_stats()
     sums = step() if graph is None else out
@@ -411,6 +432,11 @@ def main():
                 dinfo["native_engine_unavailable"] = rccl.failure_reason() or os.environ.get("TTD_COLLECTIVE")
         if probe is not None:
             dinfo["allreduce_probe"] = probe
+        pol = red.policy() if red is not None and world > 1 else None
+        if pol is not None:
+            dinfo["cta_budget"] = pol.get("cta_budget")
+            dinfo["cta_policy"] = {k: pol.get(k) for k in ("reason", "overlap_ms", "projected_ms", "first_bucket_mb",
+                                                         "probe")}
         if comm_stats is not None:
             dinfo["comm_per_step"] = comm_stats
         if backend == "nccl" and world > 1:

@@ -112,8 +112,14 @@ ncclRedOp_t to_op(int op) {
 
 thread_local std::string g_err;
 
+long long now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 struct Engine {
-  ncclComm_t comm = nullptr;
+  // written only under `wmu` (abort swaps it to null before ncclCommAbort), read lock-free
+  std::atomic<ncclComm_t> comm{nullptr};
   hipStream_t cs = nullptr;  // communicator stream
   int rank = 0, nranks = 1, device = 0;
   double timeout = 300.0;
@@ -129,13 +135,23 @@ struct Engine {
   bool timing = false;
   std::vector<hipEvent_t> t_begin, t_end;
   int n_timed = 0;
-  // ---- watchdog: every join (outside stream capture) records a marker event on the
-  // communicator stream; a thread polls the oldest marker and the communicator's asynchronous
-  // error. A marker older than `timeout` (a peer that died mid-step leaves RCCL's kernels
-  // spinning and the compute stream waiting on the join) or an asynchronous error aborts the
-  // communicator: RCCL's kernels exit, the streams drain, and the next bucket / join call
-  // returns an error the recoverable session acts on (parallel/strategy.py recover()).
-  std::mutex mu;            // guards comm calls vs. the watchdog's abort, `pend`, `pool`
+  // ---- watchdog: every join (outside stream capture) and every ttdc_arm (after a graph replay)
+  // records a marker event on the communicator stream; a thread polls the oldest marker and
+  // the communicator's asynchronous error. A marker older than `timeout` (a peer that died
+  // mid-step leaves RCCL's kernels spinning and the compute stream waiting on the join), an
+  // asynchronous error, or a host call blocked inside RCCL for longer than `timeout` (a dead
+  // peer during RCCL's lazy connection setup) aborts the communicator: RCCL's kernels exit, the
+  // streams drain, and the next bucket / join call returns an error the recoverable session
+  // acts on (parallel/strategy.py recover()).
+  // Locks: `mu` serialises the host threads' calls into RCCL and is held across them (a
+  // blocking enqueue can block); the watchdog never waits for it. It takes `mu` only with
+  // try_lock (nobody is between loading `comm` and calling RCCL: aborting is safe), and once a
+  // call has held `mu` for longer than `timeout` it aborts without it (that caller is stuck
+  // inside RCCL, which ncclCommAbort from another thread releases). `wmu` guards the watchdog's
+  // own state (`pend`, `pool`, `stop`) and the comm swap.
+  std::mutex mu;
+  std::mutex wmu;
+  std::atomic<long long> busy_ns{0};  // steady-clock start of the call holding `mu` (0 = none)
   std::condition_variable cv;
   bool stop = false;
   std::thread wd;
@@ -145,7 +161,16 @@ struct Engine {
   };
   std::deque<Mark> pend;
   std::vector<hipEvent_t> pool;
+  std::vector<void*> retired;  // outgrown staging buffers, freed once the stream drained
   std::atomic<int> aborts{0};
+};
+
+// A host call into the engine: holds `mu` and publishes how long it has been inside.
+struct Call {
+  Engine* e;
+  std::lock_guard<std::mutex> lk;
+  explicit Call(Engine* en) : e(en), lk(en->mu) { e->busy_ns = now_ns(); }
+  ~Call() { e->busy_ns = 0; }
 };
 bool set_err(Engine* e, const std::string& m) {
   if (e) {
@@ -161,7 +186,9 @@ bool settle(Engine* e, ncclResult_t r, const char* what) {
   const auto t0 = std::chrono::steady_clock::now();
   while (r == ncclInProgress) {
     ncclResult_t a = ncclSuccess;
-    const ncclResult_t q = ncclCommGetAsyncError(e->comm, &a);
+    ncclComm_t c = e->comm.load();
+    if (!c) return set_err(e, std::string(what) + ": communicator aborted");
+    const ncclResult_t q = ncclCommGetAsyncError(c, &a);
     if (q != ncclSuccess) { r = q; break; }
     r = a;
     if (r != ncclInProgress) break;
@@ -174,7 +201,8 @@ bool settle(Engine* e, ncclResult_t r, const char* what) {
     std::this_thread::sleep_for(std::chrono::microseconds(dt < 0.01 ? 5 : 500));
   }
   if (r != ncclSuccess) {
-    const char* last = e->comm ? ncclGetLastError(e->comm) : "";
+    ncclComm_t c = e->comm.load();
+    const char* last = c ? ncclGetLastError(c) : "";
     return set_err(e, std::string(what) + ": " + ncclGetErrorString(r) + (last && *last ? std::string(" (") + last + ")" : ""));
   }
   return true;
@@ -199,6 +227,8 @@ bool reduce_on(Engine* e, void* buf, size_t count, ncclDataType_t dt, size_t esz
   const int n = ttd_coll::plan(algo, static_cast<long long>(count), e->nranks, e->rank, plan);
   if (n < 0) return set_err(e, "collective plan: bad argument");
   char* p = static_cast<char*>(buf);
+  ncclComm_t comm = e->comm.load();
+  if (!comm) return set_err(e, "communicator aborted");
   for (int i = 0; i < n; ++i) {
     const ttd_coll::Step& st = plan[i];
     char* a = p + st.send * esz;
@@ -206,13 +236,13 @@ bool reduce_on(Engine* e, void* buf, size_t count, ncclDataType_t dt, size_t esz
     const size_t c = static_cast<size_t>(st.count);
     bool ok = true;
     switch (st.kind) {
-      case ttd_coll::kAllReduce: ok = settle(e, ncclAllReduce(a, a, c, dt, op, e->comm, s), "ncclAllReduce"); break;
+      case ttd_coll::kAllReduce: ok = settle(e, ncclAllReduce(a, a, c, dt, op, comm, s), "ncclAllReduce"); break;
       case ttd_coll::kReduceScatter:
-        ok = settle(e, ncclReduceScatter(a, b, c, dt, op, e->comm, s), "ncclReduceScatter");
+        ok = settle(e, ncclReduceScatter(a, b, c, dt, op, comm, s), "ncclReduceScatter");
         break;
-      case ttd_coll::kAllGather: ok = settle(e, ncclAllGather(a, b, c, dt, e->comm, s), "ncclAllGather"); break;
-      case ttd_coll::kReduce: ok = settle(e, ncclReduce(a, a, c, dt, op, st.root, e->comm, s), "ncclReduce"); break;
-      case ttd_coll::kBroadcast: ok = settle(e, ncclBroadcast(a, a, c, dt, st.root, e->comm, s), "ncclBroadcast"); break;
+      case ttd_coll::kAllGather: ok = settle(e, ncclAllGather(a, b, c, dt, comm, s), "ncclAllGather"); break;
+      case ttd_coll::kReduce: ok = settle(e, ncclReduce(a, a, c, dt, op, st.root, comm, s), "ncclReduce"); break;
+      case ttd_coll::kBroadcast: ok = settle(e, ncclBroadcast(a, a, c, dt, st.root, comm, s), "ncclBroadcast"); break;
       default: ok = set_err(e, "collective plan: unknown step");
     }
     if (!ok) return false;
@@ -225,46 +255,66 @@ bool capturing(hipStream_t s) {
   return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
-// Abort the communicator. Caller holds `lk` on e->mu; the engine is marked failed and detached
-// from the communicator first, then the lock is released around ncclCommAbort (which can wait for
-// queued work): every other call sees the failure at once instead of blocking on the lock.
-void abort_locked(Engine* e, std::unique_lock<std::mutex>& lk, const std::string& why) {
-  if (!e->comm) return;
-  ncclComm_t c = e->comm;
-  e->comm = nullptr;
-  set_err(e, why);
-  e->aborts.fetch_add(1);
-  lk.unlock();
+// Abort the communicator: detach it (every later call sees the failure at once), then
+// ncclCommAbort outside every lock (it can wait for queued work). Exactly one caller wins.
+void abort_comm(Engine* e, const std::string& why) {
+  ncclComm_t c;
+  {
+    std::lock_guard<std::mutex> g(e->wmu);
+    c = e->comm.exchange(nullptr);
+    if (!c) return;
+    set_err(e, why);
+    e->aborts.fetch_add(1);
+  }
   ncclCommAbort(c);
-  lk.lock();
+}
+
+// Why the communicator should be aborted now ("" = healthy). Caller holds wmu.
+std::string health(Engine* e) {
+  ncclComm_t c = e->comm.load();
+  if (!c) return "";
+  ncclResult_t a = ncclSuccess;
+  if (ncclCommGetAsyncError(c, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress)
+    return std::string("communicator failed: ") + ncclGetErrorString(a);
+  if (!e->pend.empty()) {
+    const double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - e->pend.front().t).count();
+    if (age > e->timeout) {
+      char b[160];
+      snprintf(b, sizeof b, "collectives made no progress for %.0f s (a peer died or hung): communicator aborted", age);
+      return b;
+    }
+  }
+  return "";
 }
 
 void watchdog(Engine* e) {
   hipSetDevice(e->device);
-  std::unique_lock<std::mutex> lk(e->mu);
+  std::unique_lock<std::mutex> wl(e->wmu);
   while (!e->stop) {
-    e->cv.wait_for(lk, std::chrono::milliseconds(e->pend.empty() ? 50 : 2));
+    e->cv.wait_for(wl, std::chrono::milliseconds(e->pend.empty() ? 50 : 2));
     if (e->stop) break;
     while (!e->pend.empty() && hipEventQuery(e->pend.front().ev) == hipSuccess) {
       e->pool.push_back(e->pend.front().ev);
       e->pend.pop_front();
     }
-    if (!e->comm) continue;
-    ncclResult_t a = ncclSuccess;
-    if (ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
-      abort_locked(e, lk, std::string("communicator failed: ") + ncclGetErrorString(a));
-      continue;
+    if (!e->comm.load()) continue;
+    std::string why = health(e);
+    const long long b = e->busy_ns.load();
+    const double busy = b ? (now_ns() - b) * 1e-9 : 0.0;
+    if (why.empty() && busy > e->timeout) {
+      char m[160];
+      snprintf(m, sizeof m, "a collective call blocked for %.0f s (a peer died or hung): communicator aborted", busy);
+      why = m;
     }
-    if (!e->pend.empty()) {
-      const double age =
-          std::chrono::duration<double>(std::chrono::steady_clock::now() - e->pend.front().t).count();
-      if (age > e->timeout) {
-        char b[160];
-        snprintf(b, sizeof b, "collectives made no progress for %.0f s (a peer died or hung): communicator aborted",
-                 age);
-        abort_locked(e, lk, b);
-      }
-    }
+    if (why.empty()) continue;
+    wl.unlock();
+    if (busy > e->timeout) {
+      abort_comm(e, why);  // the caller holding `mu` is stuck inside RCCL
+    } else if (e->mu.try_lock()) {
+      abort_comm(e, why);  // no call in flight
+      e->mu.unlock();
+    }  // else: a call is in flight; retry on the next tick (bounded by the busy deadline)
+    wl.lock();
   }
 }
 
@@ -320,10 +370,12 @@ TTDK_EXPORT void* ttdc_create(const char* id_bytes, int nranks, int rank, int de
   if (min_ctas > 0) cfg.minCTAs = min_ctas;
   if (max_ctas > 0) cfg.maxCTAs = max_ctas;
   cfg.commName = "ttd_grad";
-  const ncclResult_t r = ncclCommInitRankConfig(&e->comm, nranks, id, rank, &cfg);
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+  e->comm = c;
   if (!settle(e, r, "ncclCommInitRankConfig")) {
     g_err = e->err;
-    if (e->comm) ncclCommAbort(e->comm);
+    if (c) ncclCommAbort(c);
     for (int i = 0; i < 64; ++i) hipEventDestroy(e->fork[i]);
     hipEventDestroy(e->join);
     hipStreamDestroy(e->cs);
@@ -340,9 +392,9 @@ namespace ttdk {
 namespace {
 bool grow_stage(Engine* e, size_t need) {
   if (need <= e->stage_bytes) return true;
-  // the old staging buffer may still be read by queued work
-  if (!hip_ok(e, hipStreamSynchronize(e->cs), "hipStreamSynchronize")) return false;
-  if (e->stage) hipFree(e->stage);
+  // the old staging buffer may still be read by queued work: retire it (freed once the stream
+  // drained, ttdc_synchronize / ttdc_destroy) instead of synchronising under `mu`
+  if (e->stage) e->retired.push_back(e->stage);
   e->stage = nullptr;
   e->stage_bytes = 0;
   if (!hip_ok(e, hipMalloc(&e->stage, need), "hipMalloc")) return false;
@@ -418,7 +470,7 @@ TTDK_EXPORT int ttdc_emulate_bucket(hipStream_t stream, int ctas, double us, voi
 // elements (call once before any step is captured).
 TTDK_EXPORT int ttdc_reserve(void* h, long long count) {
   Engine* e = static_cast<Engine*>(h);
-  std::lock_guard<std::mutex> lk(e->mu);
+  Call call(e);
   if (e->failed) return -1;
   return grow_stage(e, static_cast<size_t>(count) * 2) ? 0 : -1;
 }
@@ -426,13 +478,14 @@ TTDK_EXPORT int ttdc_reserve(void* h, long long count) {
 // Bucket launch: the communicator stream waits for the work already queued on `producer`,
 // then reduces buf[0:count) in place. compress (fp32 buffers only): cast to bf16 on the
 // communicator stream, reduce in bf16, cast back.
-TTDK_EXPORT int ttdc_bucket(void* h, void* buf, long long count, int dtype, int op, int algo, int compress,
-                            hipStream_t producer) {
-  Engine* e = static_cast<Engine*>(h);
-  std::lock_guard<std::mutex> lk(e->mu);
-  if (e->failed || !e->comm) return -1;
+namespace ttdk {
+namespace {
+int bucket_launch(Engine* e, void* buf, long long count, int dtype, int op, int algo, int compress, bool fork,
+                  hipStream_t producer) {
+  Call call(e);
+  if (e->failed || !e->comm.load()) return -1;
   if (count < 0 || algo < 0 || algo > 2) return set_err(e, "ttdc_bucket: bad argument"), -1;
-  if (!fork_from(e, producer)) return -1;
+  if (fork && !fork_from(e, producer)) return -1;
   if (e->timing) {
     if (e->n_timed == static_cast<int>(e->t_begin.size())) {
       hipEvent_t a, b;
@@ -445,6 +498,19 @@ TTDK_EXPORT int ttdc_bucket(void* h, void* buf, long long count, int dtype, int 
   const int rc = bucket_body(e, buf, count, dtype, op, algo, compress);
   if (e->timing && rc == 0) hipEventRecord(e->t_end[e->n_timed++], e->cs);
   return rc;
+}
+}  // namespace
+}  // namespace ttdk
+
+TTDK_EXPORT int ttdc_bucket(void* h, void* buf, long long count, int dtype, int op, int algo, int compress,
+                            hipStream_t producer) {
+  return bucket_launch(static_cast<Engine*>(h), buf, count, dtype, op, algo, compress, true, producer);
+}
+
+// ttdc_bucket without the fork: the caller already ordered the communicator stream (an event
+// node pair of a segmented hipGraph capture, utils/graphs.py).
+TTDK_EXPORT int ttdc_bucket_nofork(void* h, void* buf, long long count, int dtype, int op, int algo, int compress) {
+  return bucket_launch(static_cast<Engine*>(h), buf, count, dtype, op, algo, compress, false, nullptr);
 }
 
 // Timing mode on (resets the bucket count) or off.
@@ -473,31 +539,51 @@ TTDK_EXPORT int ttdc_timing(void* h, float* busy_ms, float* span_ms) {
 // failure the watchdog detected (asynchronous communicator error, or no progress before the
 // deadline) as an error, and arms the watchdog with a marker after the queued collectives
 // (not under stream capture: a captured record never completes on its own).
+namespace ttdk {
+namespace {
+// Arm the watchdog: a pooled marker event recorded on `s` after the work queued so far.
+void arm(Engine* e, hipStream_t s) {
+  std::lock_guard<std::mutex> g(e->wmu);
+  hipEvent_t ev = nullptr;
+  if (!e->pool.empty()) {
+    ev = e->pool.back();
+    e->pool.pop_back();
+  } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    return;
+  }
+  if (hipEventRecord(ev, s) == hipSuccess) {
+    e->pend.push_back(Engine::Mark{ev, std::chrono::steady_clock::now()});
+    e->cv.notify_one();
+  } else {
+    e->pool.push_back(ev);
+  }
+}
+}  // namespace
+}  // namespace ttdk
+
 TTDK_EXPORT int ttdc_join(void* h, hipStream_t consumer) {
   Engine* e = static_cast<Engine*>(h);
-  std::lock_guard<std::mutex> lk(e->mu);
-  if (e->failed || !e->comm) return -1;
+  Call call(e);
+  ncclComm_t c = e->comm.load();
+  if (e->failed || !c) return -1;
   ncclResult_t a = ncclSuccess;
-  if (ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress)
+  if (ncclCommGetAsyncError(c, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress)
     return set_err(e, std::string("communicator failed: ") + ncclGetErrorString(a)), -1;
   if (!hip_ok(e, hipEventRecord(e->join, e->cs), "hipEventRecord") ||
       !hip_ok(e, hipStreamWaitEvent(consumer, e->join, 0), "hipStreamWaitEvent"))
     return -1;
-  if (!capturing(e->cs) && !capturing(consumer)) {
-    hipEvent_t ev = nullptr;
-    if (!e->pool.empty()) {
-      ev = e->pool.back();
-      e->pool.pop_back();
-    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-      ev = nullptr;
-    }
-    if (ev && hipEventRecord(ev, e->cs) == hipSuccess) {
-      e->pend.push_back(Engine::Mark{ev, std::chrono::steady_clock::now()});
-      e->cv.notify_one();
-    } else if (ev) {
-      e->pool.push_back(ev);
-    }
-  }
+  if (!capturing(e->cs) && !capturing(consumer)) arm(e, e->cs);
+  return 0;
+}
+
+// Arm the watchdog after a hipGraph replay: a captured join records no marker (a captured
+// record never completes on its own), so the replaying thread calls this with the replay stream
+// once per replay and a step whose collectives never finish still trips the deadline.
+TTDK_EXPORT int ttdc_arm(void* h, hipStream_t s) {
+  Engine* e = static_cast<Engine*>(h);
+  if (e->failed || !e->comm.load()) return -1;
+  if (capturing(s)) return set_err(e, "ttdc_arm: stream is capturing"), -1;
+  arm(e, s);
   return 0;
 }
 
@@ -506,11 +592,12 @@ TTDK_EXPORT int ttdc_join(void* h, hipStream_t consumer) {
 TTDK_EXPORT int ttdc_collective(void* h, int kind, void* buf, long long count, int dtype, int op, int root,
                                 hipStream_t s) {
   Engine* e = static_cast<Engine*>(h);
-  std::lock_guard<std::mutex> lk(e->mu);
-  if (e->failed || !e->comm) return -1;
+  Call call(e);
+  ncclComm_t c = e->comm.load();
+  if (e->failed || !c) return -1;
   if (count <= 0) return 0;
   if (kind == 1)
-    return settle(e, ncclBroadcast(buf, buf, count, to_nccl(dtype), root, e->comm, s), "ncclBroadcast") ? 0 : -1;
+    return settle(e, ncclBroadcast(buf, buf, count, to_nccl(dtype), root, c, s), "ncclBroadcast") ? 0 : -1;
   return reduce_on(e, buf, count, to_nccl(dtype), dt_size(dtype), to_op(op), 0, s) ? 0 : -1;
 }
 
@@ -518,28 +605,39 @@ TTDK_EXPORT int ttdc_collective(void* h, int kind, void* buf, long long count, i
 // against the engine's deadline (a hung peer becomes an error instead of a hang).
 TTDK_EXPORT int ttdc_synchronize(void* h) {
   Engine* e = static_cast<Engine*>(h);
+  hipEvent_t done = nullptr;
+  std::vector<void*> retired;
   {
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (e->failed || !e->comm) return -1;
+    Call call(e);
+    if (e->failed || !e->comm.load()) return -1;
     if (!hip_ok(e, hipEventRecord(e->join, e->cs), "hipEventRecord")) return -1;
+    done = e->join;
+    retired.swap(e->retired);  // queued before this record: free once it completed
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    const hipError_t q = hipEventQuery(e->join);
-    if (q == hipSuccess) return e->failed ? -1 : 0;
+    const hipError_t q = hipEventQuery(done);
+    if (q == hipSuccess) {
+      for (void* p : retired) hipFree(p);
+      return e->failed ? -1 : 0;
+    }
     if (q != hipErrorNotReady) return hip_ok(e, q, "hipEventQuery"), -1;
+    // no `mu` here: the watchdog and other threads' calls proceed while this host waits
+    if (e->failed) return -1;  // the watchdog aborted the communicator
+    ncclComm_t c = e->comm.load();
+    ncclResult_t a = ncclSuccess;
     {
-      std::unique_lock<std::mutex> lk(e->mu);
-      if (e->failed) return -1;  // the watchdog aborted the communicator
-      ncclResult_t a = ncclSuccess;
-      if (e->comm && ncclCommGetAsyncError(e->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
-        abort_locked(e, lk, std::string("communicator failed: ") + ncclGetErrorString(a));
-        return -1;
-      }
-      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > e->timeout) {
-        abort_locked(e, lk, "collectives did not complete before the deadline: communicator aborted");
-        return -1;
-      }
+      std::lock_guard<std::mutex> g(e->wmu);  // the comm cannot be swapped out under wmu
+      c = e->comm.load();
+      if (c && ncclCommGetAsyncError(c, &a) != ncclSuccess) a = ncclSuccess;
+    }
+    if (c && a != ncclSuccess && a != ncclInProgress) {
+      abort_comm(e, std::string("communicator failed: ") + ncclGetErrorString(a));
+      return -1;
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > e->timeout) {
+      abort_comm(e, "collectives did not complete before the deadline: communicator aborted");
+      return -1;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
@@ -556,7 +654,7 @@ TTDK_EXPORT int ttdc_debug_stall(void* h, const int* flag, int max_ms) {
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, e->device) != hipSuccess || rate_khz <= 0)
     rate_khz = 100000;
   const unsigned long long ticks = static_cast<unsigned long long>(rate_khz) * static_cast<unsigned long long>(max_ms);
-  std::lock_guard<std::mutex> lk(e->mu);
+  Call call(e);
   hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, e->cs, flag, ticks);
   return hip_ok(e, hipGetLastError(), "stall kernel") ? 0 : -1;
 }
@@ -571,13 +669,14 @@ TTDK_EXPORT int ttdc_probe(void* h, void* buf, long long count, int iters, float
   hipEventCreate(&b);
   int rc = 0;
   {
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (!e->comm) rc = -1;
-    if (rc == 0 && !settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, e->comm, e->cs), "ncclAllReduce"))
+    Call call(e);
+    ncclComm_t c = e->comm.load();
+    if (!c) rc = -1;
+    if (rc == 0 && !settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c, e->cs), "ncclAllReduce"))
       rc = -1;
     hipEventRecord(a, e->cs);
     for (int i = 0; rc == 0 && i < iters; ++i)
-      if (!settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, e->comm, e->cs), "ncclAllReduce")) rc = -1;
+      if (!settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c, e->cs), "ncclAllReduce")) rc = -1;
     hipEventRecord(b, e->cs);
   }
   if (rc == 0 && ttdc_synchronize(e) == 0) {
@@ -596,22 +695,26 @@ TTDK_EXPORT void ttdc_destroy(void* h, int abort) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return;
   {
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> g(e->wmu);
     e->stop = true;
   }
   e->cv.notify_all();
   if (e->wd.joinable()) e->wd.join();
-  if (e->comm) {
+  ncclComm_t c = e->comm.exchange(nullptr);
+  if (c) {
     if (abort || e->failed) {
-      ncclCommAbort(e->comm);
+      ncclCommAbort(c);
     } else {
-      ncclResult_t r = ncclCommFinalize(e->comm);
-      if (settle(e, r, "ncclCommFinalize")) ncclCommDestroy(e->comm);
-      else ncclCommAbort(e->comm);
+      e->comm = c;  // settle polls it while a non-blocking finalize completes
+      ncclResult_t r = ncclCommFinalize(c);
+      const bool fin = settle(e, r, "ncclCommFinalize");
+      e->comm = nullptr;
+      if (fin) ncclCommDestroy(c);
+      else ncclCommAbort(c);
     }
-    e->comm = nullptr;
   }
   if (!abort) hipStreamSynchronize(e->cs);
+  for (void* p : e->retired) hipFree(p);
   for (int i = 0; i < 64; ++i) hipEventDestroy(e->fork[i]);
   hipEventDestroy(e->join);
   for (hipEvent_t ev : e->t_begin) hipEventDestroy(ev);

@@ -36,6 +36,27 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restri
   }
 }
 
+// The three fp32 -> bf16 roundings every kernel uses, side by side (tests pin them bitwise to
+// torch's RNE conversion): f2bf (one element), pack_bf16x2 (a pair in one v_cvt_pk_bf16_f32),
+// pack8 (16-B chunk of four pairs). n % 8 == 0.
+__global__ void bf16_round_probe_kernel(const float* __restrict__ x, bf16_t* __restrict__ one,
+                                        uint32_t* __restrict__ pair, uint4* __restrict__ eight, long long n8) {
+  GRID_STRIDE(i, n8) {
+    float f[8];
+    const f32x4_t a = *reinterpret_cast<const f32x4_t*>(x + 8 * i), b = *reinterpret_cast<const f32x4_t*>(x + 8 * i + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = a[j];
+      f[4 + j] = b[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) one[8 * i + j] = f2bf(f[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pair[4 * i + j] = pack_bf16x2(f[2 * j], f[2 * j + 1]);
+    eight[i] = pack8(f);
+  }
+}
+
 __global__ void bf16_to_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long long n) {
   GRID_STRIDE(i, n) y[i] = bf2f(x[i]);
 }
@@ -334,6 +355,14 @@ using namespace ttdk;
 
 TTDK_EXPORT int ttdk_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st) {
   hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, x, y, n);
+  return hipGetLastError();
+}
+
+TTDK_EXPORT int ttdk_bf16_round_probe(const float* x, bf16_t* one, uint32_t* pair, void* eight, long long n,
+                                      hipStream_t st) {
+  if (n % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bf16_round_probe_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, x, one, pair,
+                     static_cast<uint4*>(eight), n / 8);
   return hipGetLastError();
 }
 

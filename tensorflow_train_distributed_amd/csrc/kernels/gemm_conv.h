@@ -552,6 +552,11 @@ struct EpiParams {
   // no separate fold launch re-reading every slab over the whole chip.
   float* kout;
   int* kctr;
+  // Row sums of the A operand over this launch's K range (gemm256_kernel RS = 1: the weight
+  // gradient dW = dY^T.X also yields the bias gradient colsum(dY) = rowsum(dY^T)): partial slab
+  // rsum[(blockIdx.y * tiles_n + tile_n) * M + m], each (split, tile column) workgroup covering the
+  // K-tiles kt with (kt - kt0) % tiles_n == tile_n; the host folds the slabs.
+  float* rsum;
 };
 
 __device__ __forceinline__ bool beta_row(const EpiParams& E, int m) {
@@ -1412,7 +1417,7 @@ struct Geo {
 // PP: ping-pong schedule — every quadrant phase is {fragment reads + DMA issue} barrier
 // {MFMA cluster} barrier, with the wm = 1 wave half one barrier behind the wm = 0 half, so
 // the two waves of a SIMD alternate MFMA clusters and load segments.
-template <int BN, class OA, class OB, int F8, int PP = 0>
+template <int BN, class OA, class OB, int F8, int PP = 0, int RS = 0>
 __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Params pa, typename OB::Params pb, EpiParams E,
                                                          int M, int N, int K, int tiles_m, int tiles_n,
                                                          int kt_per_split, int m_base) {
@@ -1426,6 +1431,13 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   constexpr bool AK = Traits<OA>::kmaj, BKM = Traits<OB>::kmaj;
   static_assert(F8 == 0 || (AK && BKM), "fp8 operands must be K-major");
   __shared__ __attribute__((aligned(16))) char smem[Gm::SMEM];
+  // RS: A-operand row sums (EpiParams::rsum). MN-major A only, PP schedule, fp32 slab / store
+  // epilogues (the per-wave sum slots [NW][256] fp32 sit after the coefficient area, inside the
+  // bf16 staging region that a mode-1/2 epilogue never uses).
+  static_assert(!RS || (!AK && PP == 1 && F8 == 0 && Traits<OA>::bnpro == 0 && BN == 256),
+                "row sums: MN-major bf16 A on the ping-pong schedule");
+  constexpr int RS_OFF = 2 * Gm::STAGE + 2048;
+  static_assert(!RS || RS_OFF + 8 * 256 * 4 <= Gm::SMEM, "row-sum slots fit the shared memory");
   const int nblk = tiles_m * tiles_n;
   const int t = xcd_remap(blockIdx.x, nblk);
   const int tile_n = t % tiles_n;
@@ -1515,6 +1527,41 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     // still trails the slower half's reads. The last half of tile kt+1 is issued 3 phases
     // before its wait.
     const bool lag = __builtin_amdgcn_readfirstlane(wm) == 1;
+    // RS: thread -> (column group cg of 8 A rows, k-set ks): chunks (ks, cg) and (ks + 32, cg) of
+    // a half (the MN-major image's 32-B slot swizzle, OpDenseMN); the four lanes of a wave with
+    // the same cg (l, l^16, l^32, l^48) are summed by permlane swaps, and lane cg < 16 adds its
+    // wave's partial into the wave's own slots: no atomics, a fixed order -> deterministic.
+    float* rs_slot = reinterpret_cast<float*>(smem + RS_OFF) + wave * 256;
+    const int rs_cg = lane & 15, rs_ks = tid >> 4;
+    const int rs_tn = tile_n, rs_nt = tiles_n;
+    auto rs_half = [&](const char* sA, int rbase) {
+      if constexpr (RS) {
+        float f[8], g2[8];
+        const int j0 = ((rs_cg >> 1) ^ swz_mn<128>(rs_ks)) * 2 + (rs_cg & 1);
+        unpack8(*reinterpret_cast<const uint4*>(sA + (rs_ks * 16 + j0) * 16), f);
+        const int j1 = ((rs_cg >> 1) ^ swz_mn<128>(rs_ks + 32)) * 2 + (rs_cg & 1);
+        unpack8(*reinterpret_cast<const uint4*>(sA + ((rs_ks + 32) * 16 + j1) * 16), g2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = f[j] + g2[j];
+          const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+          v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+          const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+          f[j] = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+        }
+        if (lane < 16) {
+          float* d = rs_slot + rbase + rs_cg * 8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[j] += f[j];
+        }
+      }
+    };
+    if constexpr (RS) {
+      if (lane < 64) {
+        float* z = reinterpret_cast<float*>(smem + RS_OFF) + wave * 256 + lane * 4;
+        *reinterpret_cast<f32x4_t*>(z) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
     if (kt0 < kt1) {
       char* b0 = buf(kt0);
       la.template issue<0>(b0 + A0, kt0, wave);
@@ -1539,6 +1586,8 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
       // P0: (A0, B0)
       read_a(cb + A0, fa[0]);
       read_b(cb + B0, fb[0]);
+      const bool rs_on = RS && ((kt - kt0) % rs_nt) == rs_tn;
+      if (rs_on) rs_half(cb + A0, 0);
       if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
       barrier();
       mma(fa[0], fb[0], acc[0][0]);
@@ -1550,6 +1599,7 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
       barrier();
       // P2: (A1, B1)
       read_a(cb + A1, fa[1]);
+      if (rs_on) rs_half(cb + A1, 128);
       if (has2) {
         la.template issue<0>(cb + A0, kt + 2, wave);
         lb.template issue<0>(cb + B0, kt + 2, wave);
@@ -1723,6 +1773,16 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   }
   wait_vm<0>();
   __syncthreads();
+  if constexpr (RS) {
+    // per-row sum of the eight waves' slots, fixed order
+    if (tid < 256 && m0 + tid < M) {
+      const float* sl = reinterpret_cast<const float*>(smem + RS_OFF);
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += sl[w * 256 + tid];
+      E.rsum[(static_cast<long long>(blockIdx.y) * tiles_n + tile_n) * M + m0 + tid] = v;
+    }
+  }
 
   // ---------------------------------------------------------------- epilogue
   const int g = lane >> 4, i16 = lane & 15;
@@ -2258,6 +2318,22 @@ hipError_t dense_pp(const bf16_t* A, long long lda, bool ak, const bf16_t* B, lo
   return launch<BN, OpDenseMN<128>, OpDenseMN<BH>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
 }
 
+// Weight gradient with the A operand's row sums (EpiParams::rsum: a bias gradient): MN-major A
+// and B, 256-wide tiles, ping-pong schedule, fp32 slab (split-K) or store epilogue.
+inline hipError_t dense_rowsum(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, const EpiParams& pe,
+                               int M, int N, int K, int splits, hipStream_t st) {
+  DenseP pa{A, lda, M}, pb{B, ldb, N};
+  const int tm = ceil_div(M, BM), tn = ceil_div(N, 256);
+  const int ktiles = K / 64;
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  hipLaunchKernelGGL((gemm256_kernel<256, OpDenseMN<128>, OpDenseMN<128>, 0, 1, 1>), dim3(tm * tn, splits), dim3(THR), 0,
+                     st, pa, pb, pe, M, N, K, tm, tn, per, 0);
+  return hipGetLastError();
+}
+
 template <int BN>
 hipError_t dense(const bf16_t* A, long long lda, bool ak, const bf16_t* B, long long ldb, bool bk,
                  const EpiParams& pe, int M, int N, int K, int splits, hipStream_t st) {
@@ -2399,6 +2475,7 @@ inline EpiParams to_epi(const TtdkEpilogue* e) {
   p.pld = 0;
   p.kout = nullptr;
   p.kctr = nullptr;
+  p.rsum = nullptr;
   return p;
 }
 

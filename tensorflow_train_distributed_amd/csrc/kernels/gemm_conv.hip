@@ -43,7 +43,7 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
 // elsewhere a fold pass follows.
 TTDK_EXPORT int ttdk_gemm_bf16_splitk(const bf16_t* A, long long lda, int a_kmajor, const bf16_t* B, long long ldb,
                                       int b_kmajor, int M, int N, int K, int splits, float* ws, float* out, int beta,
-                                      float alpha, hipStream_t st) {
+                                      float alpha, int tile_m, int tile_n, hipStream_t st) {
   TtdkEpilogue te{};
   te.mode = 1;
   te.out = ws;
@@ -56,7 +56,10 @@ TTDK_EXPORT int ttdk_gemm_bf16_splitk(const bf16_t* A, long long lda, int a_kmaj
                    (b_kmajor ? K % 8 == 0 : N % 8 == 0);
   const int bbn = big_bn(M, N, K);
   const int ktiles = K / 64;
-  if (splits > 1 && vec && bbn && (a_kmajor || M % 8 == 0) && big::inkernel_fold() && ktiles >= splits) {
+  // a forced tile (tile_m / tile_n != 0, tests and benches) always takes the slab + fold path,
+  // which honours it; the in-kernel fold exists for the 256-row kernel at its own BN only
+  const bool forced = tile_m != 0 || tile_n != 0;
+  if (!forced && splits > 1 && vec && bbn && (a_kmajor || M % 8 == 0) && big::inkernel_fold() && ktiles >= splits) {
     int* ctr = big::tile_counters(st, ceil_div(M, big::BM) * ceil_div(N, bbn));
     if (ctr) {
       pe.mode = 3;
@@ -67,9 +70,51 @@ TTDK_EXPORT int ttdk_gemm_bf16_splitk(const bf16_t* A, long long lda, int a_kmaj
                         : big::dense<128>(A, lda, a_kmajor, B, ldb, b_kmajor, pe, M, N, K, splits, st);
     }
   }
-  const int rc = ttdk_gemm_bf16(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, splits, 0, 0, &te, st);
+  const int rc = ttdk_gemm_bf16(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, splits, tile_m, tile_n, &te, st);
   if (rc != hipSuccess) return rc;
   return splitk_reduce(ws, splits, static_cast<long long>(M) * N, out, beta, st);
+}
+
+// Weight gradient + bias gradient in one pass over dY: out[M,N] (+)= alpha * A.B with A = dY^T
+// MN-major (A[k*lda + m], k = token) and B MN-major, and rowsum[M] = sum_k A[k][m] (the bias
+// gradient, written) formed from the A tiles already in LDS (gemm256_kernel RS): the separate
+// column-sum pass over dY disappears. ws: splits * M * N floats (split-K slabs) followed by
+// splits * ceil(N / 256) * M floats (row-sum partials). Returns hipErrorInvalidValue when the
+// shape does not take the 256-row ping-pong kernel (the caller keeps its column-sum pass).
+TTDK_EXPORT long long ttdk_gemm_wgrad_bias_ws(int M, int N, int K, int splits) {
+  if (big_bn(M, N, K) != 256) return -1;
+  const int ktiles = K / 64;
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  splits = ceil_div(ktiles, ceil_div(ktiles, splits));
+  return static_cast<long long>(splits) * M * N + static_cast<long long>(splits) * ceil_div(N, 256) * M;
+}
+
+TTDK_EXPORT int ttdk_gemm_wgrad_bias(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                                     int splits, float* ws, float* out, int beta, float alpha, float* rowsum,
+                                     hipStream_t st) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!al(A) || !al(B) || lda % 8 || ldb % 8 || M % 8 || N % 8 || K % 64 || big_bn(M, N, K) != 256 || !rowsum)
+    return hipErrorInvalidValue;
+  const int ktiles = K / 64;
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  splits = ceil_div(ktiles, ceil_div(ktiles, splits));
+  if (ceil_div(ktiles, splits) < 16) return hipErrorInvalidValue;  // the ping-pong schedule's K-tile floor
+  TtdkEpilogue te{};
+  te.mode = 1;
+  te.out = ws;
+  te.ldo = N;
+  te.slab_stride = static_cast<long long>(M) * N;
+  te.alpha = alpha;
+  EpiParams pe = to_epi(&te);
+  float* rs = ws + static_cast<long long>(splits) * M * N;
+  pe.rsum = rs;
+  const int rc = big::dense_rowsum(A, lda, B, ldb, pe, M, N, K, splits, st);
+  if (rc != hipSuccess) return rc;
+  const int r2 = splitk_reduce(ws, splits, static_cast<long long>(M) * N, out, beta, st);
+  if (r2 != hipSuccess) return r2;
+  return splitk_reduce(rs, splits * ceil_div(N, 256), M, rowsum, 0, st);
 }
 
 TTDK_EXPORT int ttdk_splitk_reduce(const float* ws, int splits, long long n, float* out, int beta, hipStream_t st) {

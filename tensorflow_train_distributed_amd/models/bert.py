@@ -158,6 +158,9 @@ class BertPretraining:
         # FFN1 bias gradient from the dGELU dgrad epilogue column statistics instead of a colsum pass
         # on the side stream (TTD_BERT_BIAS_STAT=1; measured neutral-to-slower: 190.4 vs 188.5 ms)
         self.fuse_bias_grad = os.environ.get("TTD_BERT_BIAS_STAT", "0") != "0" and self.device.type == "cuda"
+        # encoder bias gradients formed inside their weight-gradient GEMM from the dy tiles in LDS
+        # (ops.gemm.gemm_wgrad_bias) instead of a column-sum pass over dy (TTD_BERT_BIAS_WGRAD=0: off)
+        self.bias_in_wgrad = os.environ.get("TTD_BERT_BIAS_WGRAD", "1") != "0" and self.device.type == "cuda"
         self._wt = None
         if self.device.type == "cuda":
             from ..ops.transformer import RngState
@@ -303,19 +306,26 @@ class BertPretraining:
                 self._side = torch.cuda.Stream(device=dev)
             side = self._side
 
+        def wgrad_and_bias(dy, x, wout, bout):
+            M, N, Kd = dy.shape[1], x.shape[1], dy.shape[0]
+            splits = G.gemm_wgrad_splits(M, N, Kd, big_wgs=self.wgrad_wgs)
+            if bout is not None and self.bias_in_wgrad and G.wgrad_bias_ok(M, N, Kd, splits):
+                # bias gradient from the weight gradient's own dy tiles (no column-sum pass)
+                G.gemm_wgrad_bias(dy, x, wout, bout, splits=splits)
+                return
+            wgrad(dy, x, wout)
+            if bout is not None:
+                K.colsum(dy, out=bout)
+
         def wgrad_bias(dy, x, wout, bout):
             """weight gradient (+ bias column sum unless bout is None: the producer's epilogue
             already emitted it) on the side stream"""
             if side is None:
-                wgrad(dy, x, wout)
-                if bout is not None:
-                    K.colsum(dy, out=bout)
+                wgrad_and_bias(dy, x, wout, bout)
                 return
             graphs.fork(torch.cuda.current_stream(), side)
             with torch.cuda.stream(side):
-                wgrad(dy, x, wout)
-                if bout is not None:
-                    K.colsum(dy, out=bout)
+                wgrad_and_bias(dy, x, wout, bout)
             keep.extend((dy, x))  # alive until the streams join (no deferred record_stream frees)
 
         wt_ready = None

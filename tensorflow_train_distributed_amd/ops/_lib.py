@@ -50,7 +50,9 @@ G = ctypes.POINTER(ConvGeom)
 _SIGS = {
     # gemm_conv.hip
     "ttdk_gemm_bf16": [P, L, I, P, L, I, I, I, I, I, I, I, E, P],
-    "ttdk_gemm_bf16_splitk": [P, L, I, P, L, I, I, I, I, I, P, P, I, F, P],
+    "ttdk_gemm_bf16_splitk": [P, L, I, P, L, I, I, I, I, I, P, P, I, F, I, I, P],
+    "ttdk_gemm_wgrad_bias": [P, L, P, L, I, I, I, I, P, P, I, F, P, P],
+    "ttdk_gemm_wgrad_bias_ws": [I, I, I, I],
     "ttdk_conv_fwd": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad_bnpro": [P, P, G, P, P, P, E, P],
@@ -109,6 +111,7 @@ _SIGS = {
     # elementwise.hip
     "ttdk_f32_to_bf16": [P, P, L, P],
     "ttdk_bf16_to_f32": [P, P, L, P],
+    "ttdk_bf16_round_probe": [P, P, P, P, L, P],
     "ttdk_pad_channels": [P, P, L, I, I, P],
     "ttdk_unpad_channels": [P, P, L, I, I, P],
     "ttdk_transpose_aca_bf16": [P, P, I, I, I, P],
@@ -134,7 +137,8 @@ def register(sigs: dict):
     _SIGS.update(sigs)
 
 
-_RESTYPE = {"ttdk_conv_dgrad_subpixel_stat_rows": c_longlong, "ttdk_colsum_ws_floats": c_longlong}
+_RESTYPE = {"ttdk_conv_dgrad_subpixel_stat_rows": c_longlong, "ttdk_colsum_ws_floats": c_longlong,
+            "ttdk_gemm_wgrad_bias_ws": c_longlong}
 
 
 def fn(name):

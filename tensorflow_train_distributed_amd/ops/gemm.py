@@ -138,9 +138,11 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
             if not out.is_contiguous():
                 raise ValueError("split-K output must be contiguous")
             ws = torch.empty((splits, M, N), dtype=torch.float32, device=a.device)
-            # the 256-row kernel folds its own slabs (last split of each tile); else a fold pass
+            # the 256-row kernel folds its own slabs (last split of each tile); else (and with a
+            # forced tile, which the slab path honours) a fold pass
             _lib.call("ttdk_gemm_bf16_splitk", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K,
-                      splits, ws.data_ptr(), out.data_ptr(), beta, float(alpha), _lib.stream())
+                      splits, ws.data_ptr(), out.data_ptr(), beta, float(alpha), int(tile[0]), int(tile[1]),
+                      _lib.stream())
             return out
         e = _epi(out, mode=2, beta=beta, alpha=alpha)
     else:
@@ -148,6 +150,45 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     _lib.call("ttdk_gemm_bf16", a.data_ptr(), lda, a_kmajor, b.data_ptr(), ldb, b_kmajor, M, N, K, 1,
               tile[0], tile[1], ctypes.byref(e), _lib.stream())
     return out
+
+
+def wgrad_bias_ok(M, N, K, splits) -> bool:
+    """Whether gemm_wgrad_bias takes this weight gradient (dW[M,N] over K tokens, `splits`
+    K-slices): the 256-wide ping-pong kernel with >= 16 K-tiles per split."""
+    if M % 8 or N % 8 or K % 64:
+        return False
+    if int(_lib.query("ttdk_gemm_wgrad_bias_ws", int(M), int(N), int(K), int(splits))) < 0:
+        return False
+    kt = K // 64
+    s = max(1, min(int(splits), kt))
+    per = -(-kt // s)
+    return per >= 16
+
+
+def gemm_wgrad_bias(dy, x, out, bias_out, splits=1, beta=0, alpha=1.0):
+    """Weight AND bias gradient of a dense layer in one pass over dy: out[M,N] (+)= alpha *
+    dy^T . x (fp32) and bias_out[M] = column sums of dy (written), with dy [K, M] and x [K, N]
+    bf16 row-major (K = tokens). The bias sums are formed from dy's tiles already in LDS by the
+    weight-gradient GEMM (gemm256_kernel RS) — the separate column-sum pass over dy disappears.
+    Callers check wgrad_bias_ok first."""
+    _check2d(dy, torch.bfloat16, "dy")
+    _check2d(x, torch.bfloat16, "x")
+    K, M = dy.shape
+    K2, N = x.shape
+    if K != K2:
+        raise ValueError("gemm_wgrad_bias: token dims differ (%d vs %d)" % (K, K2))
+    if tuple(out.shape) != (M, N) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("gemm_wgrad_bias: out must be a contiguous fp32 [%d, %d]" % (M, N))
+    if bias_out.numel() != M or bias_out.dtype != torch.float32 or not bias_out.is_contiguous():
+        raise ValueError("gemm_wgrad_bias: bias_out must be a contiguous fp32 [%d]" % M)
+    nws = int(_lib.query("ttdk_gemm_wgrad_bias_ws", M, N, K, int(splits)))
+    if nws < 0:
+        raise ValueError("gemm_wgrad_bias: shape %dx%dx%d not on the 256-wide kernel" % (M, N, K))
+    ws = torch.empty(nws, dtype=torch.float32, device=dy.device)
+    _log("wgrad_bias", M, N, K, splits)
+    _lib.call("ttdk_gemm_wgrad_bias", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K, int(splits),
+              ws.data_ptr(), out.data_ptr(), int(beta), float(alpha), bias_out.data_ptr(), _lib.stream())
+    return out, bias_out
 
 
 _C3 = _os.environ.get("TTD_CONV3", "1") != "0"

@@ -251,6 +251,19 @@ def f32_to_bf16(x, out=None):
     return out
 
 
+def bf16_round_probe(x):
+    """The kernels' three fp32 -> bf16 roundings of fp32 `x` (numel % 8 == 0): (f2bf per element,
+    pack_bf16x2 per pair, pack8 per 16-B chunk), each as bf16 bits in an int16 tensor of x's size."""
+    x = x.contiguous()
+    n = x.numel()
+    assert x.dtype == torch.float32 and n % 8 == 0
+    one = torch.empty(n, dtype=torch.int16, device=x.device)
+    pair = torch.empty(n, dtype=torch.int16, device=x.device)
+    eight = torch.empty(n, dtype=torch.int16, device=x.device)
+    _lib.call("ttdk_bf16_round_probe", x.data_ptr(), one.data_ptr(), pair.data_ptr(), eight.data_ptr(), n, _s())
+    return one, pair, eight
+
+
 def bf16_to_f32(x, out=None):
     if out is None:
         out = torch.empty(x.shape, dtype=torch.float32, device=x.device)

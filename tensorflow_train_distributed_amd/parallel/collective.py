@@ -50,9 +50,11 @@ ALGORITHMS = ("allreduce", "hierarchical", "reduce_to_one")
 class BucketedAllReducer:
     def __init__(self, flat, group=None, bucket_mb: float = 32.0, first_bucket_mb: float = 4.0,
                  compress_bf16: bool = False, algorithm: str = "allreduce", num_packs: Optional[int] = None,
-                 engine: str = "auto"):
+                 engine: str = "auto", overlap_ms: Optional[float] = None):
         """engine: "auto" (native RCCL engine on GPU process groups of > 1 rank), "native"
-        (required; also on a one-rank group — tests), "torch" (torch.distributed calls)."""
+        (required; also on a one-rank group — tests), "torch" (torch.distributed calls).
+        overlap_ms: the caller's estimate of the backward the collectives hide under (the native
+        engine's start-up CTA-budget probe uses it, rccl.choose_cta_budget)."""
         if algorithm not in ALGORITHMS:
             raise ValueError("unknown all-reduce algorithm %r (one of %s)" % (algorithm, ALGORITHMS))
         self.flat = flat
@@ -73,24 +75,23 @@ class BucketedAllReducer:
         if ends:  # the alignment padding after the last variable rides in the last bucket
             ends[-1] = flat.numel
         self._var_end = {s.name: e for s, e in zip(flat.specs, ends)}
-        # greedy buckets on variable boundaries
-        self.buckets: List[Tuple[int, int]] = []
-        start = 0
-        limit = int(first_bucket_mb * (1 << 20)) // 4
-        for e in ends:
-            if e - start >= limit:
-                self.buckets.append((start, e))
-                start = e
-                limit = int(bucket_mb * (1 << 20)) // 4
-        if start < flat.numel:
-            self.buckets.append((start, flat.numel))
-        self._bucket_ends = [b[1] for b in self.buckets]
+        self._ends = ends
+        self.bucket_mb = bucket_mb
+        self.first_bucket_mb = first_bucket_mb
+        self._make_buckets()
         # GPU process groups: the native RCCL engine (rccl.py / collective.hip) unless
         # TTD_COLLECTIVE=torch or its self-check failed on some rank
         self.comm = None
         if engine == "native" or (engine == "auto" and self.world > 1 and flat.grad.is_cuda):
             from . import rccl
-            self.comm = rccl.for_group(group, required=engine == "native")
+            self.comm = rccl.for_group(group, required=engine == "native", overlap_ms=overlap_ms,
+                                       bucket_bytes=[(e - s) * (2 if compress_bf16 else 4) for s, e in self.buckets])
+            pol = getattr(self.comm, "policy", None) or {}
+            fb = pol.get("first_bucket_mb")
+            if fb and num_packs is None and fb > self.first_bucket_mb:
+                # the probe found small collectives latency-bound: start with a bigger bucket
+                self.first_bucket_mb = fb
+                self._make_buckets()
         self.engine = "native-rccl" if self.comm is not None else ("torch-" + dist.get_backend(group)
                                                                    if self.world > 1 else "none")
         # CUs the persistent kernels leave to the collectives while buckets are in flight
@@ -108,6 +109,26 @@ class BucketedAllReducer:
         self._keep = []
         self._timed = None
         self.launch_log: List[int] = []
+
+    def _make_buckets(self):
+        """Greedy buckets on variable boundaries: the first `first_bucket_mb` (communication
+        starts early), then `bucket_mb` each."""
+        self.buckets: List[Tuple[int, int]] = []
+        start = 0
+        limit = int(self.first_bucket_mb * (1 << 20)) // 4
+        for e in self._ends:
+            if e - start >= limit:
+                self.buckets.append((start, e))
+                start = e
+                limit = int(self.bucket_mb * (1 << 20)) // 4
+        if start < self.flat.numel:
+            self.buckets.append((start, self.flat.numel))
+        self._bucket_ends = [b[1] for b in self.buckets]
+
+    def policy(self):
+        """The native engine's start-up collective policy (CTA budget, probe table, reason), or
+        None on the torch / single-rank paths."""
+        return getattr(self.comm, "policy", None)
 
     def bytes_per_step(self) -> int:
         """Bytes each rank hands to the collectives per step (all buckets)."""
@@ -161,8 +182,15 @@ class BucketedAllReducer:
             # here to finish() use the remaining ones
             self._reserve(True)
         if self.comm is not None:
-            # in place on the communicator stream, ordered after the current (producing) stream
-            self.comm.bucket(t, algorithm=self.algorithm, compress=self.compress)
+            # in place on the communicator stream, ordered after the current (producing) stream;
+            # under a segmented hipGraph capture the fork is an event node pair and the
+            # communicator stream records its own linear graph segments (utils/graphs.py)
+            from ..utils import graphs
+            if graphs.capturing_segmented():
+                graphs.fork(torch.cuda.current_stream(), self.comm.stream)
+                self.comm.bucket(t, algorithm=self.algorithm, compress=self.compress, fork=False)
+            else:
+                self.comm.bucket(t, algorithm=self.algorithm, compress=self.compress)
             return
         c = t.to(torch.bfloat16) if self.compress else t
         if self.algorithm == "allreduce":
@@ -219,7 +247,11 @@ class BucketedAllReducer:
         if self.comm is not None:
             if self._timed is not None:
                 self._timed[0].record()  # the backward's last queued work
-            self.comm.join()  # the current stream waits for the buckets (no host sync)
+            from ..utils import graphs
+            if graphs.capturing_segmented():
+                graphs.join(torch.cuda.current_stream(), self.comm.stream)
+            else:
+                self.comm.join()  # the current stream waits for the buckets (no host sync)
             if self._timed is not None:
                 self._timed[1].record()
             return

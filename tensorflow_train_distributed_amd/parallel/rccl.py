@@ -10,19 +10,28 @@ synchronisation anywhere on the step path, and the calls are capture-safe (hipGr
 Co-scheduling policy (MI355X, one process per GPU): the fastest backward kernels are persistent,
 one workgroup per CU with a static work split (gemm256p, the pointwise / halo conv kernels), so
 a workgroup that finds its CU held by an all-reduce CTA delays the whole launch by a full share.
-A multi-rank communicator therefore gets a fixed CTA budget (RCCL maxCTAs, default 8 = 3 % of
-the 256 CUs: a ResNet-50 step moves ~100 MB of fp32 gradients, BERT-Large ~1.3 GB, both far
-below what 8 channels carry over xGMI in the backward's duration), and while the step's buckets
-are in flight the persistent grids size themselves to the remaining CUs
-(ttdk_set_reserved_cus, set by BucketedAllReducer from its first bucket launch to finish()).
-tools/comm_interference.py measures the policy on one GPU with an emulated all-reduce of the
-same CTA count launched at the real bucket points.
+A small RCCL CTA budget (maxCTAs 8 = 3 % of the 256 CUs) keeps the collectives out of the
+compute's way (tools/comm_interference.py: < 1 % step-time cost with 200 us of peer skew) — IF
+those 8 channels still carry the step's gradient bytes inside the backward. That is measured,
+not assumed: when a multi-rank communicator is created (`for_group`), the engine probes the
+all-reduce at 1 MB and 32 MB on RCCL's own CTA choice and on the capped budget (one
+communicator each), every rank takes the slowest rank's numbers (so all ranks decide alike),
+and `choose_cta_budget` keeps the cap only if the projected per-step all-reduce time at the
+capped bandwidth, times a 1.5 margin, fits the backward's overlap window (`overlap_ms`, the
+caller's estimate of its backward) — otherwise RCCL's own budget, the faster one. Without an
+overlap estimate the cap is kept when it delivers >= 70 % of the default bus bandwidth. The
+probe table, the choice and the reason travel with the communicator (`policy`) into the bench
+JSON. While the step's buckets are in flight the persistent grids can size themselves to the
+remaining CUs (ttdk_set_reserved_cus, opt-in TTD_RESERVE_COMM_CUS=1).
+Latency-bound small buckets: when the 1 MB probe runs at < 25 % of the 32 MB bus bandwidth
+(per-collective latency dominates), `policy["first_bucket_mb"]` raises the reducer's first
+bucket so the first collective is not a latency-bound one.
 
 Tuning knobs (environment, read at communicator creation):
   TTD_RCCL_MAX_CTAS / TTD_RCCL_MIN_CTAS  RCCL's CTA (workgroup) budget per collective: how many
                                          CUs a bucket all-reduce may occupy while it overlaps
-                                         the backward GEMMs (default max 8 on multi-rank
-                                         groups; 0 = RCCL's own choice, no CU reservation)
+                                         the backward GEMMs (unset: chosen by the start-up
+                                         probe; 0 = RCCL's own choice, no CU reservation)
   TTD_RCCL_PRIO                          communicator stream priority (default 0 = normal, below
                                          the main chain's high-priority stream)
   TTD_RCCL_TIMEOUT                       seconds before a collective that makes no progress (a
@@ -66,8 +75,12 @@ def _lib():
         lib.ttdc_stream.argtypes = [c_void_p]
         lib.ttdc_bucket.restype = c_int
         lib.ttdc_bucket.argtypes = [c_void_p, c_void_p, c_longlong, c_int, c_int, c_int, c_int, c_void_p]
+        lib.ttdc_bucket_nofork.restype = c_int
+        lib.ttdc_bucket_nofork.argtypes = [c_void_p, c_void_p, c_longlong, c_int, c_int, c_int, c_int]
         lib.ttdc_join.restype = c_int
         lib.ttdc_join.argtypes = [c_void_p, c_void_p]
+        lib.ttdc_arm.restype = c_int
+        lib.ttdc_arm.argtypes = [c_void_p, c_void_p]
         lib.ttdc_collective.restype = c_int
         lib.ttdc_collective.argtypes = [c_void_p, c_int, c_void_p, c_longlong, c_int, c_int, c_int, c_void_p]
         lib.ttdc_synchronize.restype = c_int
@@ -102,7 +115,68 @@ def rccl_version() -> int:
     return int(_lib().ttdc_version())
 
 
-DEFAULT_MAX_CTAS = 8
+DEFAULT_MAX_CTAS = 8          # the capped budget the start-up probe evaluates
+PROBE_BYTES = (1 << 20, 32 << 20)
+CAP_MIN_BW_RATIO = 0.70        # no overlap estimate: keep the cap at >= 70 % of default bandwidth
+OVERLAP_MARGIN = 1.5
+LATENCY_BOUND_RATIO = 0.25     # 1 MB bus bandwidth below this share of 32 MB's: latency-bound
+
+
+def _ring_ms(nbytes: float, busbw_gbps: float, nranks: int) -> float:
+    """Ring all-reduce time of `nbytes` at bus bandwidth `busbw_gbps` (busbw = algbw*2(n-1)/n)."""
+    if busbw_gbps <= 0:
+        return float("inf")
+    return 2.0 * (nranks - 1) / nranks * nbytes / (busbw_gbps * 1e9) * 1e3
+
+
+def projected_step_ms(probe, bucket_bytes, nranks: int) -> float:
+    """Per-step all-reduce time of `bucket_bytes` (one collective each) from a probe table
+    [{bytes, ms, busbw_GBps}, ...] of one CTA budget: t(b) = latency + ring time at the largest
+    probed size's bandwidth, latency = what the smallest probe took beyond its ring time."""
+    pts = sorted(probe, key=lambda d: d["bytes"])
+    big, small = pts[-1], pts[0]
+    bw = float(big["busbw_GBps"])
+    lat = max(0.0, float(small["ms"]) - _ring_ms(small["bytes"], bw, nranks)) if len(pts) > 1 else 0.0
+    return sum(lat + _ring_ms(b, bw, nranks) for b in bucket_bytes)
+
+
+def choose_cta_budget(probes, bucket_bytes, nranks: int, overlap_ms=None, cap: int = DEFAULT_MAX_CTAS,
+                      margin: float = OVERLAP_MARGIN):
+    """The CTA budget for the gradient communicator from measured probes.
+
+    probes: {ctas: [{"bytes", "ms", "busbw_GBps"}, ...]} with the capped budget `cap` and 0 (RCCL's
+    own choice); bucket_bytes: the reducer's per-step collective sizes; overlap_ms: the backward
+    time the collectives can hide under (None: unknown). Returns a policy dict:
+    {cta_budget, reason, projected_ms: {ctas: ms}, first_bucket_mb (or None), probe}."""
+    proj = {c: projected_step_ms(p, bucket_bytes, nranks) for c, p in probes.items()}
+    bw = {c: max(float(d["busbw_GBps"]) for d in p) for c, p in probes.items()}
+    pol = {"projected_ms": {str(c): round(v, 3) for c, v in proj.items()}, "probe": probes,
+           "overlap_ms": overlap_ms, "first_bucket_mb": None}
+    if cap not in probes:
+        pol.update(cta_budget=0, reason="no probe of the capped budget")
+    elif 0 not in probes:
+        pol.update(cta_budget=cap, reason="no probe of RCCL's default budget")
+    elif overlap_ms is not None and overlap_ms > 0:
+        if proj[cap] * margin <= overlap_ms:
+            pol.update(cta_budget=cap, reason="capped budget hides %.2f ms x %.1f in the %.1f ms backward"
+                       % (proj[cap], margin, overlap_ms))
+        else:
+            pol.update(cta_budget=0, reason="capped budget needs %.2f ms x %.1f > %.1f ms backward: RCCL default "
+                       "(%.2f ms)" % (proj[cap], margin, overlap_ms, proj[0]))
+    else:
+        ratio = bw[cap] / bw[0] if bw[0] > 0 else 1.0
+        if ratio >= CAP_MIN_BW_RATIO:
+            pol.update(cta_budget=cap, reason="capped budget delivers %.0f %% of the default bus bandwidth" % (100 * ratio))
+        else:
+            pol.update(cta_budget=0, reason="capped budget delivers only %.0f %% of the default bus bandwidth"
+                       % (100 * ratio))
+    # latency-bound small collectives: make the first bucket big enough to leave that regime
+    chosen = probes.get(pol["cta_budget"]) or next(iter(probes.values()))
+    pts = sorted(chosen, key=lambda d: d["bytes"])
+    if len(pts) > 1 and float(pts[-1]["busbw_GBps"]) > 0 and \
+            float(pts[0]["busbw_GBps"]) < LATENCY_BOUND_RATIO * float(pts[-1]["busbw_GBps"]):
+        pol["first_bucket_mb"] = 8.0
+    return pol
 
 
 def set_reserved_cus(n: int) -> int:
@@ -149,7 +223,7 @@ class RcclCommunicator:
         prio = int(env("TTD_RCCL_PRIO", "0")) if priority is None else int(priority)
         min_ctas = int(env("TTD_RCCL_MIN_CTAS", "0")) if min_ctas is None else int(min_ctas)
         if max_ctas is None:
-            max_ctas = int(env("TTD_RCCL_MAX_CTAS", str(DEFAULT_MAX_CTAS if int(nranks) > 1 else 0)))
+            max_ctas = int(env("TTD_RCCL_MAX_CTAS", "0"))
         max_ctas = int(max_ctas)
         if min_ctas > max_ctas > 0:
             min_ctas = max_ctas
@@ -166,6 +240,7 @@ class RcclCommunicator:
                                           % lib.ttdc_error(None).decode())
         self._h = h
         self.stream = torch.cuda.ExternalStream(lib.ttdc_stream(h), device=self.device)
+        self.policy = None  # set by for_group's start-up probe (choose_cta_budget)
 
     @classmethod
     def for_group(cls, group=None, device=None, **kw) -> "RcclCommunicator":
@@ -199,16 +274,29 @@ class RcclCommunicator:
         return _lib().ttdc_error(self._h).decode("utf-8", "replace") if self._h else "destroyed"
 
     def bucket(self, t: torch.Tensor, op: str = "sum", algorithm: str = "allreduce", compress: bool = False,
-               producer=None):
+               producer=None, fork: bool = True):
         """In-place reduction of contiguous `t` on the communicator stream, ordered after the
-        work already queued on `producer` (default: the current stream)."""
+        work already queued on `producer` (default: the current stream). fork=False: no fork
+        (the caller ordered `self.stream` itself, e.g. through utils.graphs.fork under a
+        segmented capture)."""
         assert t.is_contiguous() and t.device == self.device
-        self._check(_lib().ttdc_bucket(self._h, t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], _ALGO[algorithm],
-                                       1 if compress else 0, _stream_ptr(producer)), "bucket all-reduce")
+        if fork:
+            rc = _lib().ttdc_bucket(self._h, t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], _ALGO[algorithm],
+                                    1 if compress else 0, _stream_ptr(producer))
+        else:
+            rc = _lib().ttdc_bucket_nofork(self._h, t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], _ALGO[algorithm],
+                                           1 if compress else 0)
+        self._check(rc, "bucket all-reduce")
 
     def join(self, consumer=None):
         """`consumer` (default: current stream) waits for every collective queued so far."""
         self._check(_lib().ttdc_join(self._h, _stream_ptr(consumer)), "collective join")
+
+    def arm(self, stream=None):
+        """Arm the no-progress watchdog after a hipGraph replay on `stream` (default: current):
+        a join captured into the graph records no marker of its own, so without this a replayed
+        step whose collectives never finish would hang without a deadline."""
+        self._check(_lib().ttdc_arm(self._h, _stream_ptr(stream)), "watchdog arm")
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum", stream=None) -> torch.Tensor:
         """Stream-ordered in-place all-reduce on `stream` (default: current)."""
@@ -290,12 +378,50 @@ def _key(group):
     return (_PG["generation"], id(group) if group is not None else None)
 
 
-def for_group(group=None, required: bool = False) -> Optional[RcclCommunicator]:
+def _probe_budgets(group, overlap_ms, bucket_bytes):
+    """Create a communicator per candidate CTA budget, probe each, keep the one the policy
+    picks (collective: every rank reaches the same choice from the slowest rank's numbers)."""
+    world = dist.get_world_size(group)
+    comms, probes = {}, {}
+    try:
+        for ctas in (DEFAULT_MAX_CTAS, 0):
+            c = RcclCommunicator.for_group(group, max_ctas=ctas)
+            comms[ctas] = c
+            probes[ctas] = [c.probe(nb, iters=5) for nb in PROBE_BYTES]
+        # identical tables everywhere: the slowest rank's time per (budget, size)
+        t = torch.tensor([d["ms"] for c in (DEFAULT_MAX_CTAS, 0) for d in probes[c]], dtype=torch.float64,
+                         device=comms[0].device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        i = 0
+        for c in (DEFAULT_MAX_CTAS, 0):
+            for d in probes[c]:
+                d["ms"] = round(float(t[i]), 4)
+                d["busbw_GBps"] = round(2.0 * (world - 1) / world * d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1) \
+                    if d["ms"] > 0 else 0.0
+                i += 1
+        pol = choose_cta_budget(probes, bucket_bytes or [32 << 20], world, overlap_ms)
+    except Exception:
+        for c in comms.values():
+            c.destroy(abort=True)
+        raise
+    keep = pol["cta_budget"]
+    for ctas, c in comms.items():
+        if ctas != keep:
+            c.destroy(abort=False)
+    comm = comms[keep]
+    comm.policy = pol
+    return comm
+
+
+def for_group(group=None, required: bool = False, overlap_ms=None, bucket_bytes=None) -> Optional[RcclCommunicator]:
     """The native communicator of `group` (created and self-checked on first use), or None when
     the native engine does not apply: a non-RCCL group (gloo), a one-rank group, TTD_COLLECTIVE=
     torch, or a failed self-check on ANY rank (every rank then agrees to use the torch process
     group; the reason is kept in `failure_reason`). Collective: all ranks of `group` call it.
-    required=True: also on a one-rank group, and raise instead of returning None."""
+    required=True: also on a one-rank group, and raise instead of returning None.
+    Multi-rank groups without TTD_RCCL_MAX_CTAS get their CTA budget from the start-up probe
+    (module docstring): `overlap_ms` (the backward the collectives hide under) and
+    `bucket_bytes` (per-step collective sizes) feed `choose_cta_budget`."""
     if not dist.is_initialized() or dist.get_backend(group) != "nccl":
         if required:
             raise errors.FailedPreconditionError("the native RCCL engine needs an initialised nccl process group")
@@ -309,11 +435,16 @@ def for_group(group=None, required: bool = False) -> Optional[RcclCommunicator]:
         return None
     comm, reason = None, ""
     try:
-        comm = RcclCommunicator.for_group(group)
+        w = dist.get_world_size(group)
+        if w > 1 and "TTD_RCCL_MAX_CTAS" not in os.environ and os.environ.get("TTD_RCCL_PROBE", "1") == "1":
+            comm = _probe_budgets(group, overlap_ms, bucket_bytes)
+        else:
+            comm = RcclCommunicator.for_group(group)
+            comm.policy = {"cta_budget": comm.max_ctas, "reason": "fixed (TTD_RCCL_MAX_CTAS / one rank / "
+                           "TTD_RCCL_PROBE=0)", "probe": None, "first_bucket_mb": None}
         # self-check: sum of (rank + 1) over the group, stream-ordered on the current stream
         t = torch.full((1024,), float(dist.get_rank(group) + 1), dtype=torch.float32, device=comm.device)
         comm.all_reduce_(t)
-        w = dist.get_world_size(group)
         ok = bool(torch.all(t == w * (w + 1) / 2).item())
         if not ok:
             reason = "self-check all-reduce returned a wrong sum"

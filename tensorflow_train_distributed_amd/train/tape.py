@@ -205,8 +205,19 @@ class GradientTape:
 def clip_by_global_norm(t_list, clip_norm, use_norm=None):
     """tf.clip_by_global_norm: scale every tensor by clip_norm / max(global_norm, clip_norm).
     Returns (clipped list, global_norm). None entries pass through. One fused norm over the
-    list (torch._foreach_norm), no host sync."""
+    list (torch._foreach_norm), no host sync. `use_norm` may be a tensor or a Python number.
+
+    Divergence from TF MirroredStrategy (documented, parity unpinned: the reference has no
+    clipping): inside a replica context `GradientTape.gradient` here returns the gradients
+    already all-reduced across replicas (the bucketed all-reduce overlaps the backward, tape.py),
+    so clipping between `gradient()` and `apply_gradients` clips the replica-SUMMED gradient —
+    the same as clipping the big-batch gradient of a single replica. TF clips each replica's
+    local gradient there and aggregates afterwards, so its clip triggers at different norms.
+    For per-replica clipping, clip inside the loss (or scale the per-replica loss)."""
     ts = [t for t in t_list if t is not None]
+    if use_norm is not None and not isinstance(use_norm, torch.Tensor):
+        dev = ts[0].device if ts else None
+        use_norm = torch.as_tensor(float(use_norm), dtype=torch.float32, device=dev)
     if use_norm is None:
         if ts:
             norms = torch._foreach_norm([t.float() for t in ts])

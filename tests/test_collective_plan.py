@@ -121,3 +121,70 @@ def test_reducer_reserves_cus_while_buckets_are_in_flight(monkeypatch):
     red.mark_ready("v2")
     red.finish()
     assert calls == [8, 0, "join"] and len(FakeComm.launched) == len(red.buckets)
+
+
+def _probe(ms_1m, ms_32m, world):
+    def row(nb, ms):
+        return {"bytes": nb, "ms": ms, "busbw_GBps": round(2.0 * (world - 1) / world * nb / (ms * 1e-3) / 1e9, 1)}
+    return [row(1 << 20, ms_1m), row(32 << 20, ms_32m)]
+
+
+def test_cta_budget_policy_from_synthetic_probes():
+    """rccl.choose_cta_budget: the capped budget stays only when the projected per-step
+    all-reduce time at ITS measured bandwidth (x1.5 margin) fits the backward; otherwise RCCL's
+    own budget. Without an overlap estimate the bandwidth ratio decides."""
+    from tensorflow_train_distributed_amd.parallel import rccl
+    w = 8
+    buckets = [4 << 20] + [32 << 20] * 3 + [5 << 20]  # ResNet-50: ~105 MB of fp32 gradients
+    # 8 CTAs at ~150 GB/s bus bandwidth, default at ~300 GB/s: 105 MB needs ~1.4 ms capped
+    fast = {8: _probe(0.03, 0.39, w), 0: _probe(0.025, 0.195, w)}
+    pol = rccl.choose_cta_budget(fast, buckets, w, overlap_ms=44.0)
+    assert pol["cta_budget"] == 8 and "hides" in pol["reason"]
+    assert 1.0 < pol["projected_ms"]["8"] < 2.5 and pol["projected_ms"]["0"] < pol["projected_ms"]["8"]
+    # BERT-Large-sized gradients (1.34 GB) with a cap that only reaches 20 GB/s: 8 CTAs cannot
+    # hide them in a 120 ms backward -> RCCL's default
+    slow_cap = {8: _probe(0.05, 2.94, w), 0: _probe(0.025, 0.195, w)}
+    big = [32 << 20] * 42
+    pol = rccl.choose_cta_budget(slow_cap, big, w, overlap_ms=120.0)
+    assert pol["cta_budget"] == 0 and "RCCL default" in pol["reason"]
+    assert pol["projected_ms"]["8"] * 1.5 > 120.0
+    # the same probes with the small ResNet gradients: 105 MB at 20 GB/s is ~9 ms, x1.5 < 44
+    assert rccl.choose_cta_budget(slow_cap, buckets, w, overlap_ms=44.0)["cta_budget"] == 8
+    # no overlap estimate: bandwidth ratio (50 % < 70 % -> default; 90 % -> cap)
+    assert rccl.choose_cta_budget(fast, buckets, w)["cta_budget"] == 0
+    near = {8: _probe(0.03, 0.217, w), 0: _probe(0.025, 0.195, w)}
+    assert rccl.choose_cta_budget(near, buckets, w)["cta_budget"] == 8
+    # one budget missing from the table: take the one that was measured
+    assert rccl.choose_cta_budget({0: fast[0]}, buckets, w, overlap_ms=44.0)["cta_budget"] == 0
+    assert rccl.choose_cta_budget({8: fast[8]}, buckets, w, overlap_ms=44.0)["cta_budget"] == 8
+
+
+def test_cta_policy_latency_bound_small_buckets_raise_the_first_bucket():
+    """A 1 MB all-reduce at < 25 % of the 32 MB bus bandwidth is latency-bound: the policy asks
+    for an 8 MB first bucket, and BucketedAllReducer re-buckets with it."""
+    from tensorflow_train_distributed_amd.parallel import collective, rccl
+    from tensorflow_train_distributed_amd.train.flat import FlatParams, ParamSpec
+    w = 8
+    lat = {8: _probe(0.2, 0.39, w), 0: _probe(0.2, 0.195, w)}  # 1 MB in 200 us: ~9 GB/s
+    pol = rccl.choose_cta_budget(lat, [32 << 20] * 4, w, overlap_ms=44.0)
+    assert pol["first_bucket_mb"] == 8.0
+    ok = {8: _probe(0.012, 0.39, w), 0: _probe(0.01, 0.195, w)}
+    assert rccl.choose_cta_budget(ok, [32 << 20] * 4, w, overlap_ms=44.0)["first_bucket_mb"] is None
+    # latency term: 100 buckets of 1 MB cost ~100 x the per-collective latency
+    t_small = rccl.projected_step_ms(lat[0], [1 << 20] * 100, w)
+    assert t_small > 100 * 0.15
+
+    class FakeComm:
+        max_ctas = 0
+        policy = pol
+
+    specs = [ParamSpec("v%d" % i, (n,), None, True) for i, n in enumerate([600000] * 10)]
+    p = FlatParams(specs, "cpu", compute_dtype=None)
+    red = collective.BucketedAllReducer(p, bucket_mb=32.0, first_bucket_mb=2.0)
+    first_before = red.buckets[0][1] - red.buckets[0][0]
+    red.comm = FakeComm()
+    fb = red.policy()["first_bucket_mb"]
+    red.first_bucket_mb = fb
+    red._make_buckets()
+    assert (red.buckets[0][1] - red.buckets[0][0]) * 4 >= 8 << 20 > first_before * 4
+    assert red.buckets[-1][1] == p.numel and all(a[1] == b[0] for a, b in zip(red.buckets, red.buckets[1:]))

@@ -723,3 +723,34 @@ def test_bn_backward_apply_e5m2_copy_and_amax():
     back = K.dequant_fp8(q8, slot[2:3], e5m2=True).float().view(M, C)
     assert _rel(back, dz.float()) < 0.08
     assert abs(float(slot[8:72].max()) - float(dz.float().abs().max())) <= 1e-6 + 1e-2 * float(dz.float().abs().max())
+
+
+@pytest.mark.parametrize("M,N,K,splits,beta", [(1024, 1024, 8192, 4, 0), (4096, 1024, 4096, 2, 1),
+                                               (1024, 4096, 4096, 1, 0), (1032, 1160, 8192, 3, 0)])
+def test_weight_gradient_with_fused_bias_rowsum_vs_fp32(M, N, K, splits, beta):
+    """gemm_wgrad_bias: dW (+)= dy^T.x on the 256-wide ping-pong kernel AND the bias gradient
+    colsum(dy) from the same dy tiles in LDS (gemm256_kernel RS) vs fp32 torch; the last shape
+    has a partial 256-row tile (M = 1032) and a non-multiple-of-256 N. Deterministic: two runs
+    agree bitwise."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(0)
+    dy = (torch.randn(K, M, device="cuda") * 0.5).bfloat16()
+    x = torch.randn(K, N, device="cuda").bfloat16()
+    assert G.wgrad_bias_ok(M, N, K, splits)
+    out0 = torch.randn(M, N, device="cuda")
+    out = out0.clone()
+    bias = torch.full((M,), 7.0, device="cuda")
+    G.gemm_wgrad_bias(dy, x, out, bias, splits=splits, beta=beta)
+    ref = dy.float().t() @ x.float() + (out0 if beta else 0)
+    rel = float((out - ref).norm() / ref.norm())
+    assert rel < 2e-3, rel
+    bref = dy.float().sum(0)
+    torch.testing.assert_close(bias, bref, rtol=1e-4, atol=1e-3)
+    out2 = out0.clone()
+    bias2 = torch.zeros(M, device="cuda")
+    G.gemm_wgrad_bias(dy, x, out2, bias2, splits=splits, beta=beta)
+    assert torch.equal(out, out2) and torch.equal(bias, bias2)
+    # the plain split-K path computes the same weight gradient
+    out3 = out0.clone()
+    G.gemm(dy, x, trans_a=True, out=out3, splits=splits, beta=beta)
+    torch.testing.assert_close(out, out3, rtol=1e-5, atol=1e-4)

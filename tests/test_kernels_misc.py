@@ -306,3 +306,40 @@ def test_pad_channels_rgb_fast_path():
     x2 = torch.randn(3, 5, 3, 3, device="cuda").bfloat16()  # 45 rows -> generic path
     y2 = K.pad_channels(x2, 8)
     assert torch.equal(y2[..., :3], x2) and bool((y2[..., 3:] == 0).all())
+
+
+def test_bf16_rounding_matches_torch_bitwise():
+    """f2bf / pack_bf16x2 / pack8 (common.h: every kernel's fp32 -> bf16 store) against torch's
+    round-to-nearest-even conversion, bitwise, on 2^24 random bit patterns (every exponent,
+    denormals included) plus the edge classes: exact ties (low half 0x8000) with even and odd
+    kept mantissas, one ulp either side of a tie, +-0, +-inf, the largest finite values (which
+    round to inf), the smallest denormals, and NaNs (any NaN must stay a NaN)."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    g = torch.Generator().manual_seed(7)
+    rnd = torch.randint(-2**31, 2**31 - 1, (1 << 24,), generator=g, dtype=torch.int64)
+    hi = torch.randint(0, 1 << 16, (1 << 16,), generator=g, dtype=torch.int64) << 16
+    ties = torch.cat([hi | 0x8000, hi | 0x7fff, hi | 0x8001, hi | 0x0001, hi | 0xffff])
+    edges = torch.tensor([0x00000000, 0x80000000, 0x7f800000, 0xff800000, 0x7f7fffff, 0xff7fffff, 0x7f7f8000,
+                          0x7f7f7fff, 0x00000001, 0x80000001, 0x00008000, 0x00018000, 0x007fffff, 0x00800000,
+                          0x7fc00000, 0xffc00000, 0x7f800001, 0x7fbfffff, 0x3f808000, 0x3f818000, 0x3f80ffff,
+                          0xbf808000, 0x3f800000, 0x00007fff], dtype=torch.int64)
+    bits = torch.cat([rnd & 0xffffffff, ties, edges])
+    bits = bits[: bits.numel() // 8 * 8]
+    x_cpu = (bits.to(torch.int64) & 0xffffffff).to(torch.int64)
+    x_cpu = torch.where(x_cpu >= 2**31, x_cpu - 2**32, x_cpu).to(torch.int32).view(torch.float32)
+    ref = x_cpu.to(torch.bfloat16).view(torch.int16)
+    one, pair, eight = K.bf16_round_probe(x_cpu.cuda())
+    torch.cuda.synchronize()
+    isnan = torch.isnan(x_cpu)
+    for name, got in (("f2bf", one), ("pack_bf16x2", pair), ("pack8", eight)):
+        got = got.cpu()
+        bad = (got != ref) & ~isnan
+        assert int(bad.sum()) == 0, (name, int(bad.sum()), hex(int(x_cpu.view(torch.int32)[bad][0]) & 0xffffffff),
+                                     hex(int(got[bad][0]) & 0xffff), hex(int(ref[bad][0]) & 0xffff))
+        gn = got[isnan].to(torch.int32) & 0xffff
+        # a NaN stays a NaN (its sign and payload are not specified: torch's CPU conversion returns
+        # the canonical 0x7fc0, the hardware conversion a quiet NaN of its own)
+        assert bool(((gn & 0x7f80) == 0x7f80).all() and ((gn & 0x007f) != 0).all()), (name, "NaN not kept")
+    # the GPU's own torch conversion agrees too (what torch-side reference code computes on device)
+    dev_ref = x_cpu.cuda().to(torch.bfloat16).view(torch.int16).cpu()
+    assert int(((dev_ref != ref) & ~isnan).sum()) == 0

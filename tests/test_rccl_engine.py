@@ -197,3 +197,68 @@ def test_persistent_grids_follow_the_cu_reservation():
     finally:
         rccl.set_reserved_cus(old)
     assert rccl.persistent_cus() == total
+
+
+def test_segmented_capture_with_bucket_launches_matches_eager():
+    """N>1's hipGraph: under utils.graphs.capture_segmented the reducer's bucket forks and its
+    final join become event nodes and the communicator stream records its own linear graph
+    segments (parallel/collective.py). On a one-rank native communicator the replayed step
+    (gradients produced on a side stream, buckets launched as they become final, the optimizer-
+    like consumer on the main stream after finish()) matches the eager step bitwise, the
+    bucket launches are in the graph (a replay re-reduces fresh data), and arming the watchdog
+    after a replay leaves the engine healthy."""
+    import torch.distributed as dist
+    from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer
+    from tensorflow_train_distributed_amd.train.flat import FlatParams, ParamSpec
+    from tensorflow_train_distributed_amd.utils import graphs
+    assert not dist.is_initialized()
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        sizes = [20000, 3, 1200000, 5000, 250000]
+        specs = [ParamSpec("v%d" % i, (n,), None, True) for i, n in enumerate(sizes)]
+        p = FlatParams(specs, dev, compute_dtype=None)
+        red = BucketedAllReducer(p, bucket_mb=1.0, first_bucket_mb=0.05, compress_bf16=True, engine="native")
+        assert red.engine == "native-rccl" and len(red.buckets) >= 3
+        src = torch.randn(p.numel, device=dev) * p.valid_mask().to(dev)
+        out = torch.zeros(p.numel, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        main = torch.cuda.Stream(device=dev)
+
+        def step():
+            red.begin()
+            cur = torch.cuda.current_stream()
+            graphs.fork(cur, side)
+            with torch.cuda.stream(side):
+                for s in specs:  # "backward": each gradient final, then its buckets launch
+                    o, n = p.offsets[s.name], s.shape[0]
+                    p.grad[o:o + n].copy_(src[o:o + n] * 2.0)
+                    red.mark_ready(s.name)
+            graphs.join(cur, side)
+            red.finish()
+            out.copy_(p.grad * 3.0)  # consumer after the collectives
+            return out
+
+        with torch.cuda.stream(main):
+            step()
+        torch.cuda.synchronize()
+        eager = out.clone()
+        torch.testing.assert_close(eager, (src * 2.0).bfloat16().float() * 3.0, rtol=0, atol=0)
+        seg = graphs.capture_segmented(step, main=main, warmup=1)
+        assert seg.info["streams"] >= 3, seg.info  # main, side and the communicator stream
+        out.zero_()
+        p.grad.zero_()
+        seg.replay()
+        red.comm.arm(main)
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
+        src.mul_(-0.5)  # fresh data: the replayed buckets must reduce (cast) it again
+        seg.replay()
+        red.comm.arm(main)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out, (src * 2.0).bfloat16().float() * 3.0, rtol=0, atol=0)
+        assert not red.comm.aborted
+    finally:
+        from tensorflow_train_distributed_amd.parallel import rccl
+        rccl.abort_all()
+        dist.destroy_process_group()
