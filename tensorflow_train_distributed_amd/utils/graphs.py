@@ -243,6 +243,16 @@ class SegmentedCapture:
             with torch.cuda.stream(self.main):
                 out = fn()
             self._end_all()
+        except BaseException:
+            # leave no stream in capture mode behind (the caller may fall back to eager steps)
+            for s, g in list(self.cur.values()):
+                try:
+                    with torch.cuda.stream(s):
+                        g.capture_end()
+                except Exception:  # noqa: BLE001 - an invalidated capture cannot end cleanly
+                    pass
+            self.cur.clear()
+            raise
         finally:
             _SEG = None
         return out
