@@ -585,6 +585,11 @@ TTDK_EXPORT int ttdk_row_scale(const void* a, const float* g, void* out, int dt,
 
 // zero a device buffer on the stream (the runtime's fill, not a framework elementwise kernel)
 TTDK_EXPORT int ttdk_zero(void* p, long long bytes, hipStream_t st) { return hipMemsetAsync(p, 0, bytes, st); }
+// Device-to-device copy on the stream (a runtime blit, capturable as a memcpy node): small
+// parameter-row gathers without a torch cat / copy kernel in the step.
+TTDK_EXPORT int ttdk_copy(void* dst, const void* src, long long bytes, hipStream_t st) {
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st);
+}
 
 TTDK_EXPORT int ttdk_trace_marker(int tag, hipStream_t st) {
   hipLaunchKernelGGL(trace_marker_kernel, dim3(1), dim3(64), 0, st, tag);

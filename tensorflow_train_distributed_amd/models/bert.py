@@ -393,7 +393,7 @@ class BertPretraining:
                                         P.var["cls/predictions/transform/LayerNorm/beta"], eps=eps)
         logits = G.gemm(t2, P.c["bert/embeddings/word_embeddings"], trans_b=True,
                         bias=P.var["cls/predictions/output_bias"])
-        sums = torch.zeros(4, dtype=torch.float32, device=dev)
+        sums = K.zeros(4, dtype=torch.float32, device=dev)  # own memset: no torch fill kernel in the step
         inv_cnt = torch.empty(1, dtype=torch.float32, device=dev)
         T.count_valid(labels, 1.0, inv_cnt)
         gsc = inv_cnt * loss_scale
@@ -433,7 +433,7 @@ class BertPretraining:
         K.colsum(dpp, out=g["bert/pooler/dense/bias"])
         dcls = G.gemm(dpp, P.c["bert/pooler/dense/kernel"])
         hook("bert/pooler/dense/bias")
-        dy = torch.zeros((Tk, H), dtype=bf, device=dev)
+        dy = K.zeros((Tk, H), dtype=bf, device=dev)
         T.scatter_rows(dhm, pos_idx, dy)
         T.scatter_rows(dcls, cls_idx, dy, accumulate=True)
 
@@ -500,7 +500,7 @@ class BertPretraining:
                                  site_out=1, rng=rng, work=ln_work)
         dpos = g["bert/embeddings/position_embeddings"]
         if S < dpos.shape[0]:
-            dpos[S:].zero_()
+            K.zero_(dpos[S:])
         T.embed_bwd(ds0, ids, tt, g["bert/embeddings/word_embeddings"], dpos, g["bert/embeddings/token_type_embeddings"],
                     B, S)
         hook("bert/embeddings/word_embeddings")

@@ -384,12 +384,13 @@ class ResNet:
         elif pro is not None and pro_big:
             # the producing unit's BN apply + residual + ReLU inside this conv's operand tile
             psc, psh, pres, pres_bn, side, side_mask = pro
-            if psh.data_ptr() == psc.data_ptr() + 4 * psc.numel():  # BNState rows scale, shift
+            if pres_bn is None and psh.data_ptr() == psc.data_ptr() + 4 * psc.numel():  # BNState rows scale, shift
                 coef = torch.as_strided(psc, (2, psc.numel()), (psc.numel(), 1))
             else:
-                coef = torch.stack([psc, psh])
-            if pres_bn is not None:
-                coef = torch.cat([coef.reshape(-1), pres_bn[0], pres_bn[1]])
+                # [scale | shift (| residual scale | residual shift)] by device copies (no torch kernel)
+                parts = [psc, psh] + ([pres_bn[0], pres_bn[1]] if pres_bn is not None else [])
+                coef = K.concat_(torch.empty(sum(t.numel() for t in parts), dtype=torch.float32, device=psc.device),
+                                 [t.contiguous() for t in parts])
             w4 = P.c[c.name + "_conv/kernel"]
             y, partial, T = G.conv_fwd_bnpro(x, w4, coef, pres, side, side_mask, proj=pres_bn is not None)
             x = side  # the unit's input as the backward needs it

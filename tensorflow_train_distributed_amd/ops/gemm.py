@@ -194,6 +194,15 @@ def gemm_wgrad_bias(dy, x, out, bias_out, splits=1, beta=0, alpha=1.0):
 _C3 = _os.environ.get("TTD_CONV3", "1") != "0"
 
 
+_lib.register({"ttdk_set_conv3_s3": [_lib.I]})
+
+
+def set_conv3_s3(on: bool) -> bool:
+    """Switch the stage-3 (28 x 28, 128 -> 128) streamed-filter halo conv on / off (TTD_CONV3_S3);
+    returns the previous setting. Takes effect for convs dispatched afterwards."""
+    return bool(_lib.query("ttdk_set_conv3_s3", 1 if on else 0))
+
+
 def conv3_rows(H, W, C, N, pro=0):
     """Output pixels per tile of the halo 3x3 kernel (conv3_halo.hip) for a [*, H, W, C] -> N
     3x3/s1/p1 conv with prologue `pro` (0 none, 1 BN forward, 2 BN backward), or 0 when the
@@ -225,7 +234,7 @@ def conv3_halo(x, w, *, prologue=None, flip=False, out=None, stat=False, bn_stat
         raise ValueError("conv3_halo: shape %s -> %d not compiled in" % (tuple(x.shape), Co))
     if out is None:
         out = torch.empty((Nimg, H, W, Co), dtype=torch.bfloat16, device=x.device)
-    T = Nimg * H * W // bm
+    T = -(-Nimg * H * W // bm)  # (the stage-3 variant's 8-row tiles may end in a partial one)
     partial = None
     by = bmask = None
     if stat or bn_stat is not None:

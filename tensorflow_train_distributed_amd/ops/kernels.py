@@ -640,7 +640,26 @@ def row_scale(a2d, g):
     return out
 
 
-_lib.register({"ttdk_zero": [_lib.P, _lib.L, _lib.P], "ttdk_trace_marker": [_lib.I, _lib.P]})
+_lib.register({"ttdk_zero": [_lib.P, _lib.L, _lib.P], "ttdk_trace_marker": [_lib.I, _lib.P],
+               "ttdk_copy": [_lib.P, _lib.P, _lib.L, _lib.P]})
+
+
+def concat_(out, parts):
+    """out = concatenation of the contiguous tensors `parts` (same dtype), by stream-ordered
+    device copies (no torch cat kernel in a captured step)."""
+    if not out.is_contiguous():
+        raise ValueError("concat_ needs a contiguous output")
+    o = 0
+    es = out.element_size()
+    for t in parts:
+        if t.dtype != out.dtype or not t.is_contiguous():
+            raise ValueError("concat_: parts must be contiguous %s" % out.dtype)
+        n = t.numel()
+        if o + n > out.numel():
+            raise ValueError("concat_: parts exceed the output")
+        _lib.call("ttdk_copy", out.data_ptr() + o * es, t.data_ptr(), n * es, _s())
+        o += n
+    return out
 
 
 def zero_(t):

@@ -436,7 +436,8 @@ def for_group(group=None, required: bool = False, overlap_ms=None, bucket_bytes=
     comm, reason = None, ""
     try:
         w = dist.get_world_size(group)
-        if w > 1 and "TTD_RCCL_MAX_CTAS" not in os.environ and os.environ.get("TTD_RCCL_PROBE", "1") == "1":
+        probe = os.environ.get("TTD_RCCL_PROBE", "1")  # "force": also on one rank (tests)
+        if (w > 1 or probe == "force") and "TTD_RCCL_MAX_CTAS" not in os.environ and probe in ("1", "force"):
             comm = _probe_budgets(group, overlap_ms, bucket_bytes)
         else:
             comm = RcclCommunicator.for_group(group)

@@ -104,3 +104,64 @@ def test_conv3_bn_backward_prologue_and_stat_epilogue():
     torch.testing.assert_close(side.float(), want_dz.float(), rtol=8e-3, atol=1e-5)
     assert _rel(out, ref) < 2e-2
     torch.testing.assert_close(part.sum(0), rpart.sum(0), rtol=2e-2, atol=2.0)
+
+
+# ---- stage-3 streamed-filter variant (28 x 28, 128 -> 128): tiles of 8 rows of the flattened
+# (image, row) sequence, so tiles straddle images and NIMG = 3 ends in a partial tile
+S3 = (3, 28, 28, 128, 128)
+
+
+@pytest.fixture
+def s3_on():
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    old = G.set_conv3_s3(True)
+    yield
+    G.set_conv3_s3(old)
+
+
+def test_conv3_stage3_streamed_forward_bn_prologue_and_stats(s3_on):
+    G, K = _ops()
+    nimg, h, w_, c, n = S3
+    assert G.conv3_rows(h, w_, c, n) == 8 * w_
+    y = _rand((nimg, h, w_, c), seed=11)
+    sc = torch.rand(c, device="cuda") + 0.5
+    sh = torch.randn(c, device="cuda") * 0.2
+    w = _rand((n, 3, 3, c), scale=(9 * c) ** -0.5, seed=12)
+    want = torch.empty_like(y)
+    want_mask = torch.zeros(y.numel() // 8, dtype=torch.uint8, device="cuda")
+    K.bn_apply(y.view(-1, c), sc, sh, relu=True, out=want.view(-1, c), mask=want_mask)
+    side = torch.empty_like(y)
+    side_mask = torch.zeros_like(want_mask)
+    out, partial, T = G.conv3_halo(y, w, prologue=("bn_fwd", sc, sh, side, side_mask), stat=True)
+    torch.cuda.synchronize()
+    assert T == -(-nimg * h // 8)
+    assert torch.equal(side, want) and torch.equal(side_mask, want_mask)
+    ref = _conv_ref(want, w)
+    assert _rel(out, ref) < 1e-2
+    o = out.float().reshape(-1, n)
+    torch.testing.assert_close(partial[:, 0].sum(0), o.sum(0), rtol=1e-3, atol=1e-1)
+    torch.testing.assert_close(partial[:, 1].sum(0), (o * o).sum(0), rtol=1e-3, atol=1e-1)
+    # plain forward on the same kernel family
+    out0 = G.conv3_halo(want, w)
+    torch.cuda.synchronize()
+    assert _rel(out0, ref) < 1e-2
+
+
+def test_conv3_stage3_streamed_dgrad_with_bn_stat_epilogue(s3_on):
+    G, K = _ops()
+    nimg, h, w_, c, n = S3
+    dz = _rand((nimg, h, w_, n), seed=13)
+    w = _rand((n, 3, 3, c), scale=(9 * c) ** -0.5, seed=14)
+    wt = K.krsc_to_crsk(w)
+    oracle = F.conv_transpose2d(dz.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1)
+    got = G.conv3_halo(dz, wt, flip=True)
+    torch.cuda.synchronize()
+    assert _rel(got, oracle.permute(0, 2, 3, 1)) < 1e-2
+    M = nimg * h * w_
+    fy = _rand((nimg, h, w_, c), seed=15)
+    fmask = torch.randint(0, 256, (M * c // 8,), dtype=torch.uint8, device="cuda")
+    ref, rpart, _ = G.conv_dgrad(dz, wt, (nimg, h, w_, c), (1, 1), (1, 1), bn_stat=(fy, fmask))
+    out, part, T = G.conv3_halo(dz, wt, flip=True, bn_stat=(fy, fmask))
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 2e-2
+    torch.testing.assert_close(part.sum(0), rpart.sum(0), rtol=2e-2, atol=2.0)

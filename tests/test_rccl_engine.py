@@ -262,3 +262,40 @@ def test_segmented_capture_with_bucket_launches_matches_eager():
         from tensorflow_train_distributed_amd.parallel import rccl
         rccl.abort_all()
         dist.destroy_process_group()
+
+
+def test_cta_budget_probe_path_on_one_rank(monkeypatch):
+    """The start-up CTA-budget probe (rccl._probe_budgets) end to end on a one-rank RCCL group
+    (TTD_RCCL_PROBE=force): two communicators (capped / RCCL default) created and probed, the
+    slowest-rank table agreed over the process group, the policy's choice kept (the other
+    communicator finalized), the reducer reporting it."""
+    import torch.distributed as dist
+    from tensorflow_train_distributed_amd.parallel import rccl
+    from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer
+    from tensorflow_train_distributed_amd.train.flat import FlatParams, ParamSpec
+    monkeypatch.setenv("TTD_RCCL_PROBE", "force")
+    monkeypatch.delenv("TTD_RCCL_MAX_CTAS", raising=False)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        specs = [ParamSpec("v%d" % i, (n,), None, True) for i, n in enumerate([300000, 5000, 900000])]
+        p = FlatParams(specs, dev, compute_dtype=None)
+        red = BucketedAllReducer(p, bucket_mb=1.0, first_bucket_mb=0.5, engine="native", overlap_ms=40.0)
+        pol = red.policy()
+        assert pol is not None and pol["cta_budget"] in (0, rccl.DEFAULT_MAX_CTAS), pol
+        assert set(pol["probe"]) == {rccl.DEFAULT_MAX_CTAS, 0}
+        for rows in pol["probe"].values():
+            assert [r["bytes"] for r in rows] == list(rccl.PROBE_BYTES) and all(r["ms"] > 0 for r in rows)
+        assert red.comm.max_ctas == pol["cta_budget"]
+        # the kept communicator works
+        local = torch.randn(p.numel, device=dev) * p.valid_mask().to(dev)
+        p.grad.copy_(local)
+        red.begin()
+        for s in specs:
+            red.mark_ready(s.name)
+        red.finish()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(p.grad, local, rtol=0, atol=0)
+    finally:
+        rccl.abort_all()
+        dist.destroy_process_group()
