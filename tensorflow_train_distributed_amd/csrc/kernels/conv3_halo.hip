@@ -577,7 +577,7 @@ using namespace ttdk;
 // [*, H, W, C] -> N 3x3/s1/p1 conv, or 0 when the shape is not compiled in.
 namespace {
 int& conv3_s3_flag() {
-  static int on = getenv_int("TTD_CONV3_S3", 0);  // stage-3 streamed-filter variant (1: on)
+  static int on = getenv_int("TTD_CONV3_S3", 1);  // stage-3 streamed-filter variant (0: off)
   return on;
 }
 }  // namespace
