@@ -1580,13 +1580,18 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
       barrier();
       if (lag) barrier();
     }
+    // RS turn counter: K-tile kt is this workgroup's when (kt - kt0) % tiles_n == tile_n, kept as
+    // a wave-uniform cycling counter (a run-time modulo is VALU work: it made the condition
+    // divergent and the row-sum code ran exec-masked on every K-tile)
+    int rs_cnt = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool has1 = kt + 1 < kt1, has2 = kt + 2 < kt1;
       char* cb = buf(kt);
       // P0: (A0, B0)
       read_a(cb + A0, fa[0]);
       read_b(cb + B0, fb[0]);
-      const bool rs_on = RS && ((kt - kt0) % rs_nt) == rs_tn;
+      const bool rs_on = RS && __builtin_amdgcn_readfirstlane(rs_cnt == rs_tn ? 1 : 0) != 0;
+      if constexpr (RS) rs_cnt = rs_cnt + 1 == rs_nt ? 0 : rs_cnt + 1;
       if (rs_on) rs_half(cb + A0, 0);
       if (has1) la.template issue<1>(buf(kt + 1) + A1, kt + 1, wave);
       barrier();
