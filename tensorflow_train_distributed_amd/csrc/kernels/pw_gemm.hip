@@ -651,7 +651,8 @@ TTDK_EXPORT int ttdk_pw_conv(const bf16_t* x, const bf16_t* x2, const uint8_t* m
 // ttdk_pw_conv with pro = 2 (BN backward as the operand prologue) and the conv's weight gradient
 // fused in (see pw_kernel WG): dx = epilogue(dz . w^T) as ttdk_pw_conv, dw[K][N] (fp32, += when
 // beta_w) = dz^T . xw with dz never stored; ws: ttdk_pw_wgrad_slabs(M, N, K, dma, max_wgs) * K * N
-// floats.
+// floats. dw == null: the slabs are left in ws for the caller to fold (ttdk_splitk_reduce), e.g. on
+// the weight-gradient side stream so the data-gradient chain does not wait for the fold.
 TTDK_EXPORT int ttdk_pw_conv_wgrad(const bf16_t* g, const bf16_t* y, const uint8_t* mask_in, const float* coef,
                                    const bf16_t* xw, const bf16_t* w, long long ldw, int M, int N, int K,
                                    const TtdkEpilogue* epi, float* dw, float* ws, int beta_w, int max_wgs,
@@ -659,11 +660,11 @@ TTDK_EXPORT int ttdk_pw_conv_wgrad(const bf16_t* g, const bf16_t* y, const uint8
   const EpiParams e = to_epi(epi);
   const bool dma = (e.beta || e.by) && !e.residual && !e.by2 && e.act == 0 && !e.bias;
   const int slabs = ttdk_pw_wgrad_slabs(M, N, K, dma, max_wgs);
-  if (!slabs || !g || !y || !coef || !xw || !dw || !ws || ldw % 8 || (reinterpret_cast<uintptr_t>(g) & 15) ||
+  if (!slabs || !g || !y || !coef || !xw || !ws || ldw % 8 || (reinterpret_cast<uintptr_t>(g) & 15) ||
       (reinterpret_cast<uintptr_t>(xw) & 15) || e.mode != 0 || e.remap || e.ldo % 8 || (e.residual && e.ldr % 8))
     return hipErrorInvalidValue;
   const pw::Pro pa{g, y, mask_in, coef, nullptr, nullptr, nullptr, nullptr, nullptr, 1, xw, ws};
   hipError_t r = pw::dispatch_wg(pa, w, ldw, e, M, N, K, dma, slabs, st);
-  if (r != hipSuccess) return r;
+  if (r != hipSuccess || !dw) return r;
   return splitk_reduce(ws, slabs, static_cast<long long>(K) * N, dw, beta_w, st);
 }

@@ -135,6 +135,7 @@ class ResNet:
         # form their conv's weight gradient from the dz tile in LDS (pw_gemm.hip WG); 0: separate
         # side-stream weight-gradient pass over a stored dz
         self.pw_wgrad = os.environ.get("TTD_PW_WGRAD", "1") != "0"
+        self.pw_fold_side = os.environ.get("TTD_PW_FOLD_SIDE", "1") != "0"
         # cap on the persistent workgroups of that kernel when it runs on the side stream (the
         # stage-2 projection; 0 = one per CU). It holds every CU while it runs, but the main chain
         # joins on it right after: 128 / 64 measured 0.3 / 2.1 ms slower per step than the full grid
@@ -497,7 +498,8 @@ class ResNet:
                                       dstat[0], dstat[1])
             wt2 = self._crsk(wname).view(c.cin_store, c.cout)
             out = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None), out=dx,
-                            beta=dx_beta if dx is not None else 0, wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
+                            beta=dx_beta if dx is not None else 0, wgrad=(x, P.g[wname].view(c.cout, c.cin_store)),
+                            fold_stream=self._fold_stream(), keep=self._side_keep)
             self._ready_main(c.name + "_bn/moving_variance")
             return out, None
         if (need_dx and dstat is not None and feeds is not None and feeds2 is None
@@ -514,7 +516,8 @@ class ResNet:
                 # never stored, the side-stream pass re-reading dz and x disappears
                 out, partial, T = G.pw_conv(dout, wt2, prologue=("bn_bwd", y, None, coef, None), bn_stat=(fy, fmask),
                                             out=dx, beta=dx_beta if dx is not None else 0, beta_s2=bs2,
-                                            wgrad=(x, P.g[wname].view(c.cout, c.cin_store)))
+                                            wgrad=(x, P.g[wname].view(c.cout, c.cin_store)),
+                                            fold_stream=self._fold_stream(), keep=self._side_keep)
                 self._ready_main(c.name + "_bn/moving_variance")
                 return out, (partial, T)
             dz = torch.empty_like(y)
@@ -700,6 +703,16 @@ class ResNet:
             G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
             if ready:
                 self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
+
+    def _fold_stream(self):
+        """Stream for the slab fold of a main-stream fused weight gradient (pw_conv wgrad=): the
+        side stream, unless disabled (TTD_PW_FOLD_SIDE=0) or already the current stream. On the
+        main stream the fold waited ~1 ms per launch for CUs held by the side stream's weight
+        gradients (profiles/r4_resnet50_b1024_step_streams_graph.txt)."""
+        side = self._wgrad_stream
+        if side is None or not self.pw_fold_side or torch.cuda.current_stream() == side:
+            return None
+        return side
 
     def _ready(self, name):
         if self._grad_hook is not None:

@@ -343,7 +343,7 @@ def pw_wgrad_fusable(M, N, K, dma=True):
 
 
 def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None, bn_stat=None, bn_stat2=None,
-            beta_s2=None, wgrad=None, max_wgs=0):
+            beta_s2=None, wgrad=None, max_wgs=0, fold_stream=None, keep=None):
     """Unit-stride 1x1 conv / dense GEMM out[M, N] = A'[M, K] . w[N, K]^T on the persistent
     streaming kernel (pw_gemm.hip), A' = prologue(x):
 
@@ -361,7 +361,10 @@ def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None,
     wgrad=(xw, dw[, beta_w]) with the "bn_bwd" prologue (its side None): the same conv's weight
     gradient dw[K, N] (fp32; += when beta_w) = dz^T . xw is formed in the kernel from the dz tile
     in LDS (dz is never stored); xw: the conv input, bf16 [..., N] (pw_gemm.hip pw_kernel WG).
-    max_wgs > 0 caps its persistent grid (launches on a side stream next to the main chain)."""
+    max_wgs > 0 caps its persistent grid (launches on a side stream next to the main chain).
+    fold_stream: fold the per-workgroup dw slabs on that stream (after a fork from the current
+    one) instead of behind the kernel, so the data-gradient chain does not wait for the fold;
+    the slab buffer is appended to `keep`, which must stay referenced until that stream joins."""
     _check(x, torch.bfloat16, "x")
     _check(w, torch.bfloat16, "w")
     K = x.shape[-1]
@@ -414,7 +417,16 @@ def pw_conv(x, w, *, prologue=None, out=None, stat=False, beta=0, residual=None,
         _log("pw_wgrad", K, N, M)
         ws = torch.empty(slabs * K * N, dtype=torch.float32, device=x.device)
         _lib.call("ttdk_pw_conv_wgrad", x.data_ptr(), P(x2), P(mask_in), P(s), xw.data_ptr(), w.data_ptr(), K, M, N,
-                  K, ctypes.byref(e), dw.data_ptr(), ws.data_ptr(), beta_w, int(max_wgs), _lib.stream())
+                  K, ctypes.byref(e), None if fold_stream is not None else dw.data_ptr(), ws.data_ptr(), beta_w,
+                  int(max_wgs), _lib.stream())
+        if fold_stream is not None:
+            # slab fold on the given (side) stream: the caller keeps ws alive until that stream joins
+            from ..utils import graphs
+            graphs.fork(torch.cuda.current_stream(), fold_stream)
+            with torch.cuda.stream(fold_stream):
+                _lib.call("ttdk_splitk_reduce", ws.data_ptr(), slabs, K * N, dw.data_ptr(), beta_w, _lib.stream())
+            if keep is not None:
+                keep.append(ws)
         if partial is None:
             return out
         if partial2 is not None:

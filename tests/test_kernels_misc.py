@@ -343,3 +343,13 @@ def test_bf16_rounding_matches_torch_bitwise():
     # the GPU's own torch conversion agrees too (what torch-side reference code computes on device)
     dev_ref = x_cpu.cuda().to(torch.bfloat16).view(torch.int16).cpu()
     assert int(((dev_ref != ref) & ~isnan).sum()) == 0
+
+
+@pytest.mark.parametrize("A,B,C", [(1024, 1, 4096), (4096, 1, 1024), (1000, 1, 24), (13, 1, 40), (64, 9, 128)])
+def test_weight_transpose_matches_torch(A, B, C):
+    """[A][B][C] -> [C][B][A] bf16: the 8 x 8 register-block kernel (B == 1, multiples of 8) and
+    the LDS-tile kernel (everything else) against torch's permute, bit for bit."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    w = torch.randn(A, 1, B, C, device="cuda").to(torch.bfloat16)
+    out = K.krsc_to_crsk(w)
+    assert torch.equal(out.view(C, B, A), w.view(A, B, C).permute(2, 1, 0))
