@@ -1068,6 +1068,25 @@ __device__ __forceinline__ void glds(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(lds), 16, 0, 0);
 }
 
+// The same DMA as inline asm, for the MN-major operand policies: the compiler tracks the builtin
+// as an LDS write it cannot disambiguate from the ds_read_b64_tr_b16 fragment reads, so every
+// MN-major main loop got an s_waitcnt vmcnt(0) in front of its first transposed read — a full
+// drain of the K-tile + 2 prefetch on every K-tile. Untracked, these pieces are retired only by
+// the kernel's own counted waits (in-order vmcnt retirement: the compiler's waits for its own
+// loads can only get stronger from extra outstanding pieces, never weaker). M0 is saved and
+// restored. A kernel gains only if none of its operands uses the builtin.
+__device__ __forceinline__ void glds_u(const void* src, char* lds) {
+#ifdef TTD_GLDS_BUILTIN  // A/B builds only (tools/build_alt_lib.py --flags=-DTTD_GLDS_BUILTIN)
+  glds(src, lds);
+  return;
+#endif
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<size_t>((lds_void_t*)(lds))));
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l));
+}
+
 struct DenseP {
   const void* p;
   long long ld;   // elements
@@ -1134,7 +1153,7 @@ struct OpDenseMN {
   template <int H>
   __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
 #pragma unroll
-    for (int i = 0; i < G; ++i) glds(src[H][i] + kt * kstep, lds + (i * T + wave * 64) * 16);
+    for (int i = 0; i < G; ++i) glds_u(src[H][i] + kt * kstep, lds + (i * T + wave * 64) * 16);
   }
 };
 
@@ -1251,7 +1270,7 @@ struct OpWgradMN {
       const bool v = cok[HH][i] && hh >= 0 && ww >= 0 && hh < H && ww < W;
       const char* s = v ? x + ((static_cast<long long>(n * H + hh) * W + ww) * C + cc[HH][i]) * 2
                         : reinterpret_cast<const char*>(g_zero);
-      glds(s, lds + (i * T + wave * 64) * 16);
+      glds_u(s, lds + (i * T + wave * 64) * 16);
     }
   }
 };

@@ -319,18 +319,30 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int* __restrict__ 
   }
 }
 
-// dword[ids[row]] += ds[row]  (fp32 atomics; rows of distinct tokens rarely collide)
+// dword[ids[row]] += ds[row]  (fp32 atomics; rows of distinct tokens rarely collide). Lane l of
+// a wave adds column c0 + l: every atomic instruction covers 256 contiguous bytes of one row.
+// (Lane-owns-8-columns, as the loads would like, put each instruction's 64 lanes on 64
+// different 32-B pieces: 2.1 ms for BERT-Large b128's 65536 x 1024 rows.)
 __global__ __launch_bounds__(256) void embed_bwd_word_kernel(const bf16_t* __restrict__ ds, const int* __restrict__ ids,
                                                              float* __restrict__ dword, long long rows, int H) {
   const long long row = static_cast<long long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
   const long long id = ids[row];
-  for (int c = lane * 8; c < H; c += 512) {
+  const unsigned short* src = reinterpret_cast<const unsigned short*>(ds) + row * H;
+  float* dst = dword + id * H;
+  for (int c0 = 0; c0 < H; c0 += 512) {
     float a[8];
-    unpack8(ldg16(ds + row * H + c), a);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(dword + id * H + c + j, a[j]);
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j * 64 + lane;
+      a[j] = c < H ? __uint_as_float(static_cast<uint32_t>(src[c]) << 16) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j * 64 + lane;
+      if (c < H) atomicAdd(dst + c, a[j]);
+    }
   }
 }
 
