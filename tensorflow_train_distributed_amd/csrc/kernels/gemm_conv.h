@@ -1128,6 +1128,20 @@ struct OpDenseK {
   }
 };
 
+// K-major dense operand whose DMA is the untracked asm form (glds_u): for kernels whose other
+// operand is MN-major, so no tracked LDS-DMA is left to force vmcnt(0) drains in front of the
+// transposed fragment reads (the K-major x K-major kernels keep the builtin: there the compiler
+// inserts no such waits, and the asm form's 64-bit address pairs spilled the persistent kernel)
+template <int HROWS, int ESZ, int T = THR>
+struct OpDenseKU : OpDenseK<HROWS, ESZ, T> {
+  template <int H>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < OpDenseK<HROWS, ESZ, T>::G; ++i)
+      glds_u(this->src[H][i] + static_cast<long long>(kt) * 128, lds + (i * T + wave * 64) * 16);
+  }
+};
+
 // ---- dense MN-major (bf16): half = HROWS cols x 64 k
 template <int HROWS, int T = THR>
 struct OpDenseMN {
@@ -2337,8 +2351,8 @@ hipError_t dense_pp(const bf16_t* A, long long lda, bool ak, const bf16_t* B, lo
   DenseP pa{A, lda, M}, pb{B, ldb, N};
   constexpr int BH = BN / 2;
   if (ak && bk) return launch<BN, OpDenseK<128, 2>, OpDenseK<BH, 2>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
-  if (ak) return launch<BN, OpDenseK<128, 2>, OpDenseMN<BH>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
-  if (bk) return launch<BN, OpDenseMN<128>, OpDenseK<BH, 2>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
+  if (ak) return launch<BN, OpDenseKU<128, 2>, OpDenseMN<BH>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
+  if (bk) return launch<BN, OpDenseMN<128>, OpDenseKU<BH, 2>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
   return launch<BN, OpDenseMN<128>, OpDenseMN<BH>, 0, PP>(pa, pb, pe, M, N, K, splits, st);
 }
 

@@ -581,7 +581,17 @@ TTDK_EXPORT int ttdk_ln_fwd(const bf16_t* x, const bf16_t* res, bf16_t* s_out, b
   return hipGetLastError();
 }
 
-TTDK_EXPORT int ttdk_ln_bwd_num_blocks(int rows) { return rows < 256 * 16 ? (rows + 15) / 16 : 256; }
+// Blocks of ln_bwd_kernel (= partial rows of the workspace): one 8-wave block per CU. Two per CU
+// (4 waves per SIMD at the H = 1024 kernel's 120 VGPRs) measured the same standalone (146 vs 147
+// us at 65536 x 1024) and in the BERT step, four slower (TTD_LN_BWD_BLOCKS: A/B).
+TTDK_EXPORT int ttdk_ln_bwd_num_blocks(int rows) {
+  static const int cap = [] {
+    const char* e = getenv("TTD_LN_BWD_BLOCKS");
+    const int v = e ? atoi(e) : 256;
+    return v > 0 ? v : 256;
+  }();
+  return rows < cap * 16 ? (rows + 15) / 16 : cap;
+}
 
 // part: fp32 [nblocks][2][H] workspace; dgamma/dbeta written (beta=0) or accumulated.
 TTDK_EXPORT int ttdk_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean, const float* rstd,
