@@ -94,3 +94,48 @@ TTDK_EXPORT int ttdk_conv_wgrad_bn(const bf16_t* x, const bf16_t* g, const bf16_
   if (e != hipSuccess || splits == 1) return e;
   return splitk_reduce(ws, splits, static_cast<long long>(M) * N, dw, beta, st);
 }
+
+// fp8 weight gradient: dw[K,R,S,C] (fp32) = sum over pixels of dy8 (x) im2col(x8), dy8 OCP e5m2 and
+// x8 e4m3 (both NHWC bytes: the e5m2 copy of the BN-backward output that the fp8 data gradient
+// already consumes, and the e4m3 copy of the conv input that the fp8 forward consumed), both
+// MN-major in the 256-row kernel (OpDenseMN8 / OpWgradMN8, ds_read_b64_tr_b8 fragments) on the
+// block-scaled fp8 MFMA at twice the bf16 rate; ascale_dy / ascale_x: the inverse quantisation
+// scales (device fp32), folded into the fp32 output. Requires C, K % 16 == 0, pixels % 128 == 0,
+// 9C >= 256 (K < 256 output channels leave part of the 256-row tile idle).
+TTDK_EXPORT int ttdk_conv_wgrad_fp8(const uint8_t* x8, const uint8_t* dy8, const TtdkConv* g, float* dw, float* ws,
+                                    int splits, int beta, const float* ascale_dy, const float* ascale_x,
+                                    hipStream_t st) {
+  const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
+  if (g->C % 16 || g->K % 16 || K % 128 || N < 256 || M < 16 || !ascale_dy || !ascale_x ||
+      static_cast<long long>(g->N) * g->H * g->W * g->C >= (1LL << 32) ||  // 32-bit im2col offsets
+      (reinterpret_cast<uintptr_t>(x8) & 15) || (reinterpret_cast<uintptr_t>(dy8) & 15))
+    return hipErrorInvalidValue;
+  const int ktiles = K / 128;
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles;
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  if (splits > 1 && !ws) return hipErrorInvalidValue;
+  EpiParams pe{};
+  pe.alpha = 1.f;
+  pe.ascale0 = ascale_dy;
+  pe.ascale1 = ascale_x;
+  pe.ldo = N;
+  if (splits > 1) {
+    pe.mode = 1;
+    pe.out = ws;
+    pe.slab_stride = static_cast<long long>(M) * N;
+  } else {
+    pe.mode = 2;
+    pe.out = dw;
+    pe.beta = beta;
+  }
+  const big::DenseP pa{dy8, g->K, M};
+  const big::ConvP pb = conv_params(x8, g->H, g->W, g->C, g->P, g->Q, g, N);
+  // 256 x 128 tiles: with 256-wide tiles the i32x8 fragments and 128 accumulators held the whole
+  // register file and the loader state spilled inside the main loop (each reload a vmcnt(0)
+  // drain of the LDS-DMA pipeline)
+  hipError_t e = big::launch<128, big::OpDenseMN8<128>, big::OpWgradMN8<64>, 2>(pa, pb, pe, M, N, K, splits, st);
+  if (e != hipSuccess || splits == 1) return e;
+  return splitk_reduce(ws, splits, static_cast<long long>(M) * N, dw, beta, st);
+}

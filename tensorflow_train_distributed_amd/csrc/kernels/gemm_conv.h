@@ -1289,6 +1289,111 @@ struct OpWgradMN {
   }
 };
 
+// ---- fp8 MN-major operands (the fp8 weight gradient: k = pixel, column = output channel or
+// im2col column (r, s, c); OCP e4m3 / e5m2 bytes). Half = 128 columns x 128 k (one byte each),
+// the same 16 KB as a bf16 half: k-row r holds its 128 columns as 8 16-B slots, slot j stored
+// at j ^ mn8_swz(r), so the 16 k-rows one ds_read_b64_tr_b8 of a 32-lane group touches land on
+// 16 distinct 4-bank groups (rows alternate bank halves; within a half the 8 rows of one parity
+// take slots m | 4g for m = (r >> 1) & 3 and the lane group g = bit 5 of r).
+// HROWS = 64 (the B half of a 256 x 128 tile): k-rows of 64 B (4 slots); a 32-lane read covers
+// 4 bank quarters (r & 3), and the 4 rows of one quarter take slots (bit 2 of r) | (g << 1).
+template <int HROWS>
+__device__ __forceinline__ int mn8_swz(int k) {
+  if constexpr (HROWS == 128)
+    return ((k >> 1) & 3) | ((k >> 3) & 4);
+  else
+    return ((k >> 2) & 1) | ((k >> 4) & 2);
+}
+template <int HROWS>
+__device__ __forceinline__ int mn8_off(int k, int col) {
+  return k * HROWS + (((col >> 4) ^ mn8_swz<HROWS>(k)) << 4) + (col & 15);
+}
+
+template <int HROWS, int T = THR>
+struct OpDenseMN8 {  // element (k, row) at p[k * ld + row] (bytes); ld % 16 == 0, rows % 16 == 0
+  static_assert(HROWS == 128 || HROWS == 64, "fp8 MN-major halves are 128 or 64 columns");
+  static constexpr int SPR = HROWS / 16;  // 16-B slots per k-row
+  using Params = DenseP;
+  static constexpr int THREADS = T;
+  static constexpr int G = HROWS * 8 / T;
+  // 32-bit piece offsets from the uniform base (k < 128 rows of ld <= 2^24 bytes): 64-bit
+  // pointers per piece were reloaded from scratch inside the fp8 main loop
+  const char* base;
+  int off[2][G];
+  long long kstep;
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    base = static_cast<const char*>(P.p);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int q = i * T + tid;
+        const int k = q / SPR, j = q % SPR;
+        const int c = min(row0 + h * HROWS + ((j ^ mn8_swz<HROWS>(k)) << 4), P.rows - 16);
+        off[h][i] = k * static_cast<int>(P.ld) + c;
+      }
+    kstep = 128 * P.ld;
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+    const char* b = base + kt * kstep;
+#pragma unroll
+    for (int i = 0; i < G; ++i) glds_u(b + off[H][i], lds + (i * T + wave * 64) * 16);
+  }
+};
+
+// fp8 im2col columns of the weight gradient (as OpWgradMN; C % 16 == 0 so a 16-column slot stays
+// inside one filter tap)
+template <int HROWS, int T = THR>
+struct OpWgradMN8 {
+  static_assert(HROWS == 128 || HROWS == 64, "fp8 MN-major halves are 128 or 64 columns");
+  static constexpr int SPR = HROWS / 16;
+  using Params = ConvP;
+  static constexpr int THREADS = T;
+  static constexpr int G = HROWS * 8 / T;
+  const char* x;
+  int H, W, C, pq, Q, sh, sw;
+  // per piece, packed (the unpacked five arrays spilled inside the fp8 main loop, whose i32x8
+  // fragments already hold the register file at 256): kc = k | c << 7 (k < 128 pixels of the
+  // K-tile, c the channel), rs = (roff + 64) | (soff + 64) << 8 | valid-column << 16
+  int kc[2][G], rs[2][G];
+  __device__ __forceinline__ void init(const Params& P, int row0, int tid) {
+    x = static_cast<const char*>(P.x);
+    H = P.Hs; W = P.Ws; C = P.Cs; pq = P.P * P.Q; Q = P.Q; sh = P.sh; sw = P.sw;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int q = i * T + tid;
+        const int k = q / SPR, j = q % SPR;
+        const int col = row0 + h * HROWS + ((j ^ mn8_swz<HROWS>(k)) << 4);
+        const bool ok = col < P.rows;
+        const int cl = ok ? col : 0;
+        const int tap = cl / C, c = cl - tap * C;
+        const int rr = tap / P.S, ss = tap - rr * P.S;
+        kc[h][i] = k | (c << 7);
+        rs[h][i] = (rr * P.dh - P.ph + 64) | ((ss * P.dw - P.pw + 64) << 8) | (ok ? 1 << 16 : 0);
+      }
+  }
+  template <int HH>
+  __device__ __forceinline__ void issue(char* lds, int kt, int wave) const {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int k = kt * 128 + (kc[HH][i] & 127);
+      const int n = k / pq, rem = k - n * pq;
+      const int p = rem / Q, qq = rem - p * Q;
+      const int hh = p * sh + (rs[HH][i] & 255) - 64, ww = qq * sw + ((rs[HH][i] >> 8) & 255) - 64;
+      const bool v = (rs[HH][i] >> 16) && hh >= 0 && ww >= 0 && hh < H && ww < W;
+      // one 32-bit byte offset (the host keeps x8 under 4 GiB): as a 64-bit x + c hoisted per
+      // piece, the address pairs were spilled inside the main loop
+      const uint32_t o = static_cast<uint32_t>((n * H + hh) * W + ww) * static_cast<uint32_t>(C) +
+                         static_cast<uint32_t>(kc[HH][i] >> 7);
+      const char* s = v ? x + o : reinterpret_cast<const char*>(g_zero);
+      glds_u(s, lds + (i * T + wave * 64) * 16);
+    }
+  }
+};
+
 // dense K-major A operand whose tile gets a BN operand prologue (EpiParams::py/pcoef/pdz/pmask):
 // MODE 1 BN backward apply, 2 BN forward apply + residual + ReLU, 3 the same with the residual's
 // own BN (projection shortcut)
@@ -1315,6 +1420,16 @@ struct Traits<OpWgradMN<HR, T>> {
   static constexpr bool kmaj = false;
   static constexpr int bnpro = 0;
 };
+template <int HR, int T>
+struct Traits<OpDenseMN8<HR, T>> {
+  static constexpr bool kmaj = false;
+  static constexpr int bnpro = 0;
+};
+template <int HR, int T>
+struct Traits<OpWgradMN8<HR, T>> {
+  static constexpr bool kmaj = false;
+  static constexpr int bnpro = 0;
+};
 
 // fragment readers
 __device__ __forceinline__ bf16x8_t frag_k(const char* lds, int base, int ks, int lane) {
@@ -1331,6 +1446,27 @@ __device__ __forceinline__ i32x8_t frag_k8(const char* lds, int base, int lane) 
 template <int HROWS>
 __device__ __forceinline__ bf16x8_t frag_mn(const char* lds, int colbase, int ks, int lane) {
   return mn_frag<HROWS>(lds, colbase, ks, lane);
+}
+// fp8 MN-major fragment of v_mfma_scale_f32_16x16x128_f8f6f4: lane (i = lane & 15, g = lane >> 4)
+// gets column colbase + i, k = 32 g .. 32 g + 31, as four ds_read_b64_tr_b8 (measured on gfx950,
+// tools/probe/tr8_probe.hip: within a 16-lane group, lane l receives byte l % 8 of the 8-byte
+// pieces addressed by lanes 2j + (l >= 8), j = 0..7; so lane i addresses k-row k0 + i / 2 at
+// column colbase + 8 (i & 1), and every lane ends up with 8 consecutive k of its own column).
+template <int HROWS>
+__device__ __forceinline__ i32x8_t frag_mn8(const char* lds, int colbase, int lane) {
+  typedef __attribute__((ext_vector_type(2))) int i32x2_t;
+  typedef __attribute__((address_space(3))) i32x2_t lds_i32x2_t;
+  const int i = lane & 15, g = lane >> 4;
+  const int col = colbase + 8 * (i & 1);
+  i32x8_t v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 32 * g + 8 * q + (i >> 1);
+    const i32x2_t r = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_i32x2_t*)(lds + mn8_off<HROWS>(k, col)));
+    v[2 * q] = r[0];
+    v[2 * q + 1] = r[1];
+  }
+  return v;
 }
 
 template <int N>
@@ -1462,7 +1598,7 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
   static_assert(OB::THREADS == T && (NW == 8 || NW == 4), "operand policies must agree on the block size");
   constexpr int BNH = Gm::BNH, WC = BNH / WN, NB = WC / 16, GA = OA::G, GB = OB::G;
   constexpr bool AK = Traits<OA>::kmaj, BKM = Traits<OB>::kmaj;
-  static_assert(F8 == 0 || (AK && BKM), "fp8 operands must be K-major");
+  static_assert(F8 == 0 || AK == BKM, "fp8 operands: both K-major or both MN-major (OpDenseMN8 / OpWgradMN8)");
   __shared__ __attribute__((aligned(16))) char smem[Gm::SMEM];
   // RS: A-operand row sums (EpiParams::rsum). MN-major A only, PP schedule, fp32 slab / store
   // epilogues (the per-wave sum slots [NW][256] fp32 sit after the coefficient area, inside the
@@ -1512,7 +1648,8 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        if constexpr (F8 != 0) f[ks][a] = frag_k8(sA, wm * 64 + a * 16, lane);
+        if constexpr (F8 != 0 && AK) f[ks][a] = frag_k8(sA, wm * 64 + a * 16, lane);
+        else if constexpr (F8 != 0) f[ks][a] = frag_mn8<128>(sA, wm * 64 + a * 16, lane);
         else if constexpr (AK) f[ks][a] = frag_k(sA, wm * 64 + a * 16, ks, lane);
         else f[ks][a] = frag_mn<128>(sA, wm * 64 + a * 16, ks, lane);
       }
@@ -1522,7 +1659,8 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256_kernel(typename OA::Pa
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        if constexpr (F8 != 0) f[ks][b] = frag_k8(sB, wn * WC + b * 16, lane);
+        if constexpr (F8 != 0 && BKM) f[ks][b] = frag_k8(sB, wn * WC + b * 16, lane);
+        else if constexpr (F8 != 0) f[ks][b] = frag_mn8<BNH>(sB, wn * WC + b * 16, lane);
         else if constexpr (BKM) f[ks][b] = frag_k(sB, wn * WC + b * 16, ks, lane);
         else f[ks][b] = frag_mn<BNH>(sB, wn * WC + b * 16, ks, lane);
       }

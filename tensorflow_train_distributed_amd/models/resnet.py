@@ -104,6 +104,10 @@ class ResNet:
         # precision="fp8": unit-stride 3x3 data gradients on the fp8 MFMA with e5m2 gradients
         # (TTD_FP8_DGRAD=0: bf16 data gradients)
         self.fp8_dgrad = os.environ.get("TTD_FP8_DGRAD", "1") != "0"
+        # fp8 weight gradients of the convs that have both fp8 copies already (the e4m3 input of the
+        # fp8 forward and the e5m2 dz of the fp8 data gradient): ops.gemm.conv_wgrad_fp8
+        self.fp8_wgrad = os.environ.get("TTD_FP8_WGRAD", "1") != "0"
+        self._x8 = {}
         # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
         # never stored: two HBM passes of the stage's largest tensor saved; TTD_FUSE_PROJ=0: off)
         self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
@@ -408,6 +412,7 @@ class ResNet:
         elif use8:
             partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
             xq, xslot = x8
+            self._x8[c.name] = x8  # the fp8 weight gradient reuses the quantised input
             ws = self._w8_slots[self._w8_slot[c.name]]
             y = G.conv_fwd_fp8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
                                ascale=(xslot[3:4], ws[3:4]))
@@ -567,6 +572,7 @@ class ResNet:
             self._wgrad(c, x, dz, wname)
             return out, None
         dz8 = None
+        wgrad_done = False
         if dstat is not None:
             g8 = (self._fp8 is not None and need_dx and c.name in self._g8 and self._wp_cur is not None
                   and feeds is not None and feeds2 is None and dx is None)
@@ -577,11 +583,17 @@ class ResNet:
                                             ).view(N, Pp, Q, Kc)
             if g8 and self._fp8_bwd_steps >= 1:  # (step 0 only collects the gradient amax)
                 dz8 = q8.view(N, Pp, Q, Kc)
+                x8 = self._x8.get(c.name)
+                if (self.fp8_wgrad and x8 is not None and not wgrad_last
+                        and G.conv_wgrad_fp8_ok(tuple(x.shape), tuple(P.var[wname].shape), (c.stride, c.stride),
+                                                (c.pad, c.pad))):
+                    self._wgrad(c, x, dz, wname, fp8=(x8, dz8, self._g_slots[self._g8[c.name]]))
+                    wgrad_done = True
         else:
             dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
                                P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
                                mask=mask).view(N, Pp, Q, Kc)
-        if not wgrad_last:
+        if not wgrad_last and not wgrad_done:
             self._wgrad(c, x, dz, wname)
         if not need_dx:
             return None, None
@@ -681,28 +693,37 @@ class ResNet:
             return wp.phases(wname + "/phases")
         return None
 
-    def _wgrad(self, c: ConvSpec, x, dz, wname, ready=True):
+    def _wgrad(self, c: ConvSpec, x, dz, wname, ready=True, fp8=None):
         """Weight gradient of conv c into its flat gradient slice; on the side stream when enabled,
         concurrent with the data-gradient chain (fills the tail waves of the 1-workgroup-per-CU
-        GEMMs), then the gradient-ready hook (collectives order after the side stream)."""
+        GEMMs), then the gradient-ready hook (collectives order after the side stream).
+        fp8 = (x8, dz8, dz8's scale slot): the fp8 weight gradient from the quantised copies (x8 =
+        (codes, slot) of the fp8 forward) instead of the bf16 x and dz."""
         from ..ops import gemm as G
         P = self.params
         side = self._wgrad_stream
+
+        def run():
+            if fp8 is not None:
+                (xq, xslot), dz8, gslot = fp8
+                G.conv_wgrad_fp8(xq, dz8, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad),
+                                 ascale=(gslot[3:4], xslot[3:4]), out=P.g[wname])
+            else:
+                G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
+            if ready:
+                self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
+
         if side is not None:
             if torch.cuda.current_stream() != side:  # (a stream waiting on its own event breaks hipGraph capture)
                 graphs.fork(torch.cuda.current_stream(), side)
             with torch.cuda.stream(side):
-                G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
-                if ready:
-                    self._ready(c.name + "_bn/moving_variance")
+                run()
             # keep the operands alive until the streams join at the end of the backward (no
             # record_stream: its deferred frees made the allocator re-malloc when the host ran
             # several steps ahead)
-            self._side_keep += [x, dz]
+            self._side_keep += [x, dz] + ([fp8[0][0], fp8[1]] if fp8 is not None else [])
         else:
-            G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
-            if ready:
-                self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
+            run()
 
     def _fold_stream(self):
         """Stream for the slab fold of a main-stream fused weight gradient (pw_conv wgrad=): the
@@ -761,6 +782,7 @@ class ResNet:
             x = images  # the dedicated stem kernels read the packed RGB (no channel-padding pass)
         else:
             x = K.pad_channels(images.contiguous(), self.in_store)
+        self._x8 = {}
         if fp8:
             self._fp8_step_begin()
         self._wp_cur = None

@@ -63,6 +63,7 @@ _SIGS = {
     "ttdk_conv_dgrad_subpixel_stat_rows": [G],
     "ttdk_conv_wgrad": [P, P, G, P, P, I, I, I, I, P],
     "ttdk_conv_wgrad_bn": [P, P, P, P, G, P, P, I, I, I, I, P],
+    "ttdk_conv_wgrad_fp8": [P, P, G, P, P, I, I, P, P, P],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
     "ttdk_set_big_pers": [I],
     # gemm_f32.hip

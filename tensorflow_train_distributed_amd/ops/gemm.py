@@ -719,6 +719,40 @@ def conv_wgrad(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=
     return out
 
 
+def conv_wgrad_fp8_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)):
+    """Whether conv_wgrad_fp8 takes this weight gradient: C and K multiples of 16, the pixel
+    count a multiple of 128, R*S*C >= 256, the fp8 input under 4 GiB."""
+    g = conv_geom(tuple(x_shape), tuple(w_shape), stride, padding)
+    pixels = g.N * g.P * g.Q
+    return (g.C % 16 == 0 and g.K % 16 == 0 and pixels % 128 == 0 and g.R * g.S * g.C >= 256
+            and g.N * g.H * g.W * g.C < (1 << 32))
+
+
+def conv_wgrad_fp8(x8, dy8, w_shape, stride=(1, 1), padding=(0, 0), *, ascale, out=None, beta=0, splits=None):
+    """fp8 weight gradient dw[K,R,S,C] (fp32) = sum over pixels of dy8 x im2col(x8): dy8 [N,P,Q,K]
+    OCP e5m2, x8 [N,H,W,C] e4m3 (uint8 codes), ascale = (inverse scale of dy8, of x8) as device
+    fp32 scalars (conv_wgrad_fp8.hip: both operands MN-major on the block-scaled fp8 MFMA)."""
+    if x8.dtype != torch.uint8 or dy8.dtype != torch.uint8:
+        raise ValueError("conv_wgrad_fp8 wants uint8 operands")
+    if not conv_wgrad_fp8_ok(x8.shape, w_shape, stride, padding):
+        raise ValueError("conv_wgrad_fp8: shape not supported (%s, %s)" % (tuple(x8.shape), tuple(w_shape)))
+    g = conv_geom(x8.shape, w_shape, stride, padding)
+    if out is None:
+        out = torch.empty(tuple(w_shape), dtype=torch.float32, device=x8.device)
+    M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
+    if splits is None:
+        tiles = -(-M // 256) * -(-N // 128)
+        splits = max(1, min((K // 128) // 16, -(-BIG_WGRAD_WGS // tiles)))
+    _log("wgrad8_%dx%d_s%d" % (g.R, g.S, g.sh), M, N, K, splits)
+    ws = None
+    if splits > 1:
+        ws = torch.empty((splits,) + tuple(w_shape), dtype=torch.float32, device=x8.device)
+    _lib.call("ttdk_conv_wgrad_fp8", x8.data_ptr(), dy8.data_ptr(), ctypes.byref(g), out.data_ptr(),
+              ws.data_ptr() if ws is not None else None, splits, beta, ascale[0].data_ptr(), ascale[1].data_ptr(),
+              _lib.stream())
+    return out
+
+
 def conv_wgrad_bn_fusable(x_shape, w_shape, stride=(1, 1), padding=(0, 0)):
     """Whether conv_wgrad_bn runs for this conv (non-pointwise, 4-wave im2col-gather kernel)."""
     g = conv_geom(x_shape, w_shape, stride, padding)

@@ -754,3 +754,42 @@ def test_weight_gradient_with_fused_bias_rowsum_vs_fp32(M, N, K, splits, beta):
     out3 = out0.clone()
     G.gemm(dy, x, trans_a=True, out=out3, splits=splits, beta=beta)
     torch.testing.assert_close(out, out3, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(2, 16, 16, 256, 256, 1), (1, 16, 16, 128, 128, 1), (4, 8, 8, 512, 512, 1),
+                                 (2, 16, 16, 128, 256, 2), (3, 16, 8, 256, 512, 1), (2, 14, 14, 256, 256, 1)])
+def test_conv_wgrad_fp8_vs_fp32_oracle(cfg):
+    """fp8 weight gradient (e5m2 dy x e4m3 im2col(x), both MN-major through ds_read_b64_tr_b8, block-
+    scaled MFMA, split-K) of a 3x3 conv vs the fp32 weight gradient of the DEQUANTISED operands
+    (tight: only the summation order differs) and vs the bf16 weight gradient (fp8 rounding: loose)."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    N, H, W, C, Kc, s = cfg
+    torch.manual_seed(17 + C)
+    x = torch.randn(N, H, W, C, device="cuda").relu().bfloat16()
+    P = (H + 2 - 3) // s + 1
+    Q = (W + 2 - 3) // s + 1
+    dy = (torch.randn(N, P, Q, Kc, device="cuda") * 1e-3).bfloat16()
+    s_x = torch.tensor([448.0 / float(x.float().abs().max())], device="cuda")
+    s_dy = torch.tensor([57344.0 * 0.5 / float(dy.float().abs().max())], device="cuda")
+    x8 = K.quant_fp8(x, s_x)
+    dy8 = K.quant_fp8(dy, s_dy, e5m2=True)
+    inv = (1.0 / s_dy, 1.0 / s_x)
+    wshape = (Kc, 3, 3, C)
+    assert G.conv_wgrad_fp8_ok(x8.shape, wshape, (s, s), (1, 1)) == (N * P * Q % 128 == 0)
+    if N * P * Q % 128:
+        return
+    for splits in (1, 3):
+        dw = G.conv_wgrad_fp8(x8, dy8, wshape, (s, s), (1, 1), ascale=inv, splits=splits)
+        # exact decodes (fp8 values are bf16-representable at unit scale), scaled in fp32
+        one = torch.ones(1, device="cuda")
+        xq = K.dequant_fp8(x8, one).float() * inv[1]
+        dyq = K.dequant_fp8(dy8, one, e5m2=True).float() * inv[0]
+        wv = torch.zeros(Kc, C, 3, 3, device="cuda", requires_grad=True)
+        y = F.conv2d(xq.permute(0, 3, 1, 2), wv, stride=s, padding=1)
+        y.backward(dyq.permute(0, 3, 1, 2))
+        ref = wv.grad.permute(0, 2, 3, 1)
+        assert _rel(dw, ref) < 1e-4, splits
+    ref_bf = G.conv_wgrad(x, dy, wshape, (s, s), (1, 1))
+    assert _rel(dw, ref_bf) < 0.1
