@@ -394,7 +394,7 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const bf16_t* __restric
         for (int j = 0; j < 8; ++j) f[j] = ttdk::relu(f[j]);
       }
       const uint4 packed = pack8(f);
-      reinterpret_cast<uint4*>(out)[i] = packed;
+      if (out) reinterpret_cast<uint4*>(out)[i] = packed;  // null: only the fp8 copy / mask are consumed
       if (mask) {  // 1 bit per element of [stored bf16 > 0]: the ReLU mask backward reads instead of `out`
         const uint32_t w[4] = {packed.x, packed.y, packed.z, packed.w};
         uint32_t mb = 0;
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(kThreads) void bwd_apply_kernel(const bf16_t* __res
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = ca[j] * g[j] + cb[j] * yf[j] + cc[j];
       const uint4 packed = pack8(g);
-      reinterpret_cast<uint4*>(dz)[i] = packed;
+      if (dz) reinterpret_cast<uint4*>(dz)[i] = packed;  // null: the e5m2 copy is the only consumer
       if (q8) {  // the stored bf16 values, scaled, saturated to the e5m2 range
         float fq[8];
         unpack8(packed, fq);
@@ -599,7 +599,7 @@ TTDK_EXPORT int ttdk_bn_bwd_finalize(const float* sums, float count, int C, cons
 TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* shift, const bf16_t* residual,
                               const float* rscale, const float* rshift, bf16_t* out, uint8_t* mask, uint8_t* q8,
                               float* q8_slot, long long n, int C, int relu, hipStream_t st) {
-  if (C % 8 || n % 8 || (q8 && !q8_slot) || (rscale && (!residual || !rshift))) return hipErrorInvalidValue;
+  if (C % 8 || n % 8 || (q8 && !q8_slot) || (rscale && (!residual || !rshift)) || (!out && !q8)) return hipErrorInvalidValue;
   const long long n8 = n / 8;
   const int grid = grid_for(n8, kThreads * kUnroll);
   if (kThreads % (C >> 3) == 0)
@@ -614,7 +614,7 @@ TTDK_EXPORT int ttdk_bn_apply(const bf16_t* y, const float* scale, const float* 
 TTDK_EXPORT int ttdk_bn_bwd_apply_q8(const bf16_t* dy, const bf16_t* out, const uint8_t* mask, const bf16_t* y,
                                      const float* coef, bf16_t* dz, uint8_t* q8, float* q8_slot, long long n, int C,
                                      hipStream_t st) {
-  if (C % 8 || n % 8 || (q8 && !q8_slot)) return hipErrorInvalidValue;
+  if (C % 8 || n % 8 || (q8 && !q8_slot) || (!dz && !q8)) return hipErrorInvalidValue;
   const long long n8 = n / 8;
   const int grid = grid_for(n8, kThreads * kUnroll);
   if (kThreads % (C >> 3) == 0)

@@ -107,7 +107,9 @@ class ResNet:
         # fp8 weight gradients of the convs that have both fp8 copies already (the e4m3 input of the
         # fp8 forward and the e5m2 dz of the fp8 data gradient): ops.gemm.conv_wgrad_fp8
         self.fp8_wgrad = os.environ.get("TTD_FP8_WGRAD", "1") != "0"
+        self.fp8_only_input = os.environ.get("TTD_FP8_ONLY_INPUT", "1") != "0"
         self._x8 = {}
+        self._x_unstored = set()
         # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
         # never stored: two HBM passes of the stage's largest tensor saved; TTD_FUSE_PROJ=0: off)
         self.fuse_proj = os.environ.get("TTD_FUSE_PROJ", "1") != "0"
@@ -345,7 +347,7 @@ class ResNet:
                 and G.conv3_rows(H, W, c.cin_store, c.cout) > 0)
 
     def _convbn_fwd(self, c: ConvSpec, x, relu, residual=None, x8=None, want8=False, pool=False, defer=False,
-                    residual_bn=None, pro=None, pro_big=False):
+                    residual_bn=None, pro=None, pro_big=False, store_out=True):
         """conv + BN (+residual) (+ReLU). x8 = (fp8 copy of x, its scale slot) selects the fp8
         forward GEMM; want8 makes the BN-apply pass also emit an fp8 copy of the output.
         defer=True: no apply pass — returns the raw conv output (the consumer applies this BN
@@ -436,7 +438,14 @@ class ResNet:
             q8 = torch.empty((N, Pp, Q, c.cout), dtype=torch.uint8, device=x.device)
             slot = self._new_a_slot()
         out = K.bn_apply(y2, st.scale, st.shift, residual=None if residual is None else residual.view(M, c.cout),
-                         residual_bn=residual_bn, relu=relu, mask=mask, q8=q8, q8_slot=slot).view(N, Pp, Q, c.cout)
+                         residual_bn=residual_bn, relu=relu, mask=mask, q8=q8, q8_slot=slot,
+                         store_out=store_out or not want8)
+        if out is None:
+            # only the fp8 copy exists: a storage-free stand-in that carries the shape (its consumer
+            # reads x8; _wgrad refuses a bf16 weight gradient over it)
+            out = torch.empty((1,), dtype=torch.bfloat16, device=x.device).expand(N, Pp, Q, c.cout)
+        else:
+            out = out.view(N, Pp, Q, c.cout)
         if want8:
             return out, [x, y, mask, st], (q8, slot)
         return out, [x, y, mask, st]
@@ -530,7 +539,8 @@ class ResNet:
                                         out=dx, beta=dx_beta if dx is not None else 0, beta_s2=bs2)
             self._wgrad(c, x, dz, wname)
             return out, (partial, T)
-        if (need_dx and dstat is not None and feeds is not None and feeds2 is None and dx is None
+        unstored = c.name in self._x_unstored  # only the fp8 copy of x exists: the fp8 branch below
+        if (need_dx and dstat is not None and feeds is not None and feeds2 is None and dx is None and not unstored
                 and self.fuse_bn_bwd and self.c3_dgrad == 1 and self._c3_ok(c, x.shape[1], x.shape[2])):
             # halo 3x3 data gradient with this unit's BN backward as its operand prologue (dz is
             # written once there for the weight gradient) and the feeding unit's BN-backward
@@ -546,6 +556,7 @@ class ResNet:
             return out, (partial, T)
         stride, pad = (c.stride, c.stride), (c.pad, c.pad)
         if (need_dx and dstat is not None and self.fuse_bn_bwd and self.bn_pro and not wgrad_last and not sampled_only
+                and not unstored
                 and self.device.type == "cuda" and Kc <= self.BNPRO_MAX_K and c.cin_store <= self.BNPRO_MAX_N
                 and G.dgrad_bnpro_ok(tuple(x.shape), (c.cin_store, c.k, c.k, Kc), stride, pad)):
             # BN backward formed inside the data gradient's operand tile (dz stored there once for
@@ -577,17 +588,18 @@ class ResNet:
             g8 = (self._fp8 is not None and need_dx and c.name in self._g8 and self._wp_cur is not None
                   and feeds is not None and feeds2 is None and dx is None)
             q8 = torch.empty(y.numel(), dtype=torch.uint8, device=y.device) if g8 else None
+            # both consumers of dz on fp8 (data gradient and weight gradient): no bf16 dz at all
+            w8 = g8 and self._fp8_bwd_steps >= 1 and not wgrad_last and self._fp8_wgrad_ok(c, tuple(x.shape))
             dz = K.bn_backward_from_partial(dout.view(M, Kc), y.view(M, Kc), P.var[pre + "gamma"], st,
                                             P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1], q8=q8,
-                                            q8_slot=self._g_slots[self._g8[c.name]] if g8 else None
-                                            ).view(N, Pp, Q, Kc)
+                                            q8_slot=self._g_slots[self._g8[c.name]] if g8 else None,
+                                            store_dz=not w8)
+            if dz is not None:
+                dz = dz.view(N, Pp, Q, Kc)
             if g8 and self._fp8_bwd_steps >= 1:  # (step 0 only collects the gradient amax)
                 dz8 = q8.view(N, Pp, Q, Kc)
-                x8 = self._x8.get(c.name)
-                if (self.fp8_wgrad and x8 is not None and not wgrad_last
-                        and G.conv_wgrad_fp8_ok(tuple(x.shape), tuple(P.var[wname].shape), (c.stride, c.stride),
-                                                (c.pad, c.pad))):
-                    self._wgrad(c, x, dz, wname, fp8=(x8, dz8, self._g_slots[self._g8[c.name]]))
+                if w8:
+                    self._wgrad(c, x, dz, wname, fp8=(self._x8[c.name], dz8, self._g_slots[self._g8[c.name]]))
                     wgrad_done = True
         else:
             dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
@@ -693,6 +705,24 @@ class ResNet:
             return wp.phases(wname + "/phases")
         return None
 
+    def _x8_only(self, c: ConvSpec, x_shape) -> bool:
+        """The forward may skip the bf16 copy of c's input: c runs its forward on the fp8 copy and
+        this step's backward will take its weight gradient from it too (a fp8 dz exists from the
+        second step on). TTD_FP8_ONLY_INPUT=0 keeps the bf16 copy."""
+        from ..ops import gemm as G
+        return (self.fp8_only_input and self.fp8_wgrad and self._fp8 is not None and self._fp8_bwd_steps >= 1
+                and self._fp8_conv(c) and c.name in self._g8
+                and G.conv_wgrad_fp8_ok(tuple(x_shape), tuple(self.params.var[c.name + "_conv/kernel"].shape),
+                                        (c.stride, c.stride), (c.pad, c.pad)))
+
+    def _fp8_wgrad_ok(self, c: ConvSpec, x_shape) -> bool:
+        """c's weight gradient runs on fp8 (ops.gemm.conv_wgrad_fp8) in this step's backward: the
+        fp8 forward quantised its input and the fp8 data gradient quantises its dz."""
+        from ..ops import gemm as G
+        return (self.fp8_wgrad and self._fp8 is not None and c.name in self._g8 and c.name in self._x8
+                and G.conv_wgrad_fp8_ok(tuple(x_shape), tuple(self.params.var[c.name + "_conv/kernel"].shape),
+                                        (c.stride, c.stride), (c.pad, c.pad)))
+
     def _wgrad(self, c: ConvSpec, x, dz, wname, ready=True, fp8=None):
         """Weight gradient of conv c into its flat gradient slice; on the side stream when enabled,
         concurrent with the data-gradient chain (fills the tail waves of the 1-workgroup-per-CU
@@ -709,6 +739,9 @@ class ResNet:
                 G.conv_wgrad_fp8(xq, dz8, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad),
                                  ascale=(gslot[3:4], xslot[3:4]), out=P.g[wname])
             else:
+                if c.name in self._x_unstored:
+                    raise RuntimeError("%s: bf16 weight gradient asked for, but the forward stored only the fp8 "
+                                       "copy of its input" % c.name)
                 G.conv_wgrad(x, dz, tuple(P.var[wname].shape), (c.stride, c.stride), (c.pad, c.pad), out=P.g[wname])
             if ready:
                 self._ready(c.name + "_bn/moving_variance")  # last variable of this conv's group
@@ -721,7 +754,7 @@ class ResNet:
             # keep the operands alive until the streams join at the end of the backward (no
             # record_stream: its deferred frees made the allocator re-malloc when the host ran
             # several steps ahead)
-            self._side_keep += [x, dz] + ([fp8[0][0], fp8[1]] if fp8 is not None else [])
+            self._side_keep += [t for t in (x, dz) if t is not None] + ([fp8[0][0], fp8[1]] if fp8 is not None else [])
         else:
             run()
 
@@ -783,6 +816,7 @@ class ResNet:
         else:
             x = K.pad_channels(images.contiguous(), self.in_store)
         self._x8 = {}
+        self._x_unstored = set()
         if fp8:
             self._fp8_step_begin()
         self._wp_cur = None
@@ -795,9 +829,18 @@ class ResNet:
                                     self._wt8_slots)
 
         def unit(c, inp, relu, residual=None, inp8=None, want8=False, defer=False, residual_bn=None, pro=None,
-                 pro_big=False):
+                 pro_big=False, consumer=None):
+            # consumer: the conv this unit's output feeds; when that conv will take both its forward
+            # and its weight gradient from the fp8 copy, the bf16 output is never stored
+            only8 = False
+            if want8 and consumer is not None:
+                n_, h_, w_ = inp.shape[:3]
+                oshape = (n_, (h_ + 2 * c.pad - c.k) // c.stride + 1, (w_ + 2 * c.pad - c.k) // c.stride + 1, c.cout)
+                only8 = self._x8_only(consumer, oshape)
             r = self._convbn_fwd(c, inp, relu, residual=residual, x8=inp8, want8=want8, defer=defer,
-                                 residual_bn=residual_bn, pro=pro, pro_big=pro_big)
+                                 residual_bn=residual_bn, pro=pro, pro_big=pro_big, store_out=not only8)
+            if only8:
+                self._x_unstored.add(consumer.name)
             return r if want8 else (r[0], r[1], None)
 
         from ..utils import tracing
@@ -831,7 +874,8 @@ class ResNet:
                 hm = torch.empty(h.numel() // 8, dtype=torch.uint8, device=h.device)
                 ctxp[2] = hm  # the producing unit's ReLU bits (its backward reads them)
                 o1, c1, o1_8 = unit(blk["c1"], y3p, True, pro=(stp.scale, stp.shift, resp, resbnp, h, hm), defer=c3ok,
-                                    want8=fp8 and not c3ok and self._fp8_conv(blk["c2"]), pro_big=pbig)
+                                    want8=fp8 and not c3ok and self._fp8_conv(blk["c2"]), pro_big=pbig,
+                                    consumer=blk["c2"])
                 pend = None
             proj_side = blk["cd"] is not None and side is not None and self.fwd_proj_side
             if proj_side:
@@ -843,7 +887,8 @@ class ResNet:
                 # h / h8 stay referenced (c1's ctx) past the join below; cd's outputs were made on
                 # the side stream, whose next work is always ordered after this step's main stream
             if c1 is None:
-                o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]), defer=c3ok)
+                o1, c1, o1_8 = unit(blk["c1"], h, True, inp8=h8, want8=fp8 and self._fp8_conv(blk["c2"]), defer=c3ok,
+                                    consumer=blk["c2"])
             pro2 = None
             if c3ok:
                 # o1 was returned raw (deferred BN): the halo kernel writes the applied o1 + bits

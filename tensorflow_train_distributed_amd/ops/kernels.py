@@ -79,13 +79,21 @@ def bn_fwd_finalize(sums, count, gamma, beta, eps, momentum, running_mean, runni
 
 
 def bn_apply(y2d, scale, shift, *, residual=None, residual_bn=None, relu=False, out=None, mask=None, q8=None,
-             q8_slot=None):
+             q8_slot=None, store_out=True):
     """out = act(y*scale + shift (+ residual)); `residual_bn` = (rscale, rshift) applies a BN
     affine to the residual first (a raw projection-shortcut conv output); `mask` (uint8
     [M*C/8]) optionally receives the ReLU mask as bits so the backward need not re-read `out`;
     `q8` (uint8 like out) an fp8 e4m3 copy quantised with the delayed scale of `q8_slot`
-    (fp32[FP8_SLOT], see fp8.hip)."""
+    (fp32[FP8_SLOT], see fp8.hip). store_out=False (with q8): only the fp8 copy and the mask are
+    written (the bf16 output has no consumer); returns None."""
     M, C = y2d.shape
+    if not store_out:
+        if q8 is None:
+            raise ValueError("bn_apply: store_out=False needs the fp8 copy")
+        _lib.call("ttdk_bn_apply", y2d.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(residual),
+                  _p(residual_bn[0] if residual_bn else None), _p(residual_bn[1] if residual_bn else None), None,
+                  _p(mask), _p(q8), _p(q8_slot), M * C, C, int(relu), _s())
+        return None
     if out is None:
         out = torch.empty_like(y2d)
     rs, rh = residual_bn if residual_bn is not None else (None, None)
@@ -138,17 +146,21 @@ def bn_backward_coef(M, C, gamma, state, dgamma, dbeta, partial, T, *, accumulat
 
 
 def bn_backward_from_partial(g, y, gamma, state, dgamma, dbeta, partial, T, *, dz=None, accumulate=False, q8=None,
-                             q8_slot=None):
+                             q8_slot=None, store_dz=True):
     """BN backward when the producer of the (already ReLU-masked) gradient g also emitted the
     per-tile sums (sum g, sum g*y) — ops.gemm.conv_dgrad(bn_stat=...): finalize + one apply
     pass, no separate statistics pass over g and y. q8 (uint8 like dz): an OCP e5m2 copy of dz
     quantised with the delayed scale of q8_slot (fp32[FP8_SLOT]; its amax lanes collect this
-    step's amax)."""
+    step's amax). store_dz=False (with q8): only the fp8 copy is written; returns None."""
     M, C = y.shape
     coef = bn_backward_coef(M, C, gamma, state, dgamma, dbeta, partial, T, accumulate=accumulate, device=y.device)
-    if dz is None:
+    if not store_dz:
+        if q8 is None:
+            raise ValueError("bn_backward_from_partial: store_dz=False needs the fp8 copy")
+        dz = None
+    elif dz is None:
         dz = torch.empty_like(y)
-    _lib.call("ttdk_bn_bwd_apply_q8", g.data_ptr(), None, None, y.data_ptr(), coef.data_ptr(), dz.data_ptr(),
+    _lib.call("ttdk_bn_bwd_apply_q8", g.data_ptr(), None, None, y.data_ptr(), coef.data_ptr(), _p(dz),
               _p(q8), _p(q8_slot), M * C, C, _s())
     return dz
 
