@@ -113,7 +113,19 @@ constexpr uint32_t kAttnPairMul = 0x7FEB352Du;
 __device__ __forceinline__ uint32_t attn_row_term(uint32_t rowid) { return rowid * 0x9E3779B1u; }
 // hash of a precomputed input row_term + pair * kAttnPairMul (kernels walking consecutive pairs
 // form it incrementally instead of multiplying per pair)
-__device__ __forceinline__ uint32_t attn_hash_input(uint32_t key, uint32_t input) { return fmix32(key ^ input); }
+// One multiply-xorshift round (not murmur's two): the hash is regenerated for every probability
+// pair in both backward kernels, where its quarter-rate 32-bit multiplies were the dropout
+// variant's extra cost (bwd 864 vs 702 us per BERT-Large layer at p = 0.1 vs 0). The input is
+// already an odd-multiplier progression over (row, pair) xor a murmur-mixed key; statistics
+// (keep rate, pair-half / neighbour-pair / neighbour-row independence) are pinned by
+// tests/test_kernels_transformer.py::test_attention_dropout_pair_hash_statistics on the mirror.
+__device__ __forceinline__ uint32_t attn_mix(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t attn_hash_input(uint32_t key, uint32_t input) { return attn_mix(key ^ input); }
 __device__ __forceinline__ uint32_t attn_pair_hash(uint32_t key, uint32_t row_term, uint32_t pair) {
   return attn_hash_input(key, row_term + pair * kAttnPairMul);
 }

@@ -185,6 +185,14 @@ def _fmix32(h):
     return h
 
 
+def _attn_mix(h):
+    h = np.asarray(h, dtype=np.uint64) & M32
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x846CA68B)) & M32
+    h ^= h >> np.uint64(16)
+    return h
+
+
 def drop_key(seed: int, step: int, site: int) -> int:
     seed &= (1 << 64) - 1
     step &= (1 << 64) - 1
@@ -222,7 +230,7 @@ def attention_keep_mask(seed: int, step: int, site: int, p: float, B: int, H: in
     rowid = np.arange(B * H * S, dtype=np.uint64).reshape(B * H, S, 1)
     k = np.arange(S, dtype=np.uint64).reshape(1, 1, S)
     mixed = ((rowid * np.uint64(0x9E3779B1)) + ((k >> np.uint64(1)) * np.uint64(0x7FEB352D))) & M32
-    h = _fmix32(key ^ mixed)
+    h = _attn_mix(key ^ mixed)
     half = np.where((k & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
     return (half >= np.uint64(thr)).reshape(B, H, S, S)
 

@@ -48,6 +48,15 @@ def test_attention_dropout_pair_hash_statistics():
     # the two keys of a pair use different halves of one hash: not correlated
     a, b = keep[..., 0::2].ravel(), keep[..., 1::2].ravel()
     assert abs(np.mean(a & b) - np.mean(a) * np.mean(b)) < 0.01
+    # neighbouring pairs of a row, the same key in neighbouring rows, and the same (query, key)
+    # of neighbouring heads are independent too (one multiply-xorshift round per pair hash)
+    for u, v in ((keep[..., 0:-2:2], keep[..., 2::2]), (keep[..., :-1, :], keep[..., 1:, :]),
+                 (keep[:, :-1], keep[:, 1:])):
+        u, v = u.ravel(), v.ravel()
+        assert abs(np.mean(u & v) - np.mean(u) * np.mean(v)) < 0.005
+    # other sites / steps give different masks with the same rate
+    keep2 = T.attention_keep_mask(1234, 8, 3, 0.1, 2, 4, 256)
+    assert abs(keep2.mean() - 0.9) < 0.005 and np.mean(keep == keep2) < 0.85
     assert abs(T.attention_drop_scale(0.1) - 1 / 0.9) < 1e-4
 
 
