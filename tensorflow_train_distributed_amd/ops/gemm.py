@@ -289,8 +289,11 @@ def gemm_f32(a, b, *, trans_a=False, trans_b=False, out=None, bias=None, beta=0)
 
 # workgroups a split-K weight gradient on the 256-row kernel aims for (one per CU: 256 = one
 # wave over the chip; fewer leave CUs to the data-gradient chain it overlaps; TTD_WGRAD_WGS).
-# ResNet-50 b1024 sweep (2 runs each): 64: 74.1, 96: 70.0, 128: 68.8, 160: 68.8, 256: 69.3 ms
-BIG_WGRAD_WGS = int(_os.environ.get("TTD_WGRAD_WGS", "160"))
+# ResNet-50 b1024 sweep (2 runs each): 64: 74.1, 96: 70.0, 128: 68.8, 160: 68.8, 256: 69.3 ms (round 3);
+# after the untracked MN-major DMA (round 4, images/s): 96: 15,246 / 15,203, 112: 15,101 / 15,117,
+# 128: 15,196 / 15,211 (15,227 / 15,173), 144: 15,118 / 15,143, 160: 15,086 / 15,099, 208: 15,056 /
+# 15,121, 256: 15,004 / 15,099 -> 128
+BIG_WGRAD_WGS = int(_os.environ.get("TTD_WGRAD_WGS", "128"))
 
 
 def gemm_wgrad_splits(M, N, K, target_blocks=1024, min_ktiles=8, big_wgs=None):
