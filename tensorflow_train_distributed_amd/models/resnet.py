@@ -221,7 +221,14 @@ class ResNet:
         # the filter transposed to [C,R,S,K] in e4m3 with current scaling (from the step's
         # WeightPrep buffer). The first step only collects the gradient amax (bf16 dgrad).
         self._g8 = {c.name: i for i, c in enumerate(c for c in self.conv_list() if self._fp8_dgrad_conv(c))}
-        self._g_slots = torch.zeros((max(1, len(self._g8)), FP8_SLOT), dtype=torch.float32, device=self.device)
+        # e5m2 dz slots: the fp8-dgrad convs first (their row index is shared with the transposed
+        # e4m3 filter table), then the convs whose weight gradient alone runs on fp8 (the strided
+        # 3x3 convs with an fp8 forward: bf16 sub-pixel data gradient, fp8 weight gradient)
+        self._gq = dict(self._g8)
+        for c in self.conv_list():
+            if c.name not in self._gq and self._fp8_conv(c) and c.k > 1 and c.stride > 1:
+                self._gq[c.name] = len(self._gq)
+        self._g_slots = torch.zeros((max(1, len(self._gq)), FP8_SLOT), dtype=torch.float32, device=self.device)
         self._g_slots[:, 2] = 1.0
         self._g_slots[:, 3] = 1.0
         self._fp8_bwd_steps = 0
@@ -234,7 +241,7 @@ class ResNet:
     def _fp8_step_begin(self):
         from ..ops import kernels as K
         K.fp8_rollover(self._a_slots, margin=0.9)
-        if self._g8:
+        if self._gq:
             K.fp8_rollover(self._g_slots, margin=0.5, fmax=57344.0)
         K.fp8_quant_weights(self.params.compute, self._w8_flat, self._w8_table, self._w8_n, self._w8_max,
                             self._w8_slots)
@@ -587,20 +594,27 @@ class ResNet:
         if dstat is not None:
             g8 = (self._fp8 is not None and need_dx and c.name in self._g8 and self._wp_cur is not None
                   and feeds is not None and feeds2 is None and dx is None)
-            q8 = torch.empty(y.numel(), dtype=torch.uint8, device=y.device) if g8 else None
+            # fp8 weight gradient without an fp8 data gradient (strided 3x3): dz8 still produced
+            # from the first step on (the slot collects its amax), consumed from the second
+            gw8 = (not g8 and self._fp8 is not None and c.name in self._gq and c.name not in self._g8
+                   and not wgrad_last and self._fp8_wgrad_ok(c, tuple(x.shape)))
+            q8 = torch.empty(y.numel(), dtype=torch.uint8, device=y.device) if (g8 or gw8) else None
+            gslot = self._g_slots[self._gq[c.name]] if q8 is not None else None
             # both consumers of dz on fp8 (data gradient and weight gradient): no bf16 dz at all
             w8 = g8 and self._fp8_bwd_steps >= 1 and not wgrad_last and self._fp8_wgrad_ok(c, tuple(x.shape))
             dz = K.bn_backward_from_partial(dout.view(M, Kc), y.view(M, Kc), P.var[pre + "gamma"], st,
                                             P.g[pre + "gamma"], P.g[pre + "beta"], dstat[0], dstat[1], q8=q8,
-                                            q8_slot=self._g_slots[self._g8[c.name]] if g8 else None,
-                                            store_dz=not w8)
+                                            q8_slot=gslot, store_dz=not w8)
             if dz is not None:
                 dz = dz.view(N, Pp, Q, Kc)
             if g8 and self._fp8_bwd_steps >= 1:  # (step 0 only collects the gradient amax)
                 dz8 = q8.view(N, Pp, Q, Kc)
                 if w8:
-                    self._wgrad(c, x, dz, wname, fp8=(self._x8[c.name], dz8, self._g_slots[self._g8[c.name]]))
+                    self._wgrad(c, x, dz, wname, fp8=(self._x8[c.name], dz8, gslot))
                     wgrad_done = True
+            elif gw8 and self._fp8_bwd_steps >= 1:
+                self._wgrad(c, x, dz, wname, fp8=(self._x8[c.name], q8.view(N, Pp, Q, Kc), gslot))
+                wgrad_done = True
         else:
             dz = K.bn_backward(dout.view(M, Kc), None, y.view(M, Kc), P.var[pre + "gamma"], st, P.g[pre + "gamma"],
                                P.g[pre + "beta"], g_out=None if g_out is None else g_out.view(M, Kc),
@@ -711,7 +725,7 @@ class ResNet:
         second step on). TTD_FP8_ONLY_INPUT=0 keeps the bf16 copy."""
         from ..ops import gemm as G
         return (self.fp8_only_input and self.fp8_wgrad and self._fp8 is not None and self._fp8_bwd_steps >= 1
-                and self._fp8_conv(c) and c.name in self._g8
+                and self._fp8_conv(c) and c.name in self._gq
                 and G.conv_wgrad_fp8_ok(tuple(x_shape), tuple(self.params.var[c.name + "_conv/kernel"].shape),
                                         (c.stride, c.stride), (c.pad, c.pad)))
 
@@ -719,7 +733,7 @@ class ResNet:
         """c's weight gradient runs on fp8 (ops.gemm.conv_wgrad_fp8) in this step's backward: the
         fp8 forward quantised its input and the fp8 data gradient quantises its dz."""
         from ..ops import gemm as G
-        return (self.fp8_wgrad and self._fp8 is not None and c.name in self._g8 and c.name in self._x8
+        return (self.fp8_wgrad and self._fp8 is not None and c.name in self._gq and c.name in self._x8
                 and G.conv_wgrad_fp8_ok(tuple(x_shape), tuple(self.params.var[c.name + "_conv/kernel"].shape),
                                         (c.stride, c.stride), (c.pad, c.pad)))
 
