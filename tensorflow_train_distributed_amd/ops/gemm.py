@@ -679,9 +679,17 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
 _WGRAD_GATHER_X3 = _os.environ.get("TTD_WGRAD_GATHER_X3", "1") != "0"  # A/B switch
 
 
-def wgrad_splits(g, target_blocks=1024, min_ktiles=8):
+# split-K block target of the 4-wave weight-gradient kernel (im2col-gather / small-tile shapes):
+# ResNet-50 b1024, interleaved pairs on one box: 256: 14,956 / 14,974, 512: 15,107 / 15,061,
+# 1024: 15,053 / 15,008 images/s (fewer slab bytes competing with the HBM-bound main chain)
+_WGRAD_TARGET_BLOCKS = int(_os.environ.get("TTD_WGRAD_TARGET_BLOCKS", "512"))
+
+
+def wgrad_splits(g, target_blocks=None, min_ktiles=8):
     """Split-K factor for the weight gradient: enough blocks to fill 256 CUs twice, but every
     split keeps >= min_ktiles K-steps (the slab write + reduce is pure overhead)."""
+    if target_blocks is None:
+        target_blocks = _WGRAD_TARGET_BLOCKS
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
     bbn = big_bn_wgrad(M, N, K)
     if bbn:  # mirrors ttdk_conv_wgrad's choice of the 256-row LDS-DMA kernel
