@@ -2215,7 +2215,7 @@ __device__ __forceinline__ void pers_epi(const f32x4_t (&acc)[2][2][4][2], const
 template <int BN, class OA, class OB, int EK>
 __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::Params pa, typename OB::Params pb,
                                                                 EpiParams E, int M, int N, int K, int tiles_m,
-                                                                int tiles_n, int ovl, int fullwait) {
+                                                                int tiles_n, int ovl, int fullwait, int* tq) {
   using Gm = Geo<BN>;
   constexpr int T = OA::THREADS, NW = T / 64, WN = NW / 2;
   static_assert(OB::THREADS == T && NW == 8, "8-wave operand policies");
@@ -2280,9 +2280,20 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
     }
   };
 
-  int vt = blockIdx.x;
-  if (vt >= nblk) return;
-  int t = xcd_remap(vt, nblk);
+  // Tiles: XCD x = blockIdx.x & 7 owns the contiguous tile range of xcd_remap; its G8 = gridDim.x / 8
+  // workgroups take tiles idx = blockIdx.x >> 3 first, then idx + G8, ... (static), or — with the
+  // tile queue tq (9 ints: one counter per XCD + a finished-workgroup count) — the next unclaimed idx
+  // of their XCD's range: a workgroup that only gets a CU late (the BERT weight-gradient side stream
+  // holds up to 192 of them for hundreds of us) then takes fewer tiles instead of finishing its
+  // static share late and holding the whole launch.
+  const int xcd = blockIdx.x & 7, G8 = gridDim.x >> 3;
+  const int xq = nblk >> 3, xr = nblk & 7;
+  const int xbase = xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq;
+  const int xcnt = xq + (xcd < xr ? 1 : 0);
+  __shared__ int s_next;
+  int idx = blockIdx.x >> 3;
+  if (idx >= xcnt) return;  // (never with a tile queue: the host launches it only for tiles > 8 G8)
+  int t = xbase + idx;
   prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
   const float alpha_e = epi_alpha(E);
   // store instructions per thread of a whole-tile (unchecked) epilogue: 8 row blocks x 2 column
@@ -2295,6 +2306,9 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
 
   for (;;) {
     const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+    // claim the next tile now: the atomic's round trip hides under this tile's main loop
+    int claim = 0;
+    if (tq && tid == 0) claim = atomicAdd(tq + xcd, 1);
     f32x4_t acc[2][2][4][NB];
 #pragma unroll
     for (int ha = 0; ha < 2; ++ha)
@@ -2349,23 +2363,36 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
       mma(fa[1], fb[0], acc[1][0]);
       barrier();
     }
+    if (tq) {
+      if (tid == 0) s_next = claim;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     if (!lag) barrier();  // both wave halves past their last LDS read: the stage buffers are free
-    const int nvt = vt + gridDim.x;
-    if (ovl && nvt < nblk) {
-      t = xcd_remap(nvt, nblk);
+    const int nidx = tq ? G8 + __builtin_amdgcn_readfirstlane(s_next) : idx + G8;
+    const bool more = nidx < xcnt;
+    if (ovl && more) {
+      t = xbase + nidx;
       prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
     }
     // ------------------------------------------------------------ register epilogue
     const bool whole = m0 + BM <= M && n0 + BN <= N;
     if (whole) pers_epi<EK, false, BNH, WC>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
     else pers_epi<EK, true, BNH, WC>(acc, E, m0, n0, M, N, alpha_e, lane, wm, wn);
-    if (nvt >= nblk) break;
+    if (!more) break;
     prev = !ovl ? 0 : (whole && !fullwait ? 1 : 2);
     if (!ovl) {
-      t = xcd_remap(nvt, nblk);
+      t = xbase + nidx;
       prologue((t / tiles_n) * BM, (t % tiles_n) * BN);
     }
-    vt = nvt;
+    idx = nidx;
+  }
+  if (tq && tid == 0) {
+    // every workgroup's last claim (the one past its XCD's range) precedes its arrival here, so
+    // the last to arrive can reset the queue for the next launch (graph replays included)
+    if (atomicAdd(tq + 8, 1) == static_cast<int>(gridDim.x) - 1) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) tq[i] = 0;
+    }
   }
 }
 
@@ -2375,7 +2402,7 @@ __global__ __launch_bounds__(OA::THREADS, 1) void gemm256p_kernel(typename OA::P
 // Returns nullptr when more than kMaxCtr tiles are asked for (the caller keeps the fold kernel).
 constexpr int kMaxCtr = 1 << 16;
 inline int* tile_counters(hipStream_t st, int tiles) {
-  if (tiles > kMaxCtr) return nullptr;
+  if (tiles > kMaxCtr - 16) return nullptr;  // (the last 16 ints: the persistent GEMM's tile queue)
   struct Buf {
     hipStream_t st;
     int* p;
@@ -2459,10 +2486,17 @@ hipError_t launch(const typename OA::Params& pa, const typename OB::Params& pb, 
       const int ovl = ::ttdk_rt::pers_flag() == 1;
       // TTD_PERS_STORE_WAIT=1: wait for every store of the previous epilogue (A/B)
       static const int fullwait = getenv_int("TTD_PERS_STORE_WAIT", 0);
+      // per-XCD tile queue (TTD_PERS_QUEUE, default 1): the stream's counter buffer, last 16 ints
+      static const int queue = getenv_int("TTD_PERS_QUEUE", 1);
+      int* tq = nullptr;
+      if (queue && cus % 8 == 0) {
+        int* c = tile_counters(st, 0);
+        if (c) tq = c + kMaxCtr - 16;
+      }
 #define TTDK_PERS(EKV)                                                                                                \
   case EKV:                                                                                                           \
     hipLaunchKernelGGL((gemm256p_kernel<BN, OA, OB, EKV>), dim3(cus), dim3(THR), 0, st, pa, pb, pe, M, N, K, tm, tn, ovl, \
-                       fullwait);                                                                                     \
+                       fullwait, tq);                                                                                 \
     return hipGetLastError();
       switch (ek) {
         TTDK_PERS(0)
