@@ -117,7 +117,7 @@ __device__ __forceinline__ void wave_sum4(float& a, float& b, float& c, float& d
   }
 }
 
-template <int NV, int W, int U>  // W waves per block, U rows in flight per wave
+template <int NV, int W, int U, bool PF = false>  // W waves per block, U rows in flight per wave, PF: prefetch
 __global__ __launch_bounds__(W * 64) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                              const float* __restrict__ mean_in,
                                                              const float* __restrict__ rstd_in,
@@ -150,6 +150,27 @@ __global__ __launch_bounds__(W * 64) void ln_bwd_kernel(const bf16_t* __restrict
         d[j] = drop_keep(kout, static_cast<unsigned long long>(row) * H + c + j, dsp.thr_out) ? d[j] * dsp.scale_out : 0.f;
     }
   };
+  // rows of the next iteration are loaded one iteration ahead (PF): a wave otherwise had no load
+  // in flight while it reduced and stored its rows, and the kernel waited on memory 69 % of its
+  // wave cycles at ~3.4 TB/s (rocprofv3 --pmc, tools/pmc_ln.sh)
+  uint4 nd[U][NV], ns[U][NV];
+  float nmean[U], nrstd[U];
+  auto fetch = [&](long long ra) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long r = ra + u * W;
+      const bool h = r < r1;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int c = (lane + 64 * v) * 8;
+        nd[u][v] = h ? ldg16(dy + r * H + c) : make_uint4(0, 0, 0, 0);
+        ns[u][v] = h ? ldg16(s + r * H + c) : make_uint4(0, 0, 0, 0);
+      }
+      nmean[u] = h ? mean_in[r] : 0.f;
+      nrstd[u] = h ? rstd_in[r] : 0.f;
+    }
+  };
+  if (PF && r0 + w < r1) fetch(r0 + w);
 #pragma unroll 1
   for (long long ra = r0 + w; ra < r1; ra += U * W) {
     long long rw[U];
@@ -161,16 +182,30 @@ __global__ __launch_bounds__(W * 64) void ln_bwd_kernel(const bf16_t* __restrict
     }
     uint4 pd[U][NV], ps[U][NV];
     float mean[U], rstd[U];
+    if constexpr (PF) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int c = (lane + 64 * v) * 8;
-        pd[u][v] = has[u] ? ldg16(dy + rw[u] * H + c) : make_uint4(0, 0, 0, 0);
-        ps[u][v] = has[u] ? ldg16(s + rw[u] * H + c) : make_uint4(0, 0, 0, 0);
+        for (int v = 0; v < NV; ++v) {
+          pd[u][v] = nd[u][v];
+          ps[u][v] = ns[u][v];
+        }
+        mean[u] = nmean[u];
+        rstd[u] = nrstd[u];
       }
-      mean[u] = has[u] ? mean_in[rw[u]] : 0.f;
-      rstd[u] = has[u] ? rstd_in[rw[u]] : 0.f;
+      if (ra + U * W < r1) fetch(ra + U * W);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int c = (lane + 64 * v) * 8;
+          pd[u][v] = has[u] ? ldg16(dy + rw[u] * H + c) : make_uint4(0, 0, 0, 0);
+          ps[u][v] = has[u] ? ldg16(s + rw[u] * H + c) : make_uint4(0, 0, 0, 0);
+        }
+        mean[u] = has[u] ? mean_in[rw[u]] : 0.f;
+        rstd[u] = has[u] ? rstd_in[rw[u]] : 0.f;
+      }
     }
     float c1[U], c2[U];
 #pragma unroll
@@ -561,10 +596,24 @@ using namespace ttdk;
     default: return hipErrorInvalidValue;                                               \
   }
 
+// TTD_LN_BWD_PREFETCH (default 1): the H = 1024 backward loads its next rows one iteration ahead
+inline bool ln_bwd_prefetch() {
+  static const bool on = [] {
+    const char* e = getenv("TTD_LN_BWD_PREFETCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 #define TTDK_LN_BWD_DISPATCH(...)                                                        \
   switch (H) {                                                                           \
     case 512: hipLaunchKernelGGL((ln_bwd_kernel<1, 16, 1>), dim3(nb), dim3(16 * 64), __VA_ARGS__); break; \
-    case 1024: hipLaunchKernelGGL((ln_bwd_kernel<2, 8, 2>), dim3(nb), dim3(8 * 64), __VA_ARGS__); break;  \
+    case 1024:                                                                           \
+      if (ln_bwd_prefetch())                                                             \
+        hipLaunchKernelGGL((ln_bwd_kernel<2, 8, 1, true>), dim3(nb), dim3(8 * 64), __VA_ARGS__); \
+      else                                                                               \
+        hipLaunchKernelGGL((ln_bwd_kernel<2, 8, 2>), dim3(nb), dim3(8 * 64), __VA_ARGS__);       \
+      break;                                                                             \
     case 1536: hipLaunchKernelGGL((ln_bwd_kernel<3, 8, 1>), dim3(nb), dim3(8 * 64), __VA_ARGS__); break;  \
     case 2048: hipLaunchKernelGGL((ln_bwd_kernel<4, 4, 1>), dim3(nb), dim3(4 * 64), __VA_ARGS__); break;  \
     case 4096: hipLaunchKernelGGL((ln_bwd_kernel<8, 4, 1>), dim3(nb), dim3(4 * 64), __VA_ARGS__); break;  \
