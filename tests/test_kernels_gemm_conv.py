@@ -793,3 +793,40 @@ def test_conv_wgrad_fp8_vs_fp32_oracle(cfg):
         assert _rel(dw, ref) < 1e-4, splits
     ref_bf = G.conv_wgrad(x, dy, wshape, (s, s), (1, 1))
     assert _rel(dw, ref_bf) < 0.1
+
+
+@pytest.mark.gpu
+def test_persistent_gemm_tile_queue_matches_fp32_and_replays():
+    """The persistent 256-row GEMM (> one round of tiles, elementwise epilogue) with its per-XCD
+    tile queue: bias + GELU + aux epilogue vs fp32, repeated launches (the queue resets itself)
+    bitwise equal, and hipGraph replays of the same launch bitwise equal too."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(31)
+    # 264 tiles > 256 CUs, 16 K-tiles: the ping-pong schedule's persistent kernel with a dynamic tail
+    M, N, K = 33 * 256, 8 * 256, 1024
+    a = (torch.randn(M, K, device="cuda") / 8).bfloat16()
+    b = (torch.randn(N, K, device="cuda") / 8).bfloat16()
+    bias = torch.randn(N, device="cuda")
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    y = G.gemm(a, b, trans_b=True, bias=bias, act=G.ACT_GELU, aux=aux, tile=(256, 256))
+    pre = a.float() @ b.float().t() + bias
+    ref = torch.nn.functional.gelu(pre, approximate="tanh")
+    assert _rel(aux, pre) < 5e-3
+    assert _rel(y, ref) < 5e-3
+    for _ in range(3):
+        y2 = G.gemm(a, b, trans_b=True, bias=bias, act=G.ACT_GELU, aux=aux, tile=(256, 256))
+        assert torch.equal(y2, y)
+    out = torch.empty_like(y)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        G.gemm(a, b, trans_b=True, bias=bias, act=G.ACT_GELU, aux=aux, out=out, tile=(256, 256))  # warm (allocates the queue)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            G.gemm(a, b, trans_b=True, bias=bias, act=G.ACT_GELU, aux=aux, out=out, tile=(256, 256))
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, y)
