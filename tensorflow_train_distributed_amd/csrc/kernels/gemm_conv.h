@@ -1000,6 +1000,9 @@ __global__ __launch_bounds__(256) void splitk_heads_kernel(const float* __restri
 
 hipError_t splitk_reduce(const float* ws_c, int splits, long long n, float* out, int beta, hipStream_t st) {
   float* ws = const_cast<float*>(ws_c);  // pass 1 folds in place (the slabs are the caller's scratch)
+  // TTD_DIAG_SKIP_FOLD=1: diagnostic only (wrong gradients): measures what the fold passes cost a step
+  static const bool diag_skip = [] { const char* e = getenv("TTD_DIAG_SKIP_FOLD"); return e && atoi(e) != 0; }();
+  if (diag_skip) return hipSuccess;
   const long long vec = (n + 3) / 4;
   const int bx = ceil_div(vec, 256);
   long long want = ((1LL << 19) + vec - 1) / vec;  // groups for ~2^19 pass-1 threads

@@ -136,17 +136,44 @@ __global__ __launch_bounds__(256) void lamb_phase1_kernel(const float* __restric
   const float gs = clip_factor(hyper, sumsq);
   const float wd = seg_wd ? seg_wd[ch.seg] : 0.f;
   float sw = 0.f, su = 0.f;
-  for (int i = threadIdx.x; i < ch.len; i += blockDim.x) {
-    const long long o = ch.start + i;
-    const float wv = w[o], gv = g[o] * gs;
-    const float mv = b1 * m[o] + (1.f - b1) * gv;
-    const float vv = b2 * v[o] + (1.f - b2) * gv * gv;
-    m[o] = mv;
-    v[o] = vv;
+  auto one = [&](float wv, float gv, float& mo, float& vo) {
+    const float mv = b1 * mo + (1.f - b1) * gv;
+    const float vv = b2 * vo + (1.f - b2) * gv * gv;
+    mo = mv;
+    vo = vv;
     const float uu = (mv / bc1) / (sqrtf(vv / bc2) + eps) + wd * wv;
-    u[o] = uu;
     sw += wv * wv;
     su += uu * uu;
+    return uu;
+  };
+  // 16-B accesses (every variable starts 64-element aligned in the flat buffer, chunks are
+  // 16384 long): 28 B per parameter, HBM-bound
+  for (int i = threadIdx.x * 4; i < ch.len; i += blockDim.x * 4) {
+    const long long o = ch.start + i;
+    if (i + 3 < ch.len) {
+      const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(w + o);
+      const f32x4_t gv = *reinterpret_cast<const f32x4_t*>(g + o) * gs;
+      f32x4_t mv = *reinterpret_cast<const f32x4_t*>(m + o), vv = *reinterpret_cast<const f32x4_t*>(v + o);
+      f32x4_t uv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float mo = mv[j], vo = vv[j];
+        uv[j] = one(wv[j], gv[j], mo, vo);
+        mv[j] = mo;
+        vv[j] = vo;
+      }
+      *reinterpret_cast<f32x4_t*>(m + o) = mv;
+      *reinterpret_cast<f32x4_t*>(v + o) = vv;
+      *reinterpret_cast<f32x4_t*>(u + o) = uv;
+    } else {
+      for (int j = i; j < ch.len; ++j) {
+        const long long oj = ch.start + j;
+        float mo = m[oj], vo = v[oj];
+        u[oj] = one(w[oj], g[oj] * gs, mo, vo);
+        m[oj] = mo;
+        v[oj] = vo;
+      }
+    }
   }
   sw = block_sum(sw, red);
   su = block_sum(su, red + 8);
@@ -196,11 +223,25 @@ __global__ __launch_bounds__(256) void lamb_phase2_kernel(float* __restrict__ w,
   const float wn = sqrtf(seg_norms[2 * ch.seg]), un = sqrtf(seg_norms[2 * ch.seg + 1]);
   const float trust = (wn > 0.f && un > 0.f) ? wn / un : 1.f;
   const float step = hyper[kLr] * trust;
-  for (int i = threadIdx.x; i < ch.len; i += blockDim.x) {
+  for (int i = threadIdx.x * 4; i < ch.len; i += blockDim.x * 4) {
     const long long o = ch.start + i;
-    const float wv = w[o] - step * u[o];
-    w[o] = wv;
-    if (wbf) wbf[o] = f2bf(wv);
+    if (i + 3 < ch.len) {
+      const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(w + o) - step * *reinterpret_cast<const f32x4_t*>(u + o);
+      *reinterpret_cast<f32x4_t*>(w + o) = wv;
+      if (wbf) {
+        uint2 p;
+        p.x = pack_bf16x2(wv[0], wv[1]);
+        p.y = pack_bf16x2(wv[2], wv[3]);
+        *reinterpret_cast<uint2*>(wbf + o) = p;
+      }
+    } else {
+      for (int j = i; j < ch.len; ++j) {
+        const long long oj = ch.start + j;
+        const float wv = w[oj] - step * u[oj];
+        w[oj] = wv;
+        if (wbf) wbf[oj] = f2bf(wv);
+      }
+    }
   }
 }
 

@@ -430,22 +430,25 @@ __global__ __launch_bounds__(256) void embed_bwd_type_kernel(const bf16_t* __res
 }
 
 // ------------------------------------------------------------------ row gather / scatter
+// Row r reads source row (idx ? idx[r] : 0) + (r / per) * gs: with per = positions per sequence
+// and gs = the sequence length, the MLM / CLS gathers index [B*S, H] directly from the batch's
+// per-sequence positions (no per-step offset tensor built by framework kernels).
 __global__ __launch_bounds__(256) void gather_rows_kernel(const bf16_t* __restrict__ src, long long lds_,
-                                                          const int* __restrict__ idx, bf16_t* __restrict__ dst, int n,
-                                                          int H) {
+                                                          const int* __restrict__ idx, int per, long long gs,
+                                                          bf16_t* __restrict__ dst, int n, int H) {
   const long long r = static_cast<long long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (r >= n) return;
-  const long long from = idx[r];
+  const long long from = (idx ? idx[r] : 0) + (r / per) * gs;
   for (int c = (threadIdx.x & 63) * 8; c < H; c += 512)
     *reinterpret_cast<uint4*>(dst + r * H + c) = ldg16(src + from * lds_ + c);
 }
 
 __global__ __launch_bounds__(256) void scatter_rows_kernel(const bf16_t* __restrict__ src, const int* __restrict__ idx,
-                                                           bf16_t* __restrict__ dst, long long ldd, int n, int H,
-                                                           int accumulate) {
+                                                           int per, long long gs, bf16_t* __restrict__ dst,
+                                                           long long ldd, int n, int H, int accumulate) {
   const long long r = static_cast<long long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (r >= n) return;
-  const long long to = idx[r];
+  const long long to = (idx ? idx[r] : 0) + (r / per) * gs;
   for (int c = (threadIdx.x & 63) * 8; c < H; c += 512) {
     uint4 v = ldg16(src + r * H + c);
     if (accumulate) {
@@ -699,17 +702,29 @@ TTDK_EXPORT int ttdk_embed_bwd(const bf16_t* ds, const int* ids, const int* tt, 
   return hipGetLastError();
 }
 
-TTDK_EXPORT int ttdk_gather_rows(const bf16_t* src, long long ld_src, const int* idx, bf16_t* dst, int n, int H,
-                                 hipStream_t st) {
-  if (H % 8 || ld_src % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, st, src, ld_src, idx, dst, n, H);
+// idx (nullable) + per / gs: see gather_rows_kernel; per = 1, gs = 0 is a plain index gather.
+TTDK_EXPORT int ttdk_gather_rows(const bf16_t* src, long long ld_src, const int* idx, int per, long long gs, bf16_t* dst,
+                                 int n, int H, hipStream_t st) {
+  if (H % 8 || ld_src % 8 || per < 1 || (!idx && gs == 0 && n > 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, st, src, ld_src, idx, per, gs, dst, n, H);
   return hipGetLastError();
 }
 
-TTDK_EXPORT int ttdk_scatter_rows(const bf16_t* src, const int* idx, bf16_t* dst, long long ld_dst, int n, int H,
-                                  int accumulate, hipStream_t st) {
-  if (H % 8 || ld_dst % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, st, src, idx, dst, ld_dst, n, H, accumulate);
+TTDK_EXPORT int ttdk_scatter_rows(const bf16_t* src, const int* idx, int per, long long gs, bf16_t* dst, long long ld_dst,
+                                  int n, int H, int accumulate, hipStream_t st) {
+  if (H % 8 || ld_dst % 8 || per < 1 || (!idx && gs == 0 && n > 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, st, src, idx, per, gs, dst, ld_dst, n, H,
+                     accumulate);
+  return hipGetLastError();
+}
+
+// dropout RNG state [seed, step]: step += 1 on the stream (a captured node in a graph replay)
+__global__ void rng_advance_kernel(long long* __restrict__ t) {
+  if (threadIdx.x == 0) t[1] = t[1] + 1;
+}
+
+TTDK_EXPORT int ttdk_rng_advance(long long* t, hipStream_t st) {
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(64), 0, st, t);
   return hipGetLastError();
 }
 

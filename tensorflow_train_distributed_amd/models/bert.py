@@ -348,10 +348,12 @@ class BertPretraining:
         ids = batch.input_ids.reshape(-1)
         tt = batch.token_type_ids.reshape(-1)
         seqlen = batch.seqlen
-        offs = (torch.arange(B, device=dev, dtype=torch.int32) * S)
-        pos_idx = (batch.masked_lm_positions + offs[:, None]).reshape(-1).contiguous()
+        # MLM rows b*S + positions[b, p] and CLS rows b*S, formed inside the gather / scatter kernels
+        pos_idx = batch.masked_lm_positions.reshape(-1)
+        if pos_idx.dtype != torch.int32 or not pos_idx.is_contiguous():
+            pos_idx = pos_idx.to(torch.int32).contiguous()
+        pos_grp = (batch.masked_lm_positions.shape[1], S)
         labels = batch.masked_lm_ids.reshape(-1).contiguous()
-        cls_idx = offs.contiguous()
 
         # ---------------------------------------------------------------- forward
         s0 = T.embed_fwd(ids, tt, P.c["bert/embeddings/word_embeddings"], P.c["bert/embeddings/position_embeddings"],
@@ -385,7 +387,7 @@ class BertPretraining:
             ctx.append((x, qkv, ao, lse, s1, m1, r1, y1, pre, inter, s2, m2, r2))
 
         # masked-LM head
-        hm = T.gather_rows(y, pos_idx)
+        hm = T.gather_rows(y, pos_idx, group=pos_grp)
         tpre = torch.empty_like(hm)
         t = G.gemm(hm, P.c["cls/predictions/transform/dense/kernel"], trans_b=True,
                    bias=P.var["cls/predictions/transform/dense/bias"], act=G.ACT_GELU, aux=tpre)
@@ -400,7 +402,7 @@ class BertPretraining:
         T.xent_vocab(logits, V, labels, gsc, dlogits=logits, sums=sums[0:2], mscale=inv_cnt)
         dlog = logits  # gradient now, in place
         # next-sentence head
-        cls = T.gather_rows(y, cls_idx)
+        cls = T.gather_rows(y, None, group=(1, S), n=B)
         pooled = G.gemm(cls, P.c["bert/pooler/dense/kernel"], trans_b=True, bias=P.var["bert/pooler/dense/bias"],
                         act=G.ACT_TANH)
         nsp = G.gemm(pooled, P.c["cls/seq_relationship/output_weights"], trans_b=True,
@@ -434,8 +436,8 @@ class BertPretraining:
         dcls = G.gemm(dpp, P.c["bert/pooler/dense/kernel"])
         hook("bert/pooler/dense/bias")
         dy = K.zeros((Tk, H), dtype=bf, device=dev)
-        T.scatter_rows(dhm, pos_idx, dy)
-        T.scatter_rows(dcls, cls_idx, dy, accumulate=True)
+        T.scatter_rows(dhm, pos_idx, dy, group=pos_grp)
+        T.scatter_rows(dcls, None, dy, accumulate=True, group=(1, S))
 
         # ---------------------------------------------------------------- backward: encoder
         ln_work = T.ln_bwd_workspace(Tk, H, dev)

@@ -21,8 +21,9 @@ _lib.register({
     "ttdk_colreduce": [P, I, I, I, P, I, P],
     "ttdk_embed_fwd": [P, P, P, P, P, P, L, I, I, P],
     "ttdk_embed_bwd": [P, P, P, P, P, P, I, I, I, I, I, P],
-    "ttdk_gather_rows": [P, L, P, P, I, I, P],
-    "ttdk_scatter_rows": [P, P, P, L, I, I, I, P],
+    "ttdk_gather_rows": [P, L, P, I, L, P, I, I, P],
+    "ttdk_scatter_rows": [P, P, I, L, P, L, I, I, I, P],
+    "ttdk_rng_advance": [P, P],
     "ttdk_count_valid": [P, I, F, P, P],
     "ttdk_xent_vocab": [P, L, I, P, I, P, P, P, P, P],
     "ttdk_tanh_bf16": [P, L, P],
@@ -46,7 +47,10 @@ class RngState:
         self.t = torch.tensor([int(seed), 0], dtype=torch.int64, device=device)
 
     def advance(self):
-        self.t[1:2].add_(1)
+        if self.t.is_cuda:
+            _lib.call("ttdk_rng_advance", self.t.data_ptr(), _s())
+        else:
+            self.t[1:2].add_(1)
 
     def host(self):
         v = self.t.cpu().tolist()
@@ -132,17 +136,24 @@ def embed_bwd(ds, ids, tt, dword, dpos, dtype, B, S, pos_beta=0):
               _p(dtype), B, S, H, T, int(pos_beta), _s())
 
 
-def gather_rows(src, idx, out=None):
-    n = idx.numel()
+def gather_rows(src, idx, out=None, *, group=(1, 0), n=None):
+    """out[r] = src[(idx[r] if idx is not None else 0) + (r // per) * gs], group = (per, gs): e.g.
+    per-sequence positions [B, P] of a [B*S, H] activation with group = (P, S); idx None and
+    group (1, S) picks every sequence's first row. idx: contiguous int32."""
+    per, gs = group
+    n = idx.numel() if idx is not None else n
     H = src.shape[1]
     out = out if out is not None else torch.empty((n, H), dtype=src.dtype, device=src.device)
-    _lib.call("ttdk_gather_rows", src.data_ptr(), src.stride(0), idx.data_ptr(), out.data_ptr(), n, H, _s())
+    _lib.call("ttdk_gather_rows", src.data_ptr(), src.stride(0), _p(idx), int(per), int(gs), out.data_ptr(), n, H,
+              _s())
     return out
 
 
-def scatter_rows(src, idx, dst, accumulate=False):
+def scatter_rows(src, idx, dst, accumulate=False, *, group=(1, 0)):
+    """dst[(idx[r] or 0) + (r // per) * gs] (+)= src[r] (the inverse of gather_rows)."""
     n, H = src.shape
-    _lib.call("ttdk_scatter_rows", src.data_ptr(), idx.data_ptr(), dst.data_ptr(), dst.stride(0), n, H,
+    per, gs = group
+    _lib.call("ttdk_scatter_rows", src.data_ptr(), _p(idx), int(per), int(gs), dst.data_ptr(), dst.stride(0), n, H,
               int(accumulate), _s())
     return dst
 

@@ -74,7 +74,7 @@ def test_bn_apply_with_residual_bn_affine(C):
     assert float((out.float() - ref).abs().max()) <= float((unfused.float() - ref).abs().max()) + 1e-6
 
 
-@pytest.mark.parametrize("M,C", [(3000, 96), (200000, 40), (50000, 2048)])
+@pytest.mark.parametrize("M,C", [(3000, 96), (200000, 40), (50000, 2048), (600000, 256)])
 def test_bn_fused_reduce_finalize_matches_unfused(M, C):
     """Slice reduction + finalize (two launches, no atomics) == the memset/atomic-reduce/finalize
     sequence, for fwd and bwd, called repeatedly."""

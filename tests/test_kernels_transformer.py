@@ -242,3 +242,32 @@ def test_gather_scatter_rows():
     assert torch.equal(dst[idx.long()], g)
     T.scatter_rows(g[:1], idx[:1], dst, accumulate=True)
     torch.testing.assert_close(dst[3].float(), 2 * src[3].float(), atol=1e-2, rtol=1e-2)
+
+
+@gpu
+def test_gather_scatter_rows_grouped_and_rng_advance():
+    """Per-sequence positions [B, P] against a [B*S, H] activation (row b*S + pos) and the CLS
+    rows (b*S, no index tensor), both directions; the dropout RNG step advanced on the stream."""
+    dev = "cuda"
+    B, S, P, H = 3, 16, 5, 256
+    src = torch.randn(B * S, H, device=dev).bfloat16()
+    pos = torch.randint(0, S, (B, P), dtype=torch.int32, device=dev)
+    rows = (pos.long() + torch.arange(B, device=dev)[:, None] * S).reshape(-1)
+    g = T.gather_rows(src, pos.reshape(-1), group=(P, S))
+    assert torch.equal(g, src[rows])
+    c = T.gather_rows(src, None, group=(1, S), n=B)
+    assert torch.equal(c, src[::S])
+    dst = torch.zeros(B * S, H, dtype=torch.bfloat16, device=dev)
+    T.scatter_rows(c, None, dst, group=(1, S))
+    assert torch.equal(dst[::S], c)
+    T.scatter_rows(c, None, dst, accumulate=True, group=(1, S))
+    torch.testing.assert_close(dst[::S].float(), 2 * c.float(), atol=1e-2, rtol=1e-2)
+    dst.zero_()
+    uniq = torch.arange(P, dtype=torch.int32, device=dev).repeat(B, 1)  # no duplicate rows
+    T.scatter_rows(g, uniq.reshape(-1), dst, group=(P, S))
+    r2 = (uniq.long() + torch.arange(B, device=dev)[:, None] * S).reshape(-1)
+    assert torch.equal(dst[r2], g)
+    rng = T.RngState(7, dev)
+    for _ in range(3):
+        rng.advance()
+    assert rng.host() == (7, 3)
