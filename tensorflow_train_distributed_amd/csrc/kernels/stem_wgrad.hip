@@ -9,7 +9,8 @@
 // the backward pass with nothing to overlap.
 //
 // Design (MI355X-first): persistent workgroups (4 waves, 3 per CU) walk bands of 8 half output
-// rows (56 pixels) of the 112x112 stem output. The 7 input rows a half row touches live in an
+// rows (56 pixels) of the 112x112 stem output. The row loop keeps its addressing in registers
+// (formed once per thread: coefficients, dz^T destinations, im2col source offsets). The 7 input rows a half row touches live in an
 // LDS ring, so each further output row of the band loads only its 2 new input rows (prefetched
 // into registers with the row's g / y one row ahead); the 56x64 dz block is formed from g and y in registers and stored
 // channel-major (the MFMA A operand, k = pixel), and the 147 real im2col columns (r, s, c<3)
@@ -40,19 +41,47 @@ __global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                             float* __restrict__ ws, int N, int H, int W, int P, int Q,
                                                             int units) {
+  static_assert((RING & (RING - 1)) == 0 && QB % 8 == 0 && (NC * (KP / 8)) % THR == 0, "stem tiling");
   __shared__ __attribute__((aligned(16))) char xs[RING * XW * 16];  // input rows h % RING: [col][8 ch] bf16
   __shared__ __attribute__((aligned(16))) char sA[KO * 128];        // dz^T: [k_out][64 pixels] (kmaj)
   __shared__ __attribute__((aligned(16))) char sB[NC * 128];        // im2col^T: [col][64 pixels] (kmaj)
-  __shared__ float cf[3 * KO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int halves = (Q + QB - 1) / QB;
   const int bands = (P + BAND - 1) / BAND;
+  // Everything that does not change from row to row is formed once per thread: the loop body is
+  // VALU-bound otherwise (the im2col index divisions and the per-element coefficient reads cost
+  // more than the row's 20 MFMAs per wave).
+  // dz^T: thread = (8-channel chunk cc, pixel pair pj); 28 pairs x 8 chunks = 224 threads, each
+  // writing 8 packed bf16 pairs (channel k: pixels 2pj, 2pj+1)
+  const int cc = tid & 7, pj = tid >> 3;
+  const bool dz_on = pj < QB / 2;
+  // the BN coefficients stay in LDS (registers spilled): six 16-B reads per row
+  __shared__ __attribute__((aligned(16))) float cf[3 * KO];
   for (int i = tid; i < 3 * KO; i += THR) cf[i] = coef[i];
+  // dz^T destination of channel cc*8+t: kmaj_off(cc*8+t, pj/4) + (2pj % 8)*2 = da0 + 128t + swizzle
+  const int da0 = cc * 1024 + ((2 * pj) & 7) * 2, dchunk = (2 * pj) >> 3, dsw = (cc & 1) << 2;
   for (int c = tid; c < KO; c += THR)  // the padded pixel chunk (k = 56..63) of every dz^T row stays zero
     *reinterpret_cast<uint4*>(sA + kmaj_off(c, QB / 8)) = make_uint4(0, 0, 0, 0);
+  // im2col^T items: c = tid + THR*m -> pixel chunk kc = c / NC, column col = c % NC = (r, s, ch);
+  // columns >= 147 and the padded pixel chunk are zero for good (written once here)
+  constexpr int NI = NC * (KP / 8) / THR;
+  int ib[NI], id[NI];  // ib: source byte offset | r << 16 (-1: dead item)
+#pragma unroll
+  for (int m = 0; m < NI; ++m) {
+    const int c = tid + THR * m, kc = c / NC, col = c % NC;
+    id[m] = kmaj_off(col, kc);
+    if (col < 147 && kc < QB / 8) {
+      const int r = col / 21, rem = col % 21, sx = rem / 3, ch = rem % 3;
+      ib[m] = ((sx * 8 + ch) * 2 + 256 * kc) | (r << 16);  // bytes: pixel column 2j+s of j = 8kc (+2t, +1 below)
+    } else {
+      ib[m] = -1;
+      *reinterpret_cast<uint4*>(sB + id[m]) = make_uint4(0, 0, 0, 0);
+    }
+  }
   f32x4_t acc[NC / 16];
 #pragma unroll
   for (int b = 0; b < NC / 16; ++b) acc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // cf is read before the row loop's first barrier
 
   // one input row (XW 16-B pixels starting at column 2*q0-3, zero outside the image)
   auto load_xpix = [&](int n, int h, int q0, int t) -> uint4 {
@@ -62,20 +91,18 @@ __global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __rest
     if constexpr (CIN == 8) return ldg16(px);
     return make_uint4(static_cast<uint32_t>(px[0]) | (static_cast<uint32_t>(px[1]) << 16), px[2], 0, 0);
   };
-  // per output row: g / y chunks and the two input rows that row adds to the ring, prefetched
-  // into registers one row ahead
-  constexpr int NG = (QB * (KO / 8) + THR - 1) / THR;
+  // per output row: the thread's g / y pixel pair and the two input rows that row adds to the
+  // ring, prefetched into registers one row ahead
   constexpr int NX2 = (2 * XW + THR - 1) / THR;
-  uint4 pg[NG], py[NG], px[NX2];
+  uint4 pg[2], py[2], px[NX2];
   auto prefetch = [&](int n, int p, int q0) {
 #pragma unroll
-    for (int i = 0; i < NG; ++i) {
-      const int c = tid + THR * i;
-      const int j = c / (KO / 8), cc = c % (KO / 8);
-      const bool ok = c < QB * (KO / 8) && q0 + j < Q;
+    for (int e = 0; e < 2; ++e) {
+      const int j = 2 * pj + e;
+      const bool ok = dz_on && q0 + j < Q;
       const long long off = ((static_cast<long long>(n) * P + p) * Q + q0 + j) * KO + cc * 8;
-      pg[i] = ok ? ldg16(g + off) : make_uint4(0, 0, 0, 0);
-      py[i] = ok ? ldg16(y + off) : make_uint4(0, 0, 0, 0);
+      pg[e] = ok ? ldg16(g + off) : make_uint4(0, 0, 0, 0);
+      py[e] = ok ? ldg16(y + off) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < NX2; ++i) {
@@ -93,7 +120,7 @@ __global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __rest
     for (int c = tid; c < 5 * XW; c += THR) {
       const int rr = c / XW, t = c % XW;
       const int h = 2 * p0 - 3 + rr;
-      *reinterpret_cast<uint4*>(xs + (((h + 8 * RING) % RING) * XW + t) * 16) = load_xpix(n, h, q0, t);
+      *reinterpret_cast<uint4*>(xs + ((h & (RING - 1)) * XW + t) * 16) = load_xpix(n, h, q0, t);
     }
     prefetch(n, p0, q0);
     for (int p = p0; p < p1; ++p) {
@@ -103,46 +130,41 @@ __global__ __launch_bounds__(THR, 3) void stem_wgrad_kernel(const bf16_t* __rest
         const int c = tid + THR * i;
         if (c < 2 * XW) {
           const int rr = c / XW, t = c % XW;
-          *reinterpret_cast<uint4*>(xs + (((2 * p + 2 + rr) % RING) * XW + t) * 16) = px[i];
+          *reinterpret_cast<uint4*>(xs + (((2 * p + 2 + rr) & (RING - 1)) * XW + t) * 16) = px[i];
         }
       }
+      if (dz_on) {
+        float g0[8], y0[8], g1[8], y1[8], c0[8], c1[8], c2[8];
 #pragma unroll
-      for (int i = 0; i < NG; ++i) {
-        const int c = tid + THR * i;
-        if (c >= QB * (KO / 8)) break;
-        const int j = c / (KO / 8), cc = c % (KO / 8);
-        float gf[8], yf[8];
-        unpack8(pg[i], gf);
-        unpack8(py[i], yf);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int k = cc * 8 + t;
-          const float f = cf[k] * gf[t] + cf[KO + k] * yf[t] + cf[2 * KO + k];
-          *reinterpret_cast<bf16_t*>(sA + kmaj_off(k, j >> 3) + (j & 7) * 2) = f2bf(f);
+        for (int j = 0; j < 8; j += 4) {
+          *reinterpret_cast<f32x4_t*>(c0 + j) = *reinterpret_cast<const f32x4_t*>(cf + cc * 8 + j);
+          *reinterpret_cast<f32x4_t*>(c1 + j) = *reinterpret_cast<const f32x4_t*>(cf + KO + cc * 8 + j);
+          *reinterpret_cast<f32x4_t*>(c2 + j) = *reinterpret_cast<const f32x4_t*>(cf + 2 * KO + cc * 8 + j);
         }
+        unpack8(pg[0], g0);
+        unpack8(py[0], y0);
+        unpack8(pg[1], g1);
+        unpack8(py[1], y1);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          *reinterpret_cast<uint32_t*>(sA + da0 + 128 * t + ((dchunk ^ (dsw + (t >> 1))) << 4)) =
+              pack_bf16x2(c0[t] * g0[t] + c1[t] * y0[t] + c2[t], c0[t] * g1[t] + c1[t] * y1[t] + c2[t]);
       }
       __syncthreads();
       if (p + 1 < p1) prefetch(n, p + 1, q0);  // in flight under this row's im2col build and MFMAs
       // 2. im2col^T: column (r, s, c<3) -> B[col][j] = input row 2p-3+r, column 2j+s (relative), channel c
-      // consecutive lanes take consecutive columns of one pixel chunk: their scalar LDS reads
-      // fall on neighbouring bytes (the chunk-fastest order put 8 lanes 256 B apart on one bank)
-      for (int c = tid; c < NC * (KP / 8); c += THR) {
-        const int kc = c / NC, col = c % NC;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (col < 147) {
-          const int r = col / 21, rem = col % 21, s = rem / 3, ch = rem % 3;
-          const char* row = xs + (((2 * p - 3 + r + 8 * RING) % RING) * XW) * 16;
-          uint32_t w4[4];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int j0 = kc * 8 + 2 * t, j1 = j0 + 1;
-            const uint32_t lo = j0 < QB ? *reinterpret_cast<const bf16_t*>(row + ((2 * j0 + s) * 8 + ch) * 2) : 0u;
-            const uint32_t hi = j1 < QB ? *reinterpret_cast<const bf16_t*>(row + ((2 * j1 + s) * 8 + ch) * 2) : 0u;
-            w4[t] = lo | (hi << 16);
-          }
-          v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      for (int m = 0; m < NI; ++m) {
+        if (ib[m] < 0) continue;
+        const char* src = xs + ((2 * p - 3 + (ib[m] >> 16)) & (RING - 1)) * (XW * 16) + (ib[m] & 0xffff);
+        uint32_t w4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t lo = *reinterpret_cast<const bf16_t*>(src + 64 * t);
+          const uint32_t hi = *reinterpret_cast<const bf16_t*>(src + 64 * t + 32);
+          w4[t] = lo | (hi << 16);
         }
-        *reinterpret_cast<uint4*>(sB + kmaj_off(col, kc)) = v;
+        *reinterpret_cast<uint4*>(sB + id[m]) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
       }
       __syncthreads();
       // 3. wave w: output channels 16w..16w+15 x all 160 columns, K = 64 pixels

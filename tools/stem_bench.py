@@ -32,7 +32,10 @@ def timeit(fn, n=5):
 
 t_new = timeit(lambda: G.stem_wgrad(x, g, y, coef, out=out))
 t_old = timeit(lambda: G.conv_wgrad_bn(x, g, y, coef, (64, 7, 7, 8), (2, 2), (3, 3), out=out))
+x3 = x[..., :3].contiguous()
+t3 = timeit(lambda: G.stem_wgrad(x3, g, y, coef, out=out))
 gb = (g.numel() * 2 * 2 + x.numel() * 2) / 1e9
+print("stem wgrad b%d, packed RGB input (the ResNet step's): %.1f us" % (B, t3), flush=True)
 print("stem wgrad b%d: kernel %.1f us (%.2f TB/s of g+y+x)  generic %.1f us" % (B, t_new, gb / t_new * 1e3, t_old),
       flush=True)
 
