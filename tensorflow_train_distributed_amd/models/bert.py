@@ -161,10 +161,27 @@ class BertPretraining:
         # encoder bias gradients formed inside their weight-gradient GEMM from the dy tiles in LDS
         # (ops.gemm.gemm_wgrad_bias) instead of a column-sum pass over dy (TTD_BERT_BIAS_WGRAD=0: off)
         self.bias_in_wgrad = os.environ.get("TTD_BERT_BIAS_WGRAD", "1") != "0" and self.device.type == "cuda"
+        # Plain GEMMs through the vendor library (torch.addmm / mm -> hipBLASLt), TTD_BERT_BLASLT:
+        # 1 = the forward's bias-only GEMMs (QKV, attention output, FFN2, MLM logits; bf16 bias =
+        # the compute copy, as a bf16 mixed-precision layer casts it), 2 (default) = also the plain
+        # and accumulating data gradients; 0 = our persistent GEMM everywhere. The fused GEMMs stay
+        # ours: FFN1 (bias + GELU + pre-activation store), the dGELU data gradient, the weight
+        # gradients with their in-kernel bias row sums. Same box, 2 pairs: 164.1 / 163.9 ms (2),
+        # 166.2 / 166.6 (1), 170.9 / 171.1 (0) — hipBLASLt's 4-wave 256x256 tiles wait far less
+        # than our 8-wave ping-pong main loop (profiles/r3_gemm_pmc_ours_vs_hipblaslt.txt)
+        self.blaslt = int(os.environ.get("TTD_BERT_BLASLT", "2")) if self.device.type == "cuda" else 0
         self._wt = None
         if self.device.type == "cuda":
             from ..ops.transformer import RngState
             self.rng = RngState(seed * 7919 + 17, self.device)
+
+    def _plain(self, x, w, b, b16):
+        """y = x w^T + b (w [out][in] bf16; b fp32, b16 its bf16 compute copy) for the forward's
+        bias-only GEMMs."""
+        if self.blaslt:
+            return torch.addmm(b16, x, w.t())
+        from ..ops import gemm as G
+        return G.gemm(x, w, trans_b=True, bias=b)
 
     # ------------------------------------------------------------------ variables
     @staticmethod
@@ -244,26 +261,34 @@ class BertPretraining:
                 self._wt.append([torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device) for w in ws])
         for l in range(L):
             ws = [self._fused(l, "w")] + [P.c[self._ln(l, n)] for n in self._WT_NAMES]
-            for w, t in zip(ws, self._wt[l]):
+            for i, (w, t) in enumerate(zip(ws, self._wt[l])):
+                if self.blaslt >= 2 and i != 3:
+                    continue  # only the dGELU data gradient (FFN2's weight) still reads a copy
                 K.krsc_to_crsk(w.view(w.shape[0], 1, 1, w.shape[1]), out=t.view(t.shape[0], 1, 1, t.shape[1]))
 
     def _dgrad(self, dy, l, which, **kw):
         """dx = dy · W for encoder weight `which` (0 = fused QKV, 1.. = _WT_NAMES) of layer l."""
         from ..ops import gemm as G
+        if self.blaslt >= 2 and set(kw) <= {"out", "beta"}:
+            # plain / accumulating data gradients through the vendor library (A/B, TTD_BERT_BLASLT=2)
+            w = self._fused(l, "w") if which == 0 else self.params.c[self._ln(l, self._WT_NAMES[which - 1])]
+            if kw.get("beta"):
+                return kw["out"].addmm_(dy, w)
+            return torch.mm(dy, w, out=kw["out"]) if kw.get("out") is not None else torch.mm(dy, w)
         if self._wt is not None and self.transposed_dgrad:
             return G.gemm(dy, self._wt[l][which], trans_b=True, **kw)
         w = self._fused(l, "w") if which == 0 else self.params.c[self._ln(l, self._WT_NAMES[which - 1])]
         return G.gemm(dy, w, **kw)
 
     def _fused(self, l, what):
-        """Zero-copy fused q/k/v views: what in {'w', 'b', 'gw', 'gb'}."""
+        """Zero-copy fused q/k/v views: what in {'w', 'b', 'cb' (bf16 bias), 'gw', 'gb'}."""
         P, H = self.params, self.cfg.hidden_size
         if what in ("w", "gw"):
             o = P.offsets[self._ln(l, "attention/self/query/kernel")]
             buf = P.compute if what == "w" else P.grad
             return buf[o:o + 3 * H * H].view(3 * H, H)
         o = P.offsets[self._ln(l, "attention/self/query/bias")]
-        buf = P.master if what == "b" else P.grad
+        buf = {"b": P.master, "cb": P.compute}.get(what, P.grad)
         return buf[o:o + 3 * H]
 
     # ------------------------------------------------------------------ training step
@@ -364,13 +389,13 @@ class BertPretraining:
         ctx = []
         for l in range(L):
             x = y
-            qkv = G.gemm(x, self._fused(l, "w"), trans_b=True, bias=self._fused(l, "b"))
+            qkv = self._plain(x, self._fused(l, "w"), self._fused(l, "b"), self._fused(l, "cb"))
             ao = torch.empty((Tk, H), dtype=bf, device=dev)
             lse = torch.empty((B * NH, S), dtype=torch.float32, device=dev)
             T.attention_fwd(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], ao, lse, B, NH, S, seqlen=seqlen,
                             p_drop=ad, rng=rng, site=site(l, 0))
-            proj = G.gemm(ao, P.c[self._ln(l, "attention/output/dense/kernel")], trans_b=True,
-                          bias=P.var[self._ln(l, "attention/output/dense/bias")])
+            nb = self._ln(l, "attention/output/dense/bias")
+            proj = self._plain(ao, P.c[self._ln(l, "attention/output/dense/kernel")], P.var[nb], P.c[nb])
             y1, s1, m1, r1 = T.layernorm_fwd(proj, P.var[self._ln(l, "attention/output/LayerNorm/gamma")],
                                              P.var[self._ln(l, "attention/output/LayerNorm/beta")], res=x, eps=eps,
                                              p_in=hd, site_in=site(l, 1), rng=rng)
@@ -378,8 +403,8 @@ class BertPretraining:
             pre = torch.empty((Tk, c.intermediate_size), dtype=bf, device=dev)
             inter = G.gemm(y1, P.c[self._ln(l, "intermediate/dense/kernel")], trans_b=True,
                            bias=P.var[self._ln(l, "intermediate/dense/bias")], act=G.ACT_GELU, aux=pre)
-            o2 = G.gemm(inter, P.c[self._ln(l, "output/dense/kernel")], trans_b=True,
-                        bias=P.var[self._ln(l, "output/dense/bias")])
+            nb = self._ln(l, "output/dense/bias")
+            o2 = self._plain(inter, P.c[self._ln(l, "output/dense/kernel")], P.var[nb], P.c[nb])
             y, s2, m2, r2 = T.layernorm_fwd(o2, P.var[self._ln(l, "output/LayerNorm/gamma")],
                                             P.var[self._ln(l, "output/LayerNorm/beta")], res=y1, eps=eps, p_in=hd,
                                             site_in=site(l, 2), rng=rng)
@@ -393,8 +418,8 @@ class BertPretraining:
                    bias=P.var["cls/predictions/transform/dense/bias"], act=G.ACT_GELU, aux=tpre)
         t2, _, mt, rt = T.layernorm_fwd(t, P.var["cls/predictions/transform/LayerNorm/gamma"],
                                         P.var["cls/predictions/transform/LayerNorm/beta"], eps=eps)
-        logits = G.gemm(t2, P.c["bert/embeddings/word_embeddings"], trans_b=True,
-                        bias=P.var["cls/predictions/output_bias"])
+        logits = self._plain(t2, P.c["bert/embeddings/word_embeddings"], P.var["cls/predictions/output_bias"],
+                             P.c["cls/predictions/output_bias"])
         sums = K.zeros(4, dtype=torch.float32, device=dev)  # own memset: no torch fill kernel in the step
         inv_cnt = torch.empty(1, dtype=torch.float32, device=dev)
         T.count_valid(labels, 1.0, inv_cnt)
@@ -415,7 +440,8 @@ class BertPretraining:
         wgrad(dlog, t2, g["bert/embeddings/word_embeddings"])  # tied decoder (write; embedding adds later)
         K.colsum(dlog, out=g["cls/predictions/output_bias"])
         hook("cls/predictions/output_bias")
-        dt2 = G.gemm(dlog, P.c["bert/embeddings/word_embeddings"])
+        dt2 = (torch.mm(dlog, P.c["bert/embeddings/word_embeddings"]) if self.blaslt >= 2
+               else G.gemm(dlog, P.c["bert/embeddings/word_embeddings"]))
         del dlog, logits
         dt, _ = T.layernorm_bwd(dt2, t, mt, rt, P.var["cls/predictions/transform/LayerNorm/gamma"],
                                 g["cls/predictions/transform/LayerNorm/gamma"],
