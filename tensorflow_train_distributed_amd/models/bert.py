@@ -168,7 +168,8 @@ class BertPretraining:
         # ours: FFN1 (bias + GELU + pre-activation store), the dGELU data gradient, the weight
         # gradients with their in-kernel bias row sums. Same box, 2 pairs: 164.1 / 163.9 ms (2),
         # 166.2 / 166.6 (1), 170.9 / 171.1 (0) — hipBLASLt's 4-wave 256x256 tiles wait far less
-        # than our 8-wave ping-pong main loop (profiles/r3_gemm_pmc_ours_vs_hipblaslt.txt)
+        # than our 8-wave ping-pong main loop (profiles/r3_gemm_pmc_ours_vs_hipblaslt.txt). 3 = the
+        # weight gradients too (fp32 out + column-sum pass): 168.2 / 168.4 vs 164.3 / 164.7 ms, slower
         self.blaslt = int(os.environ.get("TTD_BERT_BLASLT", "2")) if self.device.type == "cuda" else 0
         self._wt = None
         if self.device.type == "cuda":
@@ -333,6 +334,11 @@ class BertPretraining:
 
         def wgrad_and_bias(dy, x, wout, bout):
             M, N, Kd = dy.shape[1], x.shape[1], dy.shape[0]
+            if self.blaslt >= 3:  # A/B: weight gradients through the library too (fp32 output)
+                torch.mm(dy.t(), x, out_dtype=torch.float32, out=wout)
+                if bout is not None:
+                    K.colsum(dy, out=bout)
+                return
             splits = G.gemm_wgrad_splits(M, N, Kd, big_wgs=self.wgrad_wgs)
             if bout is not None and self.bias_in_wgrad and G.wgrad_bias_ok(M, N, Kd, splits):
                 # bias gradient from the weight gradient's own dy tiles (no column-sum pass)
