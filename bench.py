@@ -276,7 +276,12 @@ def main():
     # set of graph launches per step instead of ~600 kernel launches from Python. Same-box A/B
     # at ResNet-50 b1024: eager 68.30 / 68.26 ms, replay 68.43 / 68.27 ms (round 4): parity, so
     # auto = on (the host, 8.5 ms of issue per 68 ms step, is free for input / hooks work).
-    use_graph = args.graph if args.graph >= 0 else 1
+    # Auto = on at N = 1 only: replay of RCCL bucket launches captured on the communicator
+    # stream has been exercised on one-rank communicators but never across real ranks (no
+    # multi-GPU box is reachable from the build loop), so N > 1 stays eager until a two-rank
+    # replay has been checked against eager; --graph 1 / TTD_BENCH_GRAPH=1 opt in.
+    auto_graph = 1 if world == 1 else int(os.environ.get("TTD_BENCH_GRAPH", "0"))
+    use_graph = args.graph if args.graph >= 0 else auto_graph
     red0 = getattr(step, "reducer", None)
     if on_cpu or (world > 1 and getattr(red0, "comm", None) is None):
         # torch process-group collectives are issued eagerly; the native RCCL engine's bucket

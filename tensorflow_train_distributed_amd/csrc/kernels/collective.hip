@@ -161,7 +161,7 @@ struct Engine {
   };
   std::deque<Mark> pend;
   std::vector<hipEvent_t> pool;
-  std::vector<void*> retired;  // outgrown staging buffers, freed once the stream drained
+  std::vector<void*> retired;  // outgrown staging buffers, freed once the stream drained (under wmu)
   std::atomic<int> aborts{0};
 };
 
@@ -185,10 +185,15 @@ bool set_err(Engine* e, const std::string& m) {
 bool settle(Engine* e, ncclResult_t r, const char* what) {
   const auto t0 = std::chrono::steady_clock::now();
   while (r == ncclInProgress) {
-    ncclResult_t a = ncclSuccess;
-    ncclComm_t c = e->comm.load();
-    if (!c) return set_err(e, std::string(what) + ": communicator aborted");
-    const ncclResult_t q = ncclCommGetAsyncError(c, &a);
+    ncclResult_t a = ncclSuccess, q = ncclSuccess;
+    {
+      // under wmu: an abort (which swaps `comm` out under wmu before ncclCommAbort frees it)
+      // cannot free the handle between this load and the query
+      std::lock_guard<std::mutex> g(e->wmu);
+      ncclComm_t c = e->comm.load();
+      if (!c) return set_err(e, std::string(what) + ": communicator aborted");
+      q = ncclCommGetAsyncError(c, &a);
+    }
     if (q != ncclSuccess) { r = q; break; }
     r = a;
     if (r != ncclInProgress) break;
@@ -201,9 +206,14 @@ bool settle(Engine* e, ncclResult_t r, const char* what) {
     std::this_thread::sleep_for(std::chrono::microseconds(dt < 0.01 ? 5 : 500));
   }
   if (r != ncclSuccess) {
-    ncclComm_t c = e->comm.load();
-    const char* last = c ? ncclGetLastError(c) : "";
-    return set_err(e, std::string(what) + ": " + ncclGetErrorString(r) + (last && *last ? std::string(" (") + last + ")" : ""));
+    std::string last;
+    {
+      std::lock_guard<std::mutex> g(e->wmu);
+      ncclComm_t c = e->comm.load();
+      const char* l = c ? ncclGetLastError(c) : "";
+      if (l) last = l;
+    }
+    return set_err(e, std::string(what) + ": " + ncclGetErrorString(r) + (!last.empty() ? " (" + last + ")" : ""));
   }
   return true;
 }
@@ -227,9 +237,10 @@ bool reduce_on(Engine* e, void* buf, size_t count, ncclDataType_t dt, size_t esz
   const int n = ttd_coll::plan(algo, static_cast<long long>(count), e->nranks, e->rank, plan);
   if (n < 0) return set_err(e, "collective plan: bad argument");
   char* p = static_cast<char*>(buf);
-  ncclComm_t comm = e->comm.load();
-  if (!comm) return set_err(e, "communicator aborted");
   for (int i = 0; i < n; ++i) {
+    // reloaded per enqueue: a deadline abort between two steps leaves null, never a freed handle
+    ncclComm_t comm = e->comm.load();
+    if (!comm) return set_err(e, "communicator aborted");
     const ttd_coll::Step& st = plan[i];
     char* a = p + st.send * esz;
     char* b = p + st.recv * esz;
@@ -394,7 +405,10 @@ bool grow_stage(Engine* e, size_t need) {
   if (need <= e->stage_bytes) return true;
   // the old staging buffer may still be read by queued work: retire it (freed once the stream
   // drained, ttdc_synchronize / ttdc_destroy) instead of synchronising under `mu`
-  if (e->stage) e->retired.push_back(e->stage);
+  if (e->stage) {
+    std::lock_guard<std::mutex> g(e->wmu);
+    e->retired.push_back(e->stage);
+  }
   e->stage = nullptr;
   e->stage_bytes = 0;
   if (!hip_ok(e, hipMalloc(&e->stage, need), "hipMalloc")) return false;
@@ -612,8 +626,30 @@ TTDK_EXPORT int ttdc_synchronize(void* h) {
     if (e->failed || !e->comm.load()) return -1;
     if (!hip_ok(e, hipEventRecord(e->join, e->cs), "hipEventRecord")) return -1;
     done = e->join;
+    std::lock_guard<std::mutex> g(e->wmu);
     retired.swap(e->retired);  // queued before this record: free once it completed
   }
+  // error returns hand the staging buffers back (ttdc_destroy frees them): recovery — abort,
+  // then recreate — is exactly when this path runs, so dropping them leaked device memory
+  auto keep_retired = [&] {
+    std::lock_guard<std::mutex> g(e->wmu);
+    e->retired.insert(e->retired.end(), retired.begin(), retired.end());
+    retired.clear();
+  };
+  // abort from this thread only when no other host call is inside RCCL with the handle (the
+  // watchdog aborts a call stuck past the busy deadline); otherwise mark the failure and leave
+  // the abort to the watchdog
+  auto fail_abort = [&](const std::string& why) {
+    keep_retired();
+    if (e->mu.try_lock()) {
+      abort_comm(e, why);
+      e->mu.unlock();
+    } else {
+      std::lock_guard<std::mutex> g(e->wmu);
+      set_err(e, why);
+    }
+    return -1;
+  };
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t q = hipEventQuery(done);
@@ -621,9 +657,9 @@ TTDK_EXPORT int ttdc_synchronize(void* h) {
       for (void* p : retired) hipFree(p);
       return e->failed ? -1 : 0;
     }
-    if (q != hipErrorNotReady) return hip_ok(e, q, "hipEventQuery"), -1;
+    if (q != hipErrorNotReady) return keep_retired(), hip_ok(e, q, "hipEventQuery"), -1;
     // no `mu` here: the watchdog and other threads' calls proceed while this host waits
-    if (e->failed) return -1;  // the watchdog aborted the communicator
+    if (e->failed) return keep_retired(), -1;  // the watchdog aborted the communicator
     ncclComm_t c = e->comm.load();
     ncclResult_t a = ncclSuccess;
     {
@@ -631,14 +667,10 @@ TTDK_EXPORT int ttdc_synchronize(void* h) {
       c = e->comm.load();
       if (c && ncclCommGetAsyncError(c, &a) != ncclSuccess) a = ncclSuccess;
     }
-    if (c && a != ncclSuccess && a != ncclInProgress) {
-      abort_comm(e, std::string("communicator failed: ") + ncclGetErrorString(a));
-      return -1;
-    }
-    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > e->timeout) {
-      abort_comm(e, "collectives did not complete before the deadline: communicator aborted");
-      return -1;
-    }
+    if (c && a != ncclSuccess && a != ncclInProgress)
+      return fail_abort(std::string("communicator failed: ") + ncclGetErrorString(a));
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > e->timeout)
+      return fail_abort("collectives did not complete before the deadline: communicator aborted");
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
@@ -670,13 +702,16 @@ TTDK_EXPORT int ttdc_probe(void* h, void* buf, long long count, int iters, float
   int rc = 0;
   {
     Call call(e);
-    ncclComm_t c = e->comm.load();
-    if (!c) rc = -1;
-    if (rc == 0 && !settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c, e->cs), "ncclAllReduce"))
-      rc = -1;
+    // the handle is reloaded per enqueue (a deadline abort leaves null, never a freed handle)
+    auto once = [&] {
+      ncclComm_t c = e->comm.load();
+      if (!c) return set_err(e, "communicator aborted");
+      return settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c, e->cs), "ncclAllReduce");
+    };
+    if (!once()) rc = -1;
     hipEventRecord(a, e->cs);
     for (int i = 0; rc == 0 && i < iters; ++i)
-      if (!settle(e, ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c, e->cs), "ncclAllReduce")) rc = -1;
+      if (!once()) rc = -1;
     hipEventRecord(b, e->cs);
   }
   if (rc == 0 && ttdc_synchronize(e) == 0) {

@@ -596,7 +596,11 @@ class ResNet:
                   and feeds is not None and feeds2 is None and dx is None)
             # fp8 weight gradient without an fp8 data gradient (strided 3x3): dz8 still produced
             # from the first step on (the slot collects its amax), consumed from the second
-            gw8 = (not g8 and self._fp8 is not None and c.name in self._gq and c.name not in self._g8
+            # Also whenever the forward stored only the fp8 copy of x (_x8_only) but the fp8 data
+            # gradient is off for this conv this step (e.g. TTD_WPREP=0: no prepared e4m3 filters):
+            # the bf16 weight gradient has no input to read, so dz8 is produced for the fp8 one.
+            gw8 = (not g8 and self._fp8 is not None and c.name in self._gq
+                   and (c.name not in self._g8 or c.name in self._x_unstored)
                    and not wgrad_last and self._fp8_wgrad_ok(c, tuple(x.shape)))
             q8 = torch.empty(y.numel(), dtype=torch.uint8, device=y.device) if (g8 or gw8) else None
             gslot = self._g_slots[self._gq[c.name]] if q8 is not None else None

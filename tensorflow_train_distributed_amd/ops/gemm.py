@@ -152,6 +152,28 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     return out
 
 
+_lib.register({"ttdk_gemm4w_bf16": [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.E, _lib.P]})
+
+
+def gemm4w(a, b, *, out=None, bias=None, act=ACT_NONE, residual=None, beta=0, alpha=1.0, aux=None):
+    """C[M,N] = alpha * a[M,K] . b[N,K]^T (+bias) (dGELU(residual) | +C if beta) -> act on the
+    4-wave 256x256 AGPR-accumulator kernel (gemm4w.hip). Both operands K-major bf16; raises when
+    the kernel does not take the shape (no silent fallback: this entry exists to pin that path)."""
+    _check2d(a, torch.bfloat16, "a")
+    _check2d(b, torch.bfloat16, "b")
+    M, K = a.shape
+    N, Kb = b.shape
+    if K != Kb:
+        raise ValueError("gemm4w inner dims differ: %d vs %d" % (K, Kb))
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    e = _epi(out, bias=bias, residual=residual, act=act, beta=beta, alpha=alpha, aux=aux)
+    _log("gemm4w", M, N, K, 1)
+    _lib.call("ttdk_gemm4w_bf16", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), M, N, K, ctypes.byref(e),
+              _lib.stream())
+    return out
+
+
 def wgrad_bias_ok(M, N, K, splits) -> bool:
     """Whether gemm_wgrad_bias takes this weight gradient (dW[M,N] over K tokens, `splits`
     K-slices): the 256-wide ping-pong kernel with >= 16 K-tiles per split."""

@@ -45,7 +45,7 @@ from __future__ import annotations
 import ctypes
 import os
 from ctypes import c_char_p, c_double, c_float, c_int, c_longlong, c_void_p
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -250,19 +250,8 @@ class RcclCommunicator:
         a different collective)."""
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        msg = torch.zeros(129, dtype=torch.uint8, device=dev if dist.get_backend(group) == "nccl" else "cpu")
-        why = ""
-        if rank == 0:
-            try:
-                msg[:128].copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
-                msg[128] = 1
-            except Exception as e:  # noqa: BLE001 - reported to every rank below
-                why = "%s: %s" % (type(e).__name__, e)
-        dist.broadcast(msg, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-        host = msg.cpu()
-        if int(host[128]) != 1:
-            raise errors.UnavailableError("RCCL unique id unavailable on rank 0%s" % (": " + why if why else ""))
-        return cls(bytes(host[:128].tolist()), world, rank, dev, **kw)
+        (uid,) = broadcast_unique_ids(group, 1, dev)
+        return cls(uid, world, rank, dev, **kw)
 
     # ------------------------------------------------------------------ step path
     def _check(self, rc: int, what: str):
@@ -378,32 +367,74 @@ def _key(group):
     return (_PG["generation"], id(group) if group is not None else None)
 
 
-def _probe_budgets(group, overlap_ms, bucket_bytes):
+def broadcast_unique_ids(group, n: int, device) -> List[bytes]:
+    """`n` RCCL unique ids drawn on rank 0 of `group`, carried to every rank by ONE broadcast of
+    the torch process group with a status byte: a failure on rank 0 reaches every rank through
+    that same broadcast and all of them raise together."""
+    rank = dist.get_rank(group)
+    dev = torch.device(device)
+    msg = torch.zeros(128 * n + 1, dtype=torch.uint8, device=dev if dist.get_backend(group) == "nccl" else "cpu")
+    why = ""
+    if rank == 0:
+        try:
+            for i in range(n):
+                msg[128 * i:128 * (i + 1)].copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
+            msg[128 * n] = 1
+        except Exception as e:  # noqa: BLE001 - reported to every rank below
+            why = "%s: %s" % (type(e).__name__, e)
+    dist.broadcast(msg, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    host = msg.cpu()
+    if int(host[128 * n]) != 1:
+        raise errors.UnavailableError("RCCL unique id unavailable on rank 0%s" % (": " + why if why else ""))
+    return [bytes(host[128 * i:128 * (i + 1)].tolist()) for i in range(n)]
+
+
+def _probe_budgets(group, overlap_ms, bucket_bytes, budgets=None, make=None):
     """Create a communicator per candidate CTA budget, probe each, keep the one the policy
-    picks (collective: every rank reaches the same choice from the slowest rank's numbers)."""
-    world = dist.get_world_size(group)
-    comms, probes = {}, {}
+    picks (collective: every rank reaches the same choice from the slowest rank's numbers).
+
+    Every rank runs the same torch process-group sequence whatever happens locally: ONE id
+    broadcast (all ids at once), then ONE MAX all-reduce whose slot 0 is a failure flag. A rank
+    whose communicator creation or probe fails records it, still joins that all-reduce, and every
+    rank then raises together (for_group's MIN vote turns that into a common fallback); a
+    failure can no longer leave one rank in the flag vote while the others sit in a different
+    collective. `make(uid, world, rank, device, max_ctas)` builds a communicator
+    (tests inject failures through it)."""
+    budgets = tuple(budgets) if budgets is not None else (DEFAULT_MAX_CTAS, 0)
+    make = make or (lambda uid, w, r, dev, ctas: RcclCommunicator(uid, w, r, dev, max_ctas=ctas))
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    uids = broadcast_unique_ids(group, len(budgets), dev)
+    comms, probes, why = {}, {}, ""
     try:
-        for ctas in (DEFAULT_MAX_CTAS, 0):
-            c = RcclCommunicator.for_group(group, max_ctas=ctas)
+        for ctas, uid in zip(budgets, uids):
+            c = make(uid, world, rank, dev, ctas)
             comms[ctas] = c
             probes[ctas] = [c.probe(nb, iters=5) for nb in PROBE_BYTES]
-        # identical tables everywhere: the slowest rank's time per (budget, size)
-        t = torch.tensor([d["ms"] for c in (DEFAULT_MAX_CTAS, 0) for d in probes[c]], dtype=torch.float64,
-                         device=comms[0].device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-        i = 0
-        for c in (DEFAULT_MAX_CTAS, 0):
-            for d in probes[c]:
-                d["ms"] = round(float(t[i]), 4)
-                d["busbw_GBps"] = round(2.0 * (world - 1) / world * d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1) \
-                    if d["ms"] > 0 else 0.0
-                i += 1
-        pol = choose_cta_budget(probes, bucket_bytes or [32 << 20], world, overlap_ms)
-    except Exception:
+    except Exception as e:  # noqa: BLE001 - shared through the status slot below
+        why = "%s: %s" % (type(e).__name__, e)
+    n = len(budgets) * len(PROBE_BYTES)
+    t = torch.zeros(1 + n, dtype=torch.float64, device=dev)
+    if why:
+        t[0] = 1.0
+    else:
+        t[1:] = torch.tensor([d["ms"] for c in budgets for d in probes[c]], dtype=torch.float64)
+    # identical tables everywhere: the slowest rank's time per (budget, size), and any failure
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    th = t.cpu()
+    if float(th[0]) > 0:
         for c in comms.values():
             c.destroy(abort=True)
-        raise
+        raise errors.UnavailableError("CTA-budget probe failed %s" % ("on this rank: " + why if why
+                                                                      else "on another rank"))
+    i = 1
+    for c in budgets:
+        for d in probes[c]:
+            d["ms"] = round(float(th[i]), 4)
+            d["busbw_GBps"] = round(2.0 * (world - 1) / world * d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1) \
+                if d["ms"] > 0 else 0.0
+            i += 1
+    pol = choose_cta_budget(probes, bucket_bytes or [32 << 20], world, overlap_ms)
     keep = pol["cta_budget"]
     for ctas, c in comms.items():
         if ctas != keep:

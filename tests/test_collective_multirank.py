@@ -227,3 +227,67 @@ def test_gradient_tape_apply_gradients_matches_big_batch(tmp_path, clip):
         opt.apply_gradients(zip(grads, model.trainable_variables))
     assert flat.names() == res[0]["names"]
     torch.testing.assert_close(res[0]["w"], flat.master, rtol=2e-5, atol=2e-5)
+
+
+class _FakeComm:
+    """Stands in for RcclCommunicator in the CTA-budget probe: fixed probe times per budget,
+    optional failure at a chosen budget."""
+
+    def __init__(self, ctas, fail, ms):
+        if fail:
+            raise RuntimeError("injected communicator failure (budget %d)" % ctas)
+        self.max_ctas, self.ms, self.destroyed = ctas, ms, None
+
+    def probe(self, nbytes, iters=5):
+        return {"bytes": int(nbytes), "ms": self.ms * (1 + nbytes / (64 << 20)), "busbw_GBps": 0.0}
+
+    def destroy(self, abort=False):
+        self.destroyed = "abort" if abort else "finalize"
+
+
+def _probe_worker(rank, world, store, q, fail_rank, fail_budget):
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from tensorflow_train_distributed_amd.parallel import rccl
+    dist.init_process_group("gloo", store=dist.FileStore(store, world), rank=rank, world_size=world)
+    rccl.unique_id = lambda: bytes(range(128))  # no RCCL on the CPU: any 128 bytes
+    made = []
+
+    def make(uid, w, r, dev, ctas):
+        c = _FakeComm(ctas, r == fail_rank and ctas == fail_budget, ms=1.0 + 0.1 * r + (0.5 if ctas else 0.0))
+        made.append(c)
+        return c
+
+    out = {"rank": rank}
+    try:
+        comm = rccl._probe_budgets(None, 40.0, [8 << 20, 32 << 20], make=make)
+        out["budget"] = comm.policy["cta_budget"]
+        out["ms"] = [d["ms"] for d in comm.policy["probe"][comm.policy["cta_budget"]]] \
+            if isinstance(comm.policy.get("probe"), dict) else None
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        out["error"] = "%s: %s" % (type(e).__name__, e)
+    out["destroyed"] = [c.destroyed for c in made]
+    # the process group must still be in step: one more collective completes on every rank
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    out["after"] = float(t.item())
+    q.put(out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank,fail_budget", [(None, None), (1, 0), (0, 8)])
+def test_cta_budget_probe_failure_on_one_rank_fails_every_rank_together(tmp_path, fail_rank, fail_budget):
+    """a communicator / probe failure on one rank must not leave the ranks in
+    different torch collectives. Every rank joins the same id broadcast and the same MAX
+    all-reduce (slot 0 = failure flag), then all raise together, or all pick the same budget."""
+    world = 3
+    res = _spawn(_probe_worker, world, tmp_path, fail_rank, fail_budget)
+    assert all(r["after"] == world for r in res)  # the group is still usable afterwards
+    if fail_rank is None:
+        assert len({r["budget"] for r in res}) == 1 and all("error" not in r for r in res)
+    else:
+        assert all("error" in r and "UnavailableError" in r["error"] for r in res), res
+        assert "this rank" in res[fail_rank]["error"]
+        assert all("another rank" in r["error"] for i, r in enumerate(res) if i != fail_rank)
+        # every communicator a rank did create is aborted
+        assert all(all(d == "abort" for d in r["destroyed"] if d is not None) for r in res)

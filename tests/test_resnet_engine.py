@@ -217,6 +217,29 @@ def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
 
 
 @pytest.mark.gpu
+def test_resnet_fp8_only_input_without_weight_prep():
+    """precision="fp8" with the per-step filter preparation off (TTD_WPREP=0 equivalent): the fp8
+    data gradient of the unit-stride 3x3 convs is then off, but their forward still stores only
+    the fp8 copy of the input (TTD_FP8_ONLY_INPUT), so the backward must take the fp8 weight
+    gradient from a freshly quantised dz instead of asking for the unstored bf16 input (ADVICE r4:
+    this raised from step 2 on). Several steps run; losses stay finite and track the default."""
+    torch.manual_seed(0)
+    stages = ((64, 2, 1), (128, 2, 2), (256, 1, 2))
+    x = torch.randn(16, 64, 64, 3, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (16,), device="cuda", dtype=torch.int32)
+    ref = ResNet(stages, num_classes=10, device="cuda", seed=7, precision="fp8")
+    f8 = ResNet(stages, num_classes=10, device="cuda", seed=7, precision="fp8")
+    f8.wprep = False
+    for _ in range(3):
+        lr_ = float(ref.forward_backward(x, y)[0])
+        l8 = float(f8.forward_backward(x, y)[0])
+        assert l8 == l8 and abs(l8 - lr_) < 0.05 * abs(lr_), (l8, lr_)
+    assert f8._x_unstored, "the fp8-only input path was not exercised"
+    a, b = f8.params.grad, ref.params.grad
+    assert float(torch.dot(a, b) / (a.norm() * b.norm())) > 0.95
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("flag,size,batch", [("fuse_pw", 64, 16), ("fuse_c3", 224, 4)])
 def test_resnet_streaming_pointwise_fusions_match_unfused_engine(flag, size, batch):
     """The BN-prologue fusions on the streaming pointwise kernel (c2 apply -> c3 conv, c3 apply ->
