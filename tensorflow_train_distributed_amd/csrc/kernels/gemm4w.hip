@@ -168,14 +168,63 @@ __device__ __forceinline__ void epilogue(const f32x4_t (&acc)[8][8], const EpiPa
   }
 }
 
-template <int EK>
+template <int N, class F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+
+// read #r of a K-step's 16 fragments in first-use order of the a-major MFMA sweep:
+// r = 0: A block 0; 1..8: B blocks 0..7; 9..15: A blocks 1..7
+constexpr bool rd_is_a(int r) { return r == 0 || r >= 9; }
+constexpr int rd_blk(int r) { return r == 0 ? 0 : (r <= 8 ? r - 1 : r - 8); }
+constexpr int rd_of_a(int a) { return a == 0 ? 0 : 8 + a; }
+constexpr int rd_of_b(int b) { return 1 + b; }
+constexpr int cmax(int x, int y) { return x > y ? x : y; }
+// phase-0 MFMA i = (a, b) = (i / 8, i % 8) needs K-step-0 reads up to need0(i); the K-step-1 reads
+// issued before it (one before every 4th MFMA) are younger: lgkmcnt(15 - need + issued)
+constexpr int need0(int i) { return cmax(rd_of_a(i / 8), rd_of_b(i % 8)); }
+constexpr int lgk0(int i) { return 15 - need0(i) + (i / 4 + 1); }
+
+// acc (+)= x . y^T as inline asm with the accumulator an AGPR operand (FIRST: C = 0)
+template <bool FIRST>
+__device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& x, const bf16x8_t& y) {
+  if constexpr (FIRST)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(y), "v"(x));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(y), "v"(x));
+}
+
+// Tile order: t (consecutive on one XCD after xcd_remap) walks column-major blocks of `group`
+// tile rows, so the ~32 workgroups an XCD runs at once cover a group x (32 / group) block and
+// share both operand panels in that XCD's L2 (row-major order: 1 A panel + 32 B panels per
+// K-tile step, most of them from beyond the L2).
+__device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int group, int& tm, int& tn) {
+  if (group <= 1) {
+    tm = t / tiles_n;
+    tn = t % tiles_n;
+    return;
+  }
+  const int per = group * tiles_n;
+  const int g0 = (t / per) * group;
+  const int gm = min(tiles_m - g0, group);
+  const int r = t - (t / per) * per;
+  tm = g0 + r % gm;
+  tn = r / gm;
+}
+
+template <int EK, int SCHED>
 __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
-                                                     int N, int K, int tiles_m, int tiles_n) {
+                                                     int N, int K, int tiles_m, int tiles_n, int group) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int nblk = tiles_m * tiles_n;
   const int t = xcd_remap(blockIdx.x, nblk);
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int tm_, tn_;
+  tile_of(t, tiles_m, tiles_n, group, tm_, tn_);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -191,7 +240,18 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   const int lk1 = i16 * 128 + (((4 | g) ^ ((i16 >> 1) & 7)) << 4);
   const int aoff = wm * 16384, boff = OPB + wn * 16384;
 
+  // accumulators zeroed in AGPRs up front: the empty "+a" statements pin them there before any
+  // DMA or MFMA asm (all volatile, so the zero writes are far ahead of the first MFMA that reads
+  // them as C); one loop body for every K-tile (a peeled first K-tile with C = 0 made hipcc
+  // place the tiles differently in the two copies and shuffle them with v_accvgpr_mov between)
   f32x4_t acc[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+a"(acc[a][b]));
+    }
   bf16x8_t fa[2][8], fb[2][8];
 
   auto stage = [&](int kt) { return smem + (kt & 1) * STAGE; };
@@ -223,6 +283,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   using F = std::false_type;
   using Tr = std::true_type;
 
+  if constexpr (SCHED == 0) {
   // prologue: K-tiles 0 and 1, wait for 0, read its K-step 0
   if (ktiles > 0) {
     la.issue<0, 8>(stage(0), 0, wave);
@@ -259,8 +320,135 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
     if (has1) read(stage(kt + 1), lk0, fa[0], fb[0]);
     mma(fa[1], fb[1], 4, 8, F{});
   };
-  ktile(0, Tr{});
-  for (int kt = 1; kt < ktiles; ++kt) ktile(kt, F{});
+  for (int kt = 0; kt < ktiles; ++kt) ktile(kt, F{});
+  } else {
+  // SCHED 1: the whole main loop as inline asm in a fixed issue order (hipcc grouped all 16
+  // fragment reads and all 16 DMA pieces of a phase in front of its MFMAs; with one wave per
+  // SIMD nothing else fills the MFMA pipe while they issue):
+  //   phase 0: one fragment read before every 4th MFMA, graduated lgkmcnt for the K-step-0
+  //            fragments still in flight (lgk0);
+  //   phase 1a: one DMA piece before every 2nd MFMA; phase 1b: one fragment read before every
+  //            2nd MFMA. LDS reads and DMA are counted by hand (hipcc does not count asm).
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
+  uint32_t va[2][2], vb[2][2];  // [stage][K-step] fragment base addresses (block offsets immediate)
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    va[st][0] = sb + st * STAGE + wm * 16384 + lk0;
+    va[st][1] = sb + st * STAGE + wm * 16384 + lk1;
+    vb[st][0] = sb + st * STAGE + OPB + wn * 16384 + lk0;
+    vb[st][1] = sb + st * STAGE + OPB + wn * 16384 + lk1;
+  }
+  const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
+  auto rd1 = [&](auto R, uint32_t a_base, uint32_t b_base, bf16x8_t (&xa)[8], bf16x8_t (&xb)[8]) {
+    constexpr int r = decltype(R)::value;
+    if constexpr (rd_is_a(r))
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(xa[rd_blk(r)]) : "v"(a_base), "i"(rd_blk(r) * 2048));
+    else
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(xb[rd_blk(r)]) : "v"(b_base), "i"(rd_blk(r) * 2048));
+  };
+  // DMA piece q (0..7 A, 8..15 B) of K-tile kt into stage st
+  auto dma1 = [&](auto Q, int st, int kt) {
+    constexpr int q = decltype(Q)::value;
+    const LoadK& L = q < 8 ? la : lb;
+    const uint32_t m0v = ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096;
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(m0v), "v"(L.voff[q & 7]), "s"(L.srd), "s"(kt * 128)
+        : "memory");
+  };
+  auto mfma1 = [&](int a, int b, const bf16x8_t& x, const bf16x8_t& y, auto first) {
+    mfma_acc<decltype(first)::value>(acc[a][b], x, y);
+  };
+  // prologue: K-tiles 0 and 1, wait for 0, K-step-0 fragments of K-tile 0
+  static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
+  if (ktiles > 1) {
+    static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
+    asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
+  if constexpr (SCHED >= 6) {
+    // DIAGNOSTIC schedules (wrong results; timing only, tools/g4_bench.py): 9 = the 128 MFMAs
+    // per K-tile alone, 8 = MFMAs + the 32 fragment reads, 7 = MFMAs + the 16 DMA pieces,
+    // 6 = MFMAs + reads + DMA without any barrier (waits lag one K-tile / one half)
+    for (int kt = 0; kt < ktiles; ++kt) {
+      const int st = kt & 1;
+      static_for<128>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if constexpr ((SCHED == 8 || SCHED == 6) && i % 4 == 0)
+          rd1(std::integral_constant<int, (i / 4) % 16>{}, va[st][i / 64], vb[st][i / 64], fa[1 - i / 64], fb[1 - i / 64]);
+        if constexpr ((SCHED == 7 || SCHED == 6) && i % 8 == 2) dma1(std::integral_constant<int, i / 8>{}, st, kt);
+        if constexpr ((SCHED == 8 || SCHED == 6) && i == 63) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        mfma1((i / 8) % 8, i % 8, fa[i / 64][(i / 8) % 8], fb[i / 64][i % 8], F{});
+      });
+      if constexpr (SCHED == 8 || SCHED == 6) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      if constexpr (SCHED == 7 || SCHED == 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    }
+  } else {
+  auto ktile = [&](int kt, auto first) {
+    const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
+    const int st = kt & 1;
+    // phase 0
+    static_for<64>([&](auto I) {
+      constexpr int i = decltype(I)::value, a = i / 8, b = i % 8;
+      if constexpr (i % 4 == 0) rd1(std::integral_constant<int, i / 4>{}, va[st][1], vb[st][1], fa[1], fb[1]);
+      if constexpr (i == 0 || need0(i) > need0(i - 1 < 0 ? 0 : i - 1))
+        if constexpr (SCHED != 5) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(lgk0(i)) : "memory");
+      mfma1(a, b, fa[0][a], fb[0][b], first);
+    });
+    if constexpr (SCHED == 3) {
+      // one barrier per K-tile: this stage is free AND K-tile kt + 1 has landed; then the 16
+      // DMA pieces of kt + 2 and the 16 K-step-0 reads of kt + 1 alternate, one every 2 MFMAs
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      static_for<64>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if constexpr (i % 4 == 0)
+          if (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
+        if constexpr (i % 4 == 2)
+          rd1(std::integral_constant<int, i / 4>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
+        mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
+      });
+    } else {
+      if constexpr (SCHED == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else if constexpr (SCHED == 5) asm volatile("s_barrier" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // phase 1a: K-tile kt + 2 into this stage (the MFMA sequence is never duplicated per
+      // branch: with the MFMAs inside if / else copies hipcc allocated the accumulators
+      // differently per copy and shuffled them with unpadded v_accvgpr_mov between).
+      // SCHED 1: all 16 pieces in the first 32 MFMAs; SCHED 2: 8 here, 8 in phase 1b.
+      // (diagnostics: 4 = SCHED 2 without barriers, 5 = SCHED 2 without LDS-read waits)
+      constexpr int DSTEP = SCHED == 1 ? 2 : 4;
+      static_for<32>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if constexpr (i % DSTEP == 0)
+          if (has2) dma1(std::integral_constant<int, i / DSTEP>{}, st, kt + 2);
+        mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
+      });
+      if (has2) {
+        if constexpr (SCHED == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if constexpr (SCHED != 4) asm volatile("s_barrier" ::: "memory");
+      // phase 1b: K-step-0 fragments of K-tile kt + 1 (read unconditionally: past the last
+      // K-tile they are never used)
+      static_for<32>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if constexpr (SCHED != 1 && i % 4 == 1)
+          if (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
+        if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
+        mfma1(4 + i / 8, i % 8, fa[1][4 + i / 8], fb[1][i % 8], F{});
+      });
+    }
+  };
+  for (int kt = 0; kt < ktiles; ++kt) ktile(kt, F{});
+  }
+  }
   // the last MFMAs' results -> the epilogue's v_accvgpr_read: XDL write -> read wait states
   // (hipcc pads nothing after asm); the empty "+a" statements order every read after the pad
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
@@ -274,9 +462,390 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   else epilogue<EK, true>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
 }
 
+// DIAGNOSTIC (timing only, wrong results): the 4-wave tile on v_mfma_f32_32x32x16_bf16 (4 x 4
+// tiles of 32 x 32 per wave, 16 accumulator AGPRs each; per K-tile 64 MFMAs of 32 cycles, 32
+// fragment reads, 16 DMA pieces). MODE 9: MFMAs only; 8: + reads (one per 2 MFMAs); 7: + DMA
+// (one per 4 MFMAs); 6: both. Measures whether the wider MFMA gaps hide the reads / DMA.
+__device__ __forceinline__ void mfma32(f32x16_t& c, const bf16x8_t& x, const bf16x8_t& y) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(y), "v"(x));
+}
+
+__device__ __forceinline__ void ds_w128(uint32_t a, const ttd_i32x4_t& v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void buf_ld16(ttd_i32x4_t& d, uint32_t voff, const ttd_i32x4_t& srd, int soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(srd), "s"(soff));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(T, 1) void g4diag32_kernel(const bf16_t* __restrict__ A, long long lda,
+                                                       const bf16_t* __restrict__ B, long long ldb, bf16_t* out,
+                                                       int M, int N, int K, int tiles_m, int tiles_n, int group) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int nblk = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  int tm_, tn_;
+  tile_of(t, tiles_m, tiles_n, group, tm_, tn_);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ktiles = K / 64;
+  LoadK la, lb;
+  la.init(A, lda, M, m0, tid);
+  lb.init(B, ldb, N, n0, tid);
+  const int r32 = lane & 31, h = lane >> 5;
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
+  uint32_t vk[4];  // per K-step s: lane offset of chunk 2s + h in row r32 (block offsets immediate)
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) vk[s4] = sb + r32 * 128 + ((((2 * s4 + h) ^ ((r32 >> 1) & 7))) << 4);
+  const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
+  f32x16_t acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      acc[a][b] = f32x16_t{};
+      asm volatile("" : "+a"(acc[a][b]));
+    }
+  bf16x8_t fa[2][4], fb[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      fa[j][a] = bf16x8_t{};
+      fb[j][a] = bf16x8_t{};
+    }
+  auto dma1 = [&](auto Q, int st, int kt) {
+    constexpr int q = decltype(Q)::value;
+    const LoadK& L = q < 8 ? la : lb;
+    const uint32_t m0v = ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096;
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(m0v), "v"(L.voff[q & 7]), "s"(L.srd), "s"(kt * 128)
+        : "memory");
+  };
+  ttd_i32x4_t stg[4] = {};
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int st = kt & 1;
+    if constexpr (MODE == 17) asm volatile("s_waitcnt vmcnt(0)" ::"v"(stg[0]), "v"(stg[1]), "v"(stg[2]), "v"(stg[3]) : "memory");
+    if constexpr (MODE >= 10) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    static_for<64>([&](auto I) {
+      constexpr int i = decltype(I)::value, s4 = i / 16, a = (i / 4) % 4, b = i % 4;
+      // reads per burst: 1 (modes 8, 6, 10: one every 2 MFMAs), 2 (11), 4 (12), 8 (13)
+      constexpr int BURST = MODE == 11 ? 2 : (MODE == 12 ? 4 : (MODE >= 13 ? 8 : 1));
+      constexpr bool RD = (MODE == 6 || MODE == 8 || MODE >= 10) && (i % (2 * BURST)) < BURST;
+      if constexpr (RD) {
+        constexpr int r = ((i / (2 * BURST)) * BURST + (i % (2 * BURST))) % 8;  // A blocks 0..3, B 0..3
+        constexpr int nxt = (s4 + 1) & 3;
+        const uint32_t base = vk[nxt] + st * STAGE + (r < 4 ? wm * 16384 : OPB + wn * 16384);
+        if constexpr (r < 4)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[(s4 + 1) & 1][r]) : "v"(base), "i"(r * 4096));
+        else
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[(s4 + 1) & 1][r - 4]) : "v"(base), "i"((r - 4) * 4096));
+      }
+      if constexpr ((MODE == 7 || MODE == 6 || MODE == 15) && i % 4 == 1) dma1(std::integral_constant<int, i / 4>{}, st, kt);
+      // 16: + 4 ds_write_b128 per K-step (burst, register data): LDS write contention alone
+      if constexpr (MODE == 16 && i % 16 == 7) {
+        static_for<4>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          const uint32_t wa = sb + st * STAGE + ((i / 16) * 4 + j) * 4096 + tid * 16;
+          ds_w128(wa, stg[j]);
+        });
+      }
+      // 17: + 4 buffer_load_dwordx4 into registers per K-step (burst): the VMEM issue alone
+      if constexpr (MODE == 17 && i % 16 == 7) {
+        static_for<4>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          constexpr int q = (i / 16) * 4 + j;
+          const LoadK& L = q < 8 ? la : lb;
+          buf_ld16(stg[j], L.voff[q & 7], L.srd, kt * 128);
+        });
+      }
+      // 14: 4 DMA pieces in a burst right after each K-step's read burst
+      if constexpr (MODE == 14 && i % 16 == 7) {
+        dma1(std::integral_constant<int, (i / 16) * 4 + 0>{}, st, kt);
+        dma1(std::integral_constant<int, (i / 16) * 4 + 1>{}, st, kt);
+        dma1(std::integral_constant<int, (i / 16) * 4 + 2>{}, st, kt);
+        dma1(std::integral_constant<int, (i / 16) * 4 + 3>{}, st, kt);
+      }
+      if constexpr ((MODE == 8 || MODE == 6) && i % 16 == 15) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+      mfma32(acc[a][b], fa[s4 & 1][a], fb[s4 & 1][b]);
+    });
+    if constexpr (MODE == 7 || MODE == 6 || MODE == 14 || MODE == 15) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  float sum = 0.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      asm volatile("" : "+a"(acc[a][b]));
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sum += acc[a][b][j];
+    }
+  if (sum == 12345.f) out[0] = 1;  // keep the accumulators live
+}
+
+// ============================================================================================
+// gemm4v: the production form. Same 256 x 256 tile, 4 waves, AGPR accumulators, but
+//  * v_mfma_f32_32x32x16_bf16 (4 x 4 tiles of 32 x 32 per wave): 32-cycle MFMA gaps leave ~24
+//    issue cycles each for the loads / LDS traffic of a one-wave-per-SIMD loop;
+//  * operands staged global -> VGPRs (buffer_load_dwordx4, two register sets) -> LDS
+//    (ds_write_b128) instead of LDS-DMA: measured on the diagnostic loop, 16 DMA pieces next to
+//    32 fragment reads per K-tile cost 25 % of the MFMA rate, loads + writes ~7 %;
+//  * per K-tile (4 K-steps of 16 MFMAs): each K-step opens with a burst of the next K-step's 8
+//    fragment reads (bursts measured faster than reads spread one per MFMA gap); K-tile kt + 2's
+//    loads go out in K-steps 0-1, K-tile kt + 1's registers are written to the other LDS stage
+//    in K-step 2, one barrier, then K-step 3 reads K-tile kt + 1's first fragments.
+// K-tiles per launch must be even (the loop body is two K-tiles: static register-set indices).
+
+template <class OFF>
+__device__ __forceinline__ void ld_frag(bf16x8_t& d, uint32_t base, OFF) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(OFF::value));
+}
+
+template <int EK, bool CHECK>
+__device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[4][4], const EpiParams& E, int m0, int n0, int M,
+                                           int N, float alpha, int lane, int wm, int wn) {
+  // acc[a][b][r] = C[m0 + wm*128 + a*32 + (lane & 31)][n0 + wn*128 + b*32 + 4h + 8(r >> 2) + (r & 3)], h = lane >> 5.
+  // Column groups j = r >> 2 (4 columns each): lanes h = 0 / 1 swap groups (1 <-> 0) and (3 <-> 2)
+  // through v_permlane32_swap so each lane stores 8 consecutive columns (16 B) twice per block.
+  const int r32 = lane & 31, h = lane >> 5;
+  bf16_t* const out = static_cast<bf16_t*>(E.out);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int m = m0 + wm * 128 + a * 32 + r32;
+    const bool mok = !CHECK || m < M;
+    const long long row = static_cast<long long>(m) * E.ldo;
+    const long long rrow = static_cast<long long>(m) * E.ldr;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int nb = n0 + wn * 128 + b * 32 + 4 * h;
+      uint32_t po[4][2], pa[4][2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + 8 * j;
+        const bool ok = mok && (!CHECK || n < N);
+        f32x4_t v = {acc[a][b][4 * j], acc[a][b][4 * j + 1], acc[a][b][4 * j + 2], acc[a][b][4 * j + 3]};
+        v *= alpha;
+        if constexpr ((EK & kEkBias) != 0)
+          if (!CHECK || n < N) v += *reinterpret_cast<const f32x4_t*>(E.bias + n);
+        if constexpr ((EK & kEkDGelu) != 0) {
+          uint2 rv = make_uint2(0, 0);
+          if (ok) rv = *reinterpret_cast<const uint2*>(E.residual + rrow + n);
+          v[0] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.x & 0xffff)));
+          v[1] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.x >> 16)));
+          v[2] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.y & 0xffff)));
+          v[3] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.y >> 16)));
+        }
+        if constexpr ((EK & kEkBeta) != 0) {
+          uint2 ov = make_uint2(0, 0);
+          if (ok) ov = *reinterpret_cast<const uint2*>(out + row + n);
+          v[0] += bf2f(static_cast<bf16_t>(ov.x & 0xffff));
+          v[1] += bf2f(static_cast<bf16_t>(ov.x >> 16));
+          v[2] += bf2f(static_cast<bf16_t>(ov.y & 0xffff));
+          v[3] += bf2f(static_cast<bf16_t>(ov.y >> 16));
+        }
+        if constexpr ((EK & kEkAux) != 0) {
+          pa[j][0] = pack_bf16x2(v[0], v[1]);
+          pa[j][1] = pack_bf16x2(v[2], v[3]);
+        }
+        if constexpr ((EK & kEkGelu) != 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = gelu_tanh(v[q]);
+        }
+        po[j][0] = pack_bf16x2(v[0], v[1]);
+        po[j][1] = pack_bf16x2(v[2], v[3]);
+      }
+      // (X, Y) = groups (2i, 2i + 1): after the swap lane h = 0 holds columns 16i + 0..7 (its X and
+      // h = 1's X), lane h = 1 columns 16i + 8..15 (h = 0's Y and its Y)
+      auto store2 = [&](uint32_t (&p)[4][2], bf16_t* base) {
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2) {
+          uint32_t x0 = p[2 * i2][0], x1 = p[2 * i2][1], y0 = p[2 * i2 + 1][0], y1 = p[2 * i2 + 1][1];
+          const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+          x0 = s0[0]; y0 = s0[1]; x1 = s1[0]; y1 = s1[1];
+          const int n = n0 + wn * 128 + b * 32 + 16 * i2 + 8 * h;
+          if (mok && (!CHECK || n < N))
+            *reinterpret_cast<uint4*>(base + row + n) = make_uint4(x0, x1, y0, y1);
+        }
+      };
+      store2(po, out);
+      if constexpr ((EK & kEkAux) != 0) store2(pa, E.aux);
+    }
+  }
+}
+
+__device__ __forceinline__ void vload16(ttd_i32x4_t& d, uint32_t voff, const ttd_i32x4_t& srd, int soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(srd), "s"(soff));
+}
+template <int OFF>
+__device__ __forceinline__ void vstore_lds(uint32_t a, const ttd_i32x4_t& v) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(OFF) : "memory");
+}
+
+template <int EK>
+__global__ __launch_bounds__(T, 1) void gemm4v_kernel(const bf16_t* __restrict__ A, long long lda,
+                                                     const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
+                                                     int N, int K, int tiles_m, int tiles_n, int group) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int nblk = tiles_m * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  int tm_, tn_;
+  tile_of(t, tiles_m, tiles_n, group, tm_, tn_);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ktiles = K / 64;
+
+  LoadK la, lb;
+  la.init(A, lda, M, m0, tid);
+  lb.init(B, ldb, N, n0, tid);
+  const int r32 = lane & 31, h = lane >> 5;
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
+  // fragment bases [stage][K-step]: row r32, chunk 2s + h XOR (r32 >> 1) & 7; blocks (32 rows,
+  // 4096 B) are immediate offsets
+  uint32_t fA[2][4], fB[2][4];
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const uint32_t l = r32 * 128 + ((((2 * s4 + h) ^ ((r32 >> 1) & 7))) << 4);
+      fA[st][s4] = sb + st * STAGE + wm * 16384 + l;
+      fB[st][s4] = sb + st * STAGE + OPB + wn * 16384 + l;
+    }
+  const uint32_t wbase = sb + tid * 16;  // ds_write of piece q: + stage + (q < 8 ? 0 : OPB) + (q & 7) * 4096
+
+  f32x16_t acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      acc[a][b] = f32x16_t{};
+      asm volatile("" : "+a"(acc[a][b]));
+    }
+  bf16x8_t fa[2][4], fb[2][4];
+  ttd_i32x4_t S0[16], S1[16];
+
+  auto loads = [&](ttd_i32x4_t (&S)[16], int kt, auto Q0) {  // pieces Q0 .. Q0 + 7 of K-tile kt
+    constexpr int q0 = decltype(Q0)::value;
+    static_for<8>([&](auto J) {
+      constexpr int q = q0 + decltype(J)::value;
+      const LoadK& L = q < 8 ? la : lb;
+      vload16(S[q], L.voff[q & 7], L.srd, kt * 128);
+    });
+  };
+  auto writes = [&](const ttd_i32x4_t (&S)[16], uint32_t stage_off) {
+    static_for<16>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      vstore_lds<(q < 8 ? 0 : OPB) + (q & 7) * 4096>(wbase + stage_off, S[q]);
+    });
+  };
+  auto reads = [&](int st, auto S4, bf16x8_t (&xa)[4], bf16x8_t (&xb)[4]) {
+    constexpr int s4 = decltype(S4)::value;
+    static_for<4>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      ld_frag(xa[j], fA[st][s4], std::integral_constant<int, j * 4096>{});
+    });
+    static_for<4>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      ld_frag(xb[j], fB[st][s4], std::integral_constant<int, j * 4096>{});
+    });
+  };
+  auto mma16 = [&](const bf16x8_t (&xa)[4], const bf16x8_t (&xb)[4]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mfma32(acc[a][b], xa[a], xb[b]);
+  };
+
+  // prologue: K-tiles 0 and 1 into the register sets, K-tile 0 into LDS stage 0
+  loads(S0, 0, std::integral_constant<int, 0>{});
+  loads(S0, 0, std::integral_constant<int, 8>{});
+  if (ktiles > 1) {
+    loads(S1, 1, std::integral_constant<int, 0>{});
+    loads(S1, 1, std::integral_constant<int, 8>{});
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  writes(S0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  reads(0, std::integral_constant<int, 0>{}, fa[0], fb[0]);
+
+  // one K-tile; P = kt & 1 (compile time): tile kt in LDS stage P and register set P (now
+  // free), tile kt + 1 in register set P ^ 1
+  auto ktile = [&](int kt, auto PAR, ttd_i32x4_t (&Sp)[16], ttd_i32x4_t (&Sq)[16]) {
+    constexpr int P = decltype(PAR)::value;
+    const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
+    // K-step 0
+    reads(P, std::integral_constant<int, 1>{}, fa[1], fb[1]);
+    if (has2) loads(Sp, kt + 2, std::integral_constant<int, 0>{});
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+    mma16(fa[0], fb[0]);
+    // K-step 1
+    reads(P, std::integral_constant<int, 2>{}, fa[0], fb[0]);
+    if (has2) loads(Sp, kt + 2, std::integral_constant<int, 8>{});
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+    mma16(fa[1], fb[1]);
+    // K-step 2: K-tile kt + 1 -> the other stage
+    reads(P, std::integral_constant<int, 3>{}, fa[1], fb[1]);
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // K-step 2's fragments (older than the 8 reads)
+    if (has1) {
+      if (has2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      writes(Sq, (P ^ 1) * STAGE);
+    }
+    mma16(fa[0], fb[0]);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // K-step 3: first fragments of K-tile kt + 1 (read unconditionally: unused past the end)
+    reads(P ^ 1, std::integral_constant<int, 0>{}, fa[0], fb[0]);
+    mma16(fa[1], fb[1]);
+  };
+  for (int kt = 0; kt < ktiles; kt += 2) {
+    ktile(kt, std::integral_constant<int, 0>{}, S0, S1);
+    ktile(kt + 1, std::integral_constant<int, 1>{}, S1, S0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) asm volatile("" : "+a"(acc[a][b]));
+  const float alpha = epi_alpha(E);
+  if (m0 + BM <= M && n0 + BN <= N) epilogue32<EK, false>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
+  else epilogue32<EK, true>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
+}
+
 }  // namespace g4
 }  // namespace
 }  // namespace ttdk
+
+// TTD_G4_SCHED: 1 (default) = asm-scheduled main loop, 0 = compiler-scheduled (A/B, tests)
+static int& g4_sched() {
+  static int v = ttdk::getenv_int("TTD_G4_SCHED", 1);
+  return v;
+}
+// TTD_G4_GROUP: tile rows per column-major tile block (1 = row-major order)
+static int& g4_group() {
+  static int v = ttdk::getenv_int("TTD_G4_GROUP", 8);
+  return v;
+}
+TTDK_EXPORT int ttdk_set_g4_group(int v) {
+  const int old = g4_group();
+  g4_group() = v;
+  return old;
+}
+TTDK_EXPORT int ttdk_set_g4_sched(int v) {
+  const int old = g4_sched();
+  g4_sched() = v;
+  return old;
+}
 
 // C[M,N] = epilogue(alpha * A . B^T), A [M][K] (lda), B [N][K] (ldb) bf16 K-major; K % 64 == 0,
 // N % 8 == 0, ldo % 8 == 0, 16-B aligned operands and outputs. Returns hipErrorInvalidValue for
@@ -300,10 +869,35 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
   if (pe.beta) ek |= g4::kEkBeta;
   if (pe.aux) ek |= g4::kEkAux;
   const int tm = ceil_div(M, g4::BM), tn = ceil_div(N, g4::BN);
-#define TTDK_G4(EKV)                                                                                             \
-  case EKV:                                                                                                      \
-    hipLaunchKernelGGL((g4::gemm4w_kernel<EKV>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M, N, K, \
-                       tm, tn);                                                                                  \
+  const int sched = g4_sched();
+  const int group = g4_group();
+#define TTDK_G4(EKV)                                                                                        \
+  case EKV:                                                                                                 \
+    switch (sched) {                                                                                        \
+      case 0: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 0>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 2: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 3: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 3>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 4: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 4>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                   \
+      case 5: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 5>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                   \
+      case 6: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 6>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 7: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 7>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 8: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 8>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 9: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 9>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
+                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 20: if (K % 128) return hipErrorInvalidValue;                                                   \
+               hipLaunchKernelGGL((g4::gemm4v_kernel<EKV>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb,   \
+                                  pe, M, N, K, tm, tn, group); break;                                        \
+      default: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 1>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda,   \
+                                  B, ldb, pe, M, N, K, tm, tn, group); break;                                      \
+    }                                                                                                       \
     return hipGetLastError();
   switch (ek) {
     TTDK_G4(0)
@@ -315,4 +909,27 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
   }
 #undef TTDK_G4
   return hipErrorInvalidValue;
+}
+
+// diagnostic entry (tools/g4_bench.py arms d32:MODE): the 32x32x16 MFMA form of the main loop
+TTDK_EXPORT int ttdk_g4diag32(int mode, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* out,
+                              int M, int N, int K, hipStream_t st) {
+  using namespace ttdk;
+  const int tm = ceil_div(M, g4::BM), tn = ceil_div(N, g4::BN);
+  const int group = g4_group();
+  switch (mode) {
+    case 6: hipLaunchKernelGGL((g4::g4diag32_kernel<6>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 7: hipLaunchKernelGGL((g4::g4diag32_kernel<7>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 10: hipLaunchKernelGGL((g4::g4diag32_kernel<10>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 11: hipLaunchKernelGGL((g4::g4diag32_kernel<11>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 12: hipLaunchKernelGGL((g4::g4diag32_kernel<12>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 13: hipLaunchKernelGGL((g4::g4diag32_kernel<13>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 14: hipLaunchKernelGGL((g4::g4diag32_kernel<14>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 15: hipLaunchKernelGGL((g4::g4diag32_kernel<15>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 16: hipLaunchKernelGGL((g4::g4diag32_kernel<16>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 17: hipLaunchKernelGGL((g4::g4diag32_kernel<17>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    case 8: hipLaunchKernelGGL((g4::g4diag32_kernel<8>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+    default: hipLaunchKernelGGL((g4::g4diag32_kernel<9>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
+  }
+  return hipGetLastError();
 }

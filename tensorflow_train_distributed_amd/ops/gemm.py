@@ -152,7 +152,20 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
     return out
 
 
-_lib.register({"ttdk_gemm4w_bf16": [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.E, _lib.P]})
+_lib.register({"ttdk_gemm4w_bf16": [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.E, _lib.P],
+               "ttdk_set_g4_sched": [_lib.I], "ttdk_set_g4_group": [_lib.I]})
+
+
+def set_g4_group(v: int) -> int:
+    """Tile rows per column-major tile block of the 4-wave GEMM's tile order (1 = row-major).
+    Returns the previous setting."""
+    return int(_lib.query("ttdk_set_g4_group", int(v)))
+
+
+def set_g4_sched(v: int) -> int:
+    """Main-loop schedule of the 4-wave GEMM: 1 = hand-ordered inline asm (default), 0 = the
+    compiler-scheduled form (A/B and tests). Returns the previous setting."""
+    return int(_lib.query("ttdk_set_g4_sched", int(v)))
 
 
 def gemm4w(a, b, *, out=None, bias=None, act=ACT_NONE, residual=None, beta=0, alpha=1.0, aux=None):

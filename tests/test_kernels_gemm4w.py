@@ -15,12 +15,20 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-SHAPES = [(256, 256, 64), (512, 512, 128), (1000, 264, 320), (300, 1000, 1024), (4096, 4096, 1024),
-          (2048, 1024, 4096), (65, 8, 64)]
+SHAPES = [(256, 256, 128), (512, 512, 128), (1000, 264, 384), (300, 1000, 1024), (4096, 4096, 1024),
+          (2048, 1024, 4096), (65, 8, 128)]
+
+
+@pytest.fixture(params=[20, 1, 2, 3, 0], ids=["vstage32", "asm_sched1", "asm_sched2", "asm_sched3", "compiler_sched"])
+def sched(request):
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    old = G.set_g4_sched(request.param)
+    yield request.param
+    G.set_g4_sched(old)
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_gemm4w_plain_vs_fp32(M, N, K):
+def test_gemm4w_plain_vs_fp32(M, N, K, sched):
     from tensorflow_train_distributed_amd.ops import gemm as G
     torch.manual_seed(M + N + K)
     a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
@@ -34,8 +42,8 @@ def test_gemm4w_plain_vs_fp32(M, N, K):
         assert torch.equal(G.gemm4w(eye, b), (eye.float() @ b.float().t()).bfloat16())
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 264, 320), (4096, 4096, 1024)])
-def test_gemm4w_epilogues_vs_fp32(M, N, K):
+@pytest.mark.parametrize("M,N,K", [(1000, 264, 384), (4096, 4096, 1024)])
+def test_gemm4w_epilogues_vs_fp32(M, N, K, sched):
     from tensorflow_train_distributed_amd.ops import gemm as G
     torch.manual_seed(7)
     a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
@@ -61,7 +69,7 @@ def test_gemm4w_epilogues_vs_fp32(M, N, K):
     assert _rel(o, acc + old.float()) < 8e-3
 
 
-def test_gemm4w_strided_operands():
+def test_gemm4w_strided_operands(sched):
     """Column slices of a fused buffer as operands (row stride = leading dimension)."""
     from tensorflow_train_distributed_amd.ops import gemm as G
     torch.manual_seed(3)

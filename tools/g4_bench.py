@@ -18,7 +18,7 @@ def arg(name, default):
 T = int(arg("--tokens", "65536"))
 ONLY = arg("--only", None)
 ROUNDS = int(arg("--rounds", "3"))
-ARMS = arg("--arms", "g4,big,torch").split(",")
+ARMS = arg("--arms", "g4:1,g4:2,g4:3,g4:0,big,torch").split(",")
 SHAPES = [  # (name, M, N, K, epilogue)
     ("sq4096", 4096, 4096, 4096, ""),
     ("sq8192", 8192, 8192, 8192, ""),
@@ -57,11 +57,22 @@ def main():
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         b16 = bias.bfloat16() if bias is not None else None
         arms = {
-            "g4": lambda: G.gemm4w(a, b, out=out, bias=bias, act=act, residual=res, aux=aux),
             "big": lambda: G.gemm(a, b, trans_b=True, out=out, bias=bias, act=act, residual=res, aux=aux),
             "torch": (lambda: torch.addmm(b16, a, b.t(), out=out)) if b16 is not None
             else (lambda: torch.mm(a, b.t(), out=out)),
         }
+        for k in ARMS:
+            if k.startswith("d32:"):  # diagnostic 32x32x16 main loop (timing only)
+                from tensorflow_train_distributed_amd.ops import _lib
+                _lib.register({"ttdk_g4diag32": [_lib.I, _lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.I, _lib.I,
+                                                 _lib.I, _lib.P]})
+                arms[k] = (lambda v: lambda: _lib.call("ttdk_g4diag32", v, a.data_ptr(), K, b.data_ptr(), K,
+                                                       out.data_ptr(), M, N, K, _lib.stream()))(int(k[4:]))
+            if k.startswith("g4:"):  # g4:SCHED[/GROUP]
+                sv, _, gv = k[3:].partition("/")
+                arms[k] = (lambda v, gr: lambda: (G.set_g4_sched(v), G.set_g4_group(gr),
+                                                  G.gemm4w(a, b, out=out, bias=bias, act=act, residual=res, aux=aux)))(
+                    int(sv), int(gv or 8))
         fl = 2.0 * M * N * K
         res_t = {k: [] for k in ARMS}
         for _ in range(ROUNDS):
