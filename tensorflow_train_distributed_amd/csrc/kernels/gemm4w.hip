@@ -104,66 +104,97 @@ using big::kEkAux;
 using big::kEkGelu;
 
 // Register epilogue: acc[a][b] = C[m0 + wm*128 + a*16 + (lane & 15)][n0 + wn*128 + b*16 + 4*(lane >> 4) + v].
-// Lanes g and g ^ 1 (g = lane >> 4) swap halves of the column-block pair (2p, 2p + 1) so each lane
-// stores 8 consecutive columns (16 B).
+// Lanes g and g ^ 1 (g = lane >> 4) swap halves of the column-block pair (2p, 2p + 1) with ONE
+// v_permlane16_swap per packed dword so each lane stores 8 consecutive columns (16 B): 16 rows
+// x 64 B per store instruction. Measured with in-kernel stamps, the first form of this epilogue
+// (a ds_bpermute round trip per exchange, one dependent bias / residual load per 4 columns) took
+// 23k cycles per tile for bias + store alone, half the K = 1024 main loop: now the bias of the
+// wave's 128 columns is loaded once (8 x 16 B) and residual / old-output loads run one row block
+// ahead of the arithmetic.
 template <int EK, bool CHECK>
 __device__ __forceinline__ void epilogue(const f32x4_t (&acc)[8][8], const EpiParams& E, int m0, int n0, int M, int N,
                                          float alpha, int lane, int wm, int wn) {
   const int g = lane >> 4, i16 = lane & 15;
   const bool odd = g & 1;
   bf16_t* const out = static_cast<bf16_t*>(E.out);
+  const int ncol = n0 + wn * 128 + 4 * g;  // column of block b = ncol + 16 b
+  f32x4_t bias[8];
+  if constexpr ((EK & kEkBias) != 0) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+      bias[b] = (!CHECK || ncol + 16 * b < N) ? *reinterpret_cast<const f32x4_t*>(E.bias + ncol + 16 * b)
+                                              : f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr bool LD = (EK & (kEkDGelu | kEkBeta)) != 0;
+  uint2 ldv[2][8];  // [row-block parity][b]: residual (dGELU) or old output (beta), one row block ahead
+  auto load_rows = [&](int a, uint2 (&v)[8]) {
+    const int m = m0 + wm * 128 + a * 16 + i16;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int n = ncol + 16 * b;
+      v[b] = make_uint2(0, 0);
+      if (!CHECK || (m < M && n < N)) {
+        if constexpr ((EK & kEkDGelu) != 0)
+          v[b] = *reinterpret_cast<const uint2*>(E.residual + static_cast<long long>(m) * E.ldr + n);
+        else if constexpr ((EK & kEkBeta) != 0)
+          v[b] = *reinterpret_cast<const uint2*>(out + static_cast<long long>(m) * E.ldo + n);
+      }
+    }
+  };
+  if constexpr (LD) load_rows(0, ldv[0]);
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
+    if constexpr (LD)
+      if (a + 1 < 8) load_rows(a + 1, ldv[(a + 1) & 1]);
     const int m = m0 + wm * 128 + a * 16 + i16;
-    if (CHECK && m >= M) continue;
+    const bool mok = !CHECK || m < M;
     const long long row = static_cast<long long>(m) * E.ldo;
-    const long long rrow = static_cast<long long>(m) * E.ldr;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const int nb = n0 + wn * 128 + p * 32 + 4 * g;  // block b = 2p + j: columns nb + 16 j
-      uint2 po[2], pa[2];
+      uint32_t po[2][2], pa[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int n = nb + 16 * j;
-        f32x4_t v = acc[a][2 * p + j] * alpha;
-        if constexpr ((EK & kEkBias) != 0)
-          if (!CHECK || n < N) v += *reinterpret_cast<const f32x4_t*>(E.bias + n);
-        if constexpr ((EK & kEkDGelu) != 0) {
-          uint2 rv = make_uint2(0, 0);
-          if (!CHECK || n < N) rv = *reinterpret_cast<const uint2*>(E.residual + rrow + n);
-          v[0] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.x & 0xffff)));
-          v[1] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.x >> 16)));
-          v[2] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.y & 0xffff)));
-          v[3] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.y >> 16)));
+        const int b = 2 * p + j;
+        f32x4_t v = acc[a][b] * alpha;
+        if constexpr ((EK & kEkBias) != 0) v += bias[b];
+        if constexpr (LD) {
+          const uint2 w = ldv[a & 1][b];
+          const float x0 = bf2f(static_cast<bf16_t>(w.x & 0xffff)), x1 = bf2f(static_cast<bf16_t>(w.x >> 16));
+          const float x2 = bf2f(static_cast<bf16_t>(w.y & 0xffff)), x3 = bf2f(static_cast<bf16_t>(w.y >> 16));
+          if constexpr ((EK & kEkDGelu) != 0) {
+            v[0] *= gelu_tanh_grad(x0);
+            v[1] *= gelu_tanh_grad(x1);
+            v[2] *= gelu_tanh_grad(x2);
+            v[3] *= gelu_tanh_grad(x3);
+          } else {
+            v[0] += x0;
+            v[1] += x1;
+            v[2] += x2;
+            v[3] += x3;
+          }
         }
-        if constexpr ((EK & kEkBeta) != 0) {
-          uint2 ov = make_uint2(0, 0);
-          if (!CHECK || n < N) ov = *reinterpret_cast<const uint2*>(out + row + n);
-          v[0] += bf2f(static_cast<bf16_t>(ov.x & 0xffff));
-          v[1] += bf2f(static_cast<bf16_t>(ov.x >> 16));
-          v[2] += bf2f(static_cast<bf16_t>(ov.y & 0xffff));
-          v[3] += bf2f(static_cast<bf16_t>(ov.y >> 16));
+        if constexpr ((EK & kEkAux) != 0) {
+          pa[j][0] = pack_bf16x2(v[0], v[1]);
+          pa[j][1] = pack_bf16x2(v[2], v[3]);
         }
-        if constexpr ((EK & kEkAux) != 0) pa[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         if constexpr ((EK & kEkGelu) != 0) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = gelu_tanh(v[q]);
         }
-        po[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        po[j][0] = pack_bf16x2(v[0], v[1]);
+        po[j][1] = pack_bf16x2(v[2], v[3]);
       }
-      const int nst = odd ? nb + 12 : nb;
-      {
-        const uint2 snd = odd ? po[0] : po[1];
-        const uint2 rcv = make_uint2(__shfl_xor(snd.x, 16, 64), __shfl_xor(snd.y, 16, 64));
-        const uint4 w = odd ? make_uint4(rcv.x, rcv.y, po[1].x, po[1].y) : make_uint4(po[0].x, po[0].y, rcv.x, rcv.y);
-        if (!CHECK || nst < N) *reinterpret_cast<uint4*>(out + row + nst) = w;
-      }
-      if constexpr ((EK & kEkAux) != 0) {
-        const uint2 snd = odd ? pa[0] : pa[1];
-        const uint2 rcv = make_uint2(__shfl_xor(snd.x, 16, 64), __shfl_xor(snd.y, 16, 64));
-        const uint4 w = odd ? make_uint4(rcv.x, rcv.y, pa[1].x, pa[1].y) : make_uint4(pa[0].x, pa[0].y, rcv.x, rcv.y);
-        if (!CHECK || nst < N) *reinterpret_cast<uint4*>(E.aux + row + nst) = w;
-      }
+      // even rows (g even) keep block 2p's own columns and receive the odd neighbour's; odd
+      // rows receive the even neighbour's block 2p + 1 columns: 8 consecutive columns per lane
+      const int nst = odd ? ncol + 32 * p + 12 : ncol + 32 * p;
+      auto swap_store = [&](uint32_t (&q)[2][2], bf16_t* base) {
+        const auto s0 = __builtin_amdgcn_permlane16_swap(q[0][0], q[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(q[0][1], q[1][1], false, false);
+        const uint4 w = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        if (mok && (!CHECK || nst < N)) *reinterpret_cast<uint4*>(base + row + nst) = w;
+      };
+      swap_store(po, out);
+      if constexpr ((EK & kEkAux) != 0) swap_store(pa, E.aux);
     }
   }
 }
@@ -591,6 +622,218 @@ __global__ __launch_bounds__(T, 1) void g4diag32_kernel(const bf16_t* __restrict
 }
 
 // ============================================================================================
+// gemm4p: the production form — persistent 4-wave 256 x 256 kernel on the SCHED 2 main loop
+// (16x16x32 MFMAs, LDS-DMA staging, 2 barriers per K-tile; 64 % MFMA busy at 8192^3 with 12.8 %
+// of wave cycles waiting, profiles/r5_gemm4_pmc_8192.txt). One workgroup per CU walks its
+// XCD's tile range (xcd_remap order, column-major blocks of `group` tile rows): as soon as a
+// tile's last K-tile is consumed, the next tile's first two K-tiles are DMA'd into the idle
+// stages and only then does the register epilogue run, so the operand latency of tile i + 1
+// hides under tile i's epilogue and its stores drain under tile i + 1's MFMAs. The first
+// K-step of every tile runs its MFMAs with C = 0 (no accumulator zero-fill).
+// Epilogues that load (dGELU residual, accumulate) issue the next tile's DMA after the
+// epilogue instead: hipcc counts only its own loads, so an older DMA in the queue would make
+// every epilogue load wait for it.
+
+__device__ __forceinline__ void dma_piece(uint32_t m0v, uint32_t voff, const ttd_i32x4_t& srd, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(m0v), "v"(voff), "s"(srd), "s"(soff)
+      : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void ds_rd(bf16x8_t& d, uint32_t base) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(OFF));
+}
+
+// STAMP (diagnostic build, TTD_G4_SCHED=31): s_memtime around the tile phases, per-wave sums
+// written to g_stamps[block][wave][4] = (tile start -> K-tile 0 landed, main loop, epilogue, tiles)
+__device__ unsigned long long g_stamps[2048 * 4 * 4];
+
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+template <int EK, bool STAMP = false>
+__global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__ A, long long lda,
+                                                     const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
+                                                     int N, int K, int tiles_m, int tiles_n, int group,
+                                                     int stagger) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  constexpr bool EPI_LOADS = (EK & (kEkDGelu | kEkBeta)) != 0;
+  constexpr int EPI_ST = 32 * (((EK & kEkAux) != 0) ? 2 : 1);  // stores per lane, unchecked epilogue
+  const int nblk = tiles_m * tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ktiles = K / 64;
+  // XCD x = blockIdx.x & 7 owns tiles [xbase, xbase + xcnt) of the order; its G8 workgroups
+  // take idx = blockIdx.x >> 3, + G8, ... (the host launches a multiple of 8 workgroups)
+  const int xcd = blockIdx.x & 7, G8 = gridDim.x >> 3;
+  const int xq = nblk >> 3, xr = nblk & 7;
+  const int xbase = xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq;
+  const int xcnt = xq + (xcd < xr ? 1 : 0);
+  int idx = blockIdx.x >> 3;
+  if (idx >= xcnt) return;
+
+  const int i16 = lane & 15, g = lane >> 4;
+  const int lk0 = i16 * 128 + (((g) ^ ((i16 >> 1) & 7)) << 4);
+  const int lk1 = i16 * 128 + (((4 | g) ^ ((i16 >> 1) & 7)) << 4);
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
+  uint32_t va[2][2], vb[2][2];  // [stage][K-step] fragment bases (block offsets immediate)
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    va[st][0] = sb + st * STAGE + wm * 16384 + lk0;
+    va[st][1] = sb + st * STAGE + wm * 16384 + lk1;
+    vb[st][0] = sb + st * STAGE + OPB + wn * 16384 + lk0;
+    vb[st][1] = sb + st * STAGE + OPB + wn * 16384 + lk1;
+  }
+  const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
+  LoadK la, lb;
+  f32x4_t acc[8][8];
+  bf16x8_t fa[2][8], fb[2][8];
+
+  auto rd1 = [&](auto R, uint32_t a_base, uint32_t b_base, bf16x8_t (&xa)[8], bf16x8_t (&xb)[8]) {
+    constexpr int r = decltype(R)::value;
+    if constexpr (rd_is_a(r)) ds_rd<rd_blk(r) * 2048>(xa[rd_blk(r)], a_base);
+    else ds_rd<rd_blk(r) * 2048>(xb[rd_blk(r)], b_base);
+  };
+  auto dma1 = [&](auto Q, int st, int kt) {  // piece q (0..7 A, 8..15 B) of K-tile kt into stage st
+    constexpr int q = decltype(Q)::value;
+    const LoadK& L = q < 8 ? la : lb;
+    dma_piece(ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096, L.voff[q & 7], L.srd, kt * 128);
+  };
+  auto mfma1 = [&](int a, int b, const bf16x8_t& x, const bf16x8_t& y, auto first) {
+    mfma_acc<decltype(first)::value>(acc[a][b], x, y);
+  };
+  auto coords = [&](int i, int& m0, int& n0) {
+    int tm, tn;
+    tile_of(xbase + i, tiles_m, tiles_n, group, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  auto prologue = [&](int m0, int n0) {  // K-tiles 0 and 1 of tile (m0, n0) into stages 0 and 1
+    la.init(A, lda, M, m0, tid);
+    lb.init(B, ldb, N, n0, tid);
+    static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
+    if (ktiles > 1) static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
+  };
+  // one K-tile of the SCHED 2 schedule (see gemm4w_kernel); FIRST: phase 0 with C = 0
+  auto ktile = [&](int kt, auto first) {
+    const bool has2 = kt + 2 < ktiles;
+    const int st = kt & 1;
+    static_for<64>([&](auto I) {
+      constexpr int i = decltype(I)::value, a = i / 8, b = i % 8;
+      if constexpr (i % 4 == 0) rd1(std::integral_constant<int, i / 4>{}, va[st][1], vb[st][1], fa[1], fb[1]);
+      if constexpr (i == 0 || need0(i) > need0(i - 1 < 0 ? 0 : i - 1))
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(lgk0(i)) : "memory");
+      mfma1(a, b, fa[0][a], fb[0][b], first);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    static_for<32>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 4 == 0)
+        if (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
+      mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], std::false_type{});
+    });
+    if (has2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    static_for<32>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 4 == 1)
+        if (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
+      if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
+      mfma1(4 + i / 8, i % 8, fa[1][4 + i / 8], fb[1][i % 8], std::false_type{});
+    });
+  };
+
+  int m0, n0;
+  coords(idx, m0, n0);
+  prologue(m0, n0);
+  // Stagger: every workgroup walks identical tiles, so without it all 256 CUs reach their
+  // epilogues together and the chip's HBM write bandwidth is shared by every CU's 128-256 KB of
+  // stores at once (in-kernel stamps: a bias epilogue took 23k cycles per tile, half the main
+  // loop, profiles/r5_gemm4p_stamps.txt). Workgroup i starts (i / 8) % 4 quarters of `stagger`
+  // sleep units later (64 cycles each), so at any time about a quarter of the CUs store.
+  if (stagger > 0) {
+    const int q = (blockIdx.x >> 3) & 3;
+    for (int k = 0; k < q * stagger; ++k) __builtin_amdgcn_s_sleep(127);
+  }
+  int prev = 0;  // what the previous tile left in the VMEM queue after this tile's DMA: 0 none,
+                 // 1 an unchecked epilogue's EPI_ST stores, 2 a data-dependent count
+  const float alpha = epi_alpha(E);
+  unsigned long long st_land = 0, st_loop = 0, st_epi = 0, st_n = 0, tA = 0, tB = 0;
+  for (;;) {
+    if constexpr (STAMP) tA = stamp();
+    // K-tile 0 has landed: the queue holds (K-tile 0, K-tile 1 [16 each], previous stores)
+    if (prev == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (ktiles > 1) {
+      if (prev == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(16 + EPI_ST > 63 ? 63 : 16 + EPI_ST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      if (prev == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_ST > 63 ? 63 : EPI_ST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");
+    if constexpr (STAMP) {
+      tB = stamp();
+      st_land += tB - tA;
+    }
+    static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
+    ktile(0, std::true_type{});
+    for (int kt = 1; kt < ktiles; ++kt) ktile(kt, std::false_type{});
+    // every wave past its last LDS read before the stages are refilled
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (STAMP) {
+      tA = stamp();
+      st_loop += tA - tB;
+    }
+    const int nidx = idx + G8;
+    const bool more = nidx < xcnt;
+    int nm0 = 0, nn0 = 0;
+    if (more) coords(nidx, nm0, nn0);
+    if (!EPI_LOADS && more) prologue(nm0, nn0);
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+    const bool whole = m0 + BM <= M && n0 + BN <= N;
+    if (whole) epilogue<EK, false>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
+    else epilogue<EK, true>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
+    if constexpr (STAMP) {
+      st_epi += stamp() - tA;
+      st_n += 1;
+    }
+    if (!more) break;
+    if (EPI_LOADS) {
+      prologue(nm0, nn0);
+      prev = 0;
+    } else {
+      prev = whole ? 1 : 2;
+    }
+    m0 = nm0;
+    n0 = nn0;
+    idx = nidx;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0 && blockIdx.x < 2048) {
+      unsigned long long* o = g_stamps + (blockIdx.x * 4 + wave) * 4;
+      o[0] = st_land;
+      o[1] = st_loop;
+      o[2] = st_epi;
+      o[3] = st_n;
+    }
+  }
+}
+
+// ============================================================================================
 // gemm4v: the production form. Same 256 x 256 tile, 4 waves, AGPR accumulators, but
 //  * v_mfma_f32_32x32x16_bf16 (4 x 4 tiles of 32 x 32 per wave): 32-cycle MFMA gaps leave ~24
 //    issue cycles each for the loads / LDS traffic of a one-wave-per-SIMD loop;
@@ -826,11 +1069,26 @@ __global__ __launch_bounds__(T, 1) void gemm4v_kernel(const bf16_t* __restrict__
 }  // namespace
 }  // namespace ttdk
 
-// TTD_G4_SCHED: 1 (default) = asm-scheduled main loop, 0 = compiler-scheduled (A/B, tests)
+// TTD_G4_SCHED: main-loop form. 30 (default) = persistent SCHED-2 kernel (gemm4p); 0-3 the
+// one-tile-per-workgroup forms (0 compiler-scheduled, 1-3 hand-ordered asm), 20 the VGPR-staged
+// 32x32x16 form, 31 = 30 with phase stamps, 4-9 / d32 diagnostics (wrong results, timing only)
 static int& g4_sched() {
-  static int v = ttdk::getenv_int("TTD_G4_SCHED", 1);
+  static int v = ttdk::getenv_int("TTD_G4_SCHED", 30);
   return v;
 }
+static int g4_cus() { return ttdk::big::device_cus(); }
+// TTD_G4_STAGGER: stagger the persistent workgroups' tile phases (default off: +8 % on the
+// GELU + aux epilogue, -10 % on the bias-only shapes, tools/g4_bench.py)
+static int& g4_stagger() {
+  static int v = ttdk::getenv_int("TTD_G4_STAGGER", 0);
+  return v;
+}
+TTDK_EXPORT int ttdk_set_g4_stagger(int v) {
+  const int old = g4_stagger();
+  g4_stagger() = v;
+  return old;
+}
+
 // TTD_G4_GROUP: tile rows per column-major tile block (1 = row-major order)
 static int& g4_group() {
   static int v = ttdk::getenv_int("TTD_G4_GROUP", 8);
@@ -858,7 +1116,8 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
   const long long lim = 1LL << 32;
   if (K < 64 || K % 64 || N % 8 || lda % 8 || ldb % 8 || pe.ldo % 8 || !al16(A) || !al16(B) || !al16(pe.out) ||
       (static_cast<long long>(M) + 256) * lda * 2 >= lim || (static_cast<long long>(N) + 256) * ldb * 2 >= lim ||
-      pe.mode != 0 || pe.remap || pe.stat || pe.by || pe.bH)
+      pe.mode != 0 || pe.remap || pe.stat || pe.by || pe.bH || (pe.bias && !al16(pe.bias)) ||
+      (pe.aux && !al16(pe.aux)) || (pe.residual && ((reinterpret_cast<uintptr_t>(pe.residual) & 7) || pe.ldr % 4)))
     return hipErrorInvalidValue;
   int ek = -1;
   if (pe.act == kActNone && !pe.residual) ek = 0;
@@ -871,6 +1130,9 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
   const int tm = ceil_div(M, g4::BM), tn = ceil_div(N, g4::BN);
   const int sched = g4_sched();
   const int group = g4_group();
+  // stagger of the persistent kernel's workgroups: a quarter tile in s_sleep 127 units (~8k
+  // cycles each), from the K-tile count (~3k cycles per K-tile + the epilogue)
+  const int stag = g4_stagger() ? std::max(1, ((K / 64) * 3000 + 20000) / 4 / 8128) : 0;
 #define TTDK_G4(EKV)                                                                                        \
   case EKV:                                                                                                 \
     switch (sched) {                                                                                        \
@@ -892,6 +1154,24 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
       case 9: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 9>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 31: {                                                                                          \
+        const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
+        if (grid < 8) return hipErrorInvalidValue;                                                          \
+        hipLaunchKernelGGL((g4::gemm4p_kernel<EKV, true>), dim3(grid), dim3(g4::T), 0, st, A, lda, B, ldb, pe, \
+                           M, N, K, tm, tn, group, stag);                                                   \
+        break;                                                                                              \
+      }                                                                                                     \
+      case 30: {                                                                                          \
+        const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
+        if (grid < 8 || tm * tn <= g4_cus()) { /* one tile per workgroup: nothing to overlap */           \
+          hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, \
+                             pe, M, N, K, tm, tn, group);                                                   \
+          break;                                                                                            \
+        }                                                                                                   \
+        hipLaunchKernelGGL((g4::gemm4p_kernel<EKV>), dim3(grid), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M, N,  \
+                           K, tm, tn, group, stag);                                                         \
+        break;                                                                                              \
+      }                                                                                                     \
       case 20: if (K % 128) return hipErrorInvalidValue;                                                   \
                hipLaunchKernelGGL((g4::gemm4v_kernel<EKV>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb,   \
                                   pe, M, N, K, tm, tn, group); break;                                        \
@@ -932,4 +1212,9 @@ TTDK_EXPORT int ttdk_g4diag32(int mode, const bf16_t* A, long long lda, const bf
     default: hipLaunchKernelGGL((g4::g4diag32_kernel<9>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
   }
   return hipGetLastError();
+}
+
+// diagnostic: copy the per-wave phase stamps of the last TTD_G4_SCHED=31 launch (2048 x 4 x 4 u64)
+TTDK_EXPORT int ttdk_g4_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ttdk::g4::g_stamps), sizeof(ttdk::g4::g_stamps), 0, hipMemcpyDeviceToHost);
 }

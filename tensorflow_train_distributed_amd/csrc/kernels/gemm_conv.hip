@@ -1,6 +1,9 @@
 // Dense bf16 GEMM entry point (+ split-K reduce); kernels in gemm_conv.h.
 #include "gemm_conv.h"
 
+extern "C" int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                                const TtdkEpilogue* epi, hipStream_t st);
+
 // General GEMM: C[M,N] = alpha * A·B with A either K-major (a_kmajor=1: A[m*lda + k]) or
 // MN-major (A[k*lda + m]); B either K-major (B[n*ldb + k]) or MN-major (B[k*ldb + n]).
 TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, const bf16_t* B, long long ldb,
@@ -14,6 +17,16 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
                    (b_kmajor ? K % 8 == 0 : N % 8 == 0);
   DenseParams pa{A, lda, M, K};
   DenseParams pb{B, ldb, N, K};
+  // K-major x K-major GEMMs with an elementwise epilogue: the 4-wave AGPR-accumulator kernel
+  // (gemm4w.hip; persistent, ~5-15 % ahead of the 8-wave 256-row kernel at every BERT-Large
+  // shape, tools/g4_bench.py). It refuses what it does not take (hipErrorInvalidValue) and the
+  // 256-row path below runs instead. TTD_G4=0: off.
+  static const int g4_on = getenv_int("TTD_G4", 1);
+  if (g4_on && a_kmajor && b_kmajor && vec && bm == 0 && bn == 0 && pe.mode == 0 && M >= 256 && N >= 256 &&
+      K >= 128 && K % 128 == 0) {
+    const int rc = ttdk_gemm4w_bf16(A, lda, B, ldb, M, N, K, epi, st);
+    if (rc != hipErrorInvalidValue) return rc;
+  }
   // 256-row LDS-DMA path for big GEMMs (explicit tile 256 forces it; 128/64 force the 4-wave kernel)
   const int bbn = big_bn(M, N, K);
   // per-tile statistics rows follow the kernel's tile height: with `stat` the 256-row kernel runs

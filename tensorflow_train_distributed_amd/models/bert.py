@@ -161,16 +161,13 @@ class BertPretraining:
         # encoder bias gradients formed inside their weight-gradient GEMM from the dy tiles in LDS
         # (ops.gemm.gemm_wgrad_bias) instead of a column-sum pass over dy (TTD_BERT_BIAS_WGRAD=0: off)
         self.bias_in_wgrad = os.environ.get("TTD_BERT_BIAS_WGRAD", "1") != "0" and self.device.type == "cuda"
-        # Plain GEMMs through the vendor library (torch.addmm / mm -> hipBLASLt), TTD_BERT_BLASLT:
-        # 1 = the forward's bias-only GEMMs (QKV, attention output, FFN2, MLM logits; bf16 bias =
-        # the compute copy, as a bf16 mixed-precision layer casts it), 2 (default) = also the plain
-        # and accumulating data gradients; 0 = our persistent GEMM everywhere. The fused GEMMs stay
-        # ours: FFN1 (bias + GELU + pre-activation store), the dGELU data gradient, the weight
-        # gradients with their in-kernel bias row sums. Same box, 2 pairs: 164.1 / 163.9 ms (2),
-        # 166.2 / 166.6 (1), 170.9 / 171.1 (0) — hipBLASLt's 4-wave 256x256 tiles wait far less
-        # than our 8-wave ping-pong main loop (profiles/r3_gemm_pmc_ours_vs_hipblaslt.txt). 3 = the
-        # weight gradients too (fp32 out + column-sum pass): 168.2 / 168.4 vs 164.3 / 164.7 ms, slower
-        self.blaslt = int(os.environ.get("TTD_BERT_BLASLT", "2")) if self.device.type == "cuda" else 0
+        # GEMM path. 0 (default): every GEMM on our kernels — the K-major dense layers (QKV,
+        # attention output, FFN1 with bias + GELU + pre-activation store, FFN2, MLM logits, and the
+        # data gradients on the [in][out] weight copies) on the 4-wave AGPR-accumulator kernel
+        # (gemm4w.hip), the rest on the 256-row kernels. The vendor library (torch.addmm / mm ->
+        # hipBLASLt) is an A/B and oracle mode only, TTD_BERT_BLASLT: 1 = the forward's bias-only
+        # GEMMs, 2 = also the plain / accumulating data gradients, 3 = the weight gradients too.
+        self.blaslt = int(os.environ.get("TTD_BERT_BLASLT", "0")) if self.device.type == "cuda" else 0
         self._wt = None
         if self.device.type == "cuda":
             from ..ops.transformer import RngState

@@ -153,7 +153,14 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat
 
 
 _lib.register({"ttdk_gemm4w_bf16": [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.E, _lib.P],
-               "ttdk_set_g4_sched": [_lib.I], "ttdk_set_g4_group": [_lib.I]})
+               "ttdk_set_g4_sched": [_lib.I], "ttdk_set_g4_group": [_lib.I],
+               "ttdk_set_g4_stagger": [_lib.I]})
+
+
+def set_g4_stagger(v: int) -> int:
+    """Stagger the persistent 4-wave GEMM's workgroup tile phases (1) or not (0); returns the
+    previous setting."""
+    return int(_lib.query("ttdk_set_g4_stagger", int(v)))
 
 
 def set_g4_group(v: int) -> int:

@@ -42,11 +42,16 @@ def test_bert_checkpoint_export_tf_layout(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("full_length", [True, False])
-def test_bert_engine_matches_reference(full_length):
+@pytest.mark.parametrize("gemms", ["own", "vendor_ab"])
+def test_bert_engine_matches_reference(full_length, gemms):
+    """gemms="own": every GEMM on our kernels (the product default: the 4-wave AGPR kernel for
+    the K-major dense layers, the 256-row kernel for the rest); "vendor_ab": the hipBLASLt A/B
+    mode (TTD_BERT_BLASLT=2), kept as an oracle path."""
     torch.manual_seed(0)
     cfg = BertConfig(vocab_size=1000, hidden_size=512, num_hidden_layers=2, num_attention_heads=8,
                      intermediate_size=1024, max_position_embeddings=256)
     m = BertPretraining(cfg, device="cuda", seed=3, dropout=False)
+    m.blaslt = 0 if gemms == "own" else 2
     batch = synthetic_batch(cfg, 2, 256, max_predictions=20, device="cuda", seed=1, full_length=full_length)
     sums = m.forward_backward(batch)
     torch.cuda.synchronize()

@@ -19,7 +19,7 @@ SHAPES = [(256, 256, 128), (512, 512, 128), (1000, 264, 384), (300, 1000, 1024),
           (2048, 1024, 4096), (65, 8, 128)]
 
 
-@pytest.fixture(params=[20, 1, 2, 3, 0], ids=["vstage32", "asm_sched1", "asm_sched2", "asm_sched3", "compiler_sched"])
+@pytest.fixture(params=[30, 20, 1, 2, 3, 0], ids=["persistent", "vstage32", "asm_sched1", "asm_sched2", "asm_sched3", "compiler_sched"])
 def sched(request):
     from tensorflow_train_distributed_amd.ops import gemm as G
     old = G.set_g4_sched(request.param)

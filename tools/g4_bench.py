@@ -68,11 +68,12 @@ def main():
                                                  _lib.I, _lib.P]})
                 arms[k] = (lambda v: lambda: _lib.call("ttdk_g4diag32", v, a.data_ptr(), K, b.data_ptr(), K,
                                                        out.data_ptr(), M, N, K, _lib.stream()))(int(k[4:]))
-            if k.startswith("g4:"):  # g4:SCHED[/GROUP]
-                sv, _, gv = k[3:].partition("/")
-                arms[k] = (lambda v, gr: lambda: (G.set_g4_sched(v), G.set_g4_group(gr),
-                                                  G.gemm4w(a, b, out=out, bias=bias, act=act, residual=res, aux=aux)))(
-                    int(sv), int(gv or 8))
+            if k.startswith("g4:"):  # g4:SCHED[/GROUP[/STAGGER]]
+                sv, _, rest = k[3:].partition("/")
+                gv, _, stv = rest.partition("/")
+                arms[k] = (lambda v, gr, sg: lambda: (G.set_g4_sched(v), G.set_g4_group(gr), G.set_g4_stagger(sg),
+                                                      G.gemm4w(a, b, out=out, bias=bias, act=act, residual=res,
+                                                               aux=aux)))(int(sv), int(gv or 8), int(stv or 1))
         fl = 2.0 * M * N * K
         res_t = {k: [] for k in ARMS}
         for _ in range(ROUNDS):
