@@ -662,8 +662,9 @@ template <int EK, bool STAMP = false>
 __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
                                                      int N, int K, int tiles_m, int tiles_n, int group,
-                                                     int stagger) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+                                                     int stagger, int* tq) {
+  // (+16 B: the claimed next tile, broadcast to the workgroup; one __shared__ object)
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 16];
   constexpr bool EPI_LOADS = (EK & (kEkDGelu | kEkBeta)) != 0;
   constexpr int EPI_ST = 32 * (((EK & kEkAux) != 0) ? 2 : 1);  // stores per lane, unchecked epilogue
   const int nblk = tiles_m * tiles_n;
@@ -770,6 +771,13 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
   unsigned long long st_land = 0, st_loop = 0, st_epi = 0, st_n = 0, tA = 0, tB = 0;
   for (;;) {
     if constexpr (STAMP) tA = stamp();
+    // Tile queue (tq: 8 per-XCD counters + a finished-workgroup count): after its static first
+    // tile a workgroup claims the next unclaimed tile of its XCD's range. In the two-stream
+    // BERT step the side stream's weight gradients hold up to 192 CUs for hundreds of us, so
+    // some workgroups of a persistent grid get a CU late; with a static share each would finish
+    // its whole share late and hold the launch. The claim's round trip hides under the loop.
+    int claim = 0;
+    if (tq && tid == 0) claim = atomicAdd(tq + xcd, 1);
     // K-tile 0 has landed: the queue holds (K-tile 0, K-tile 1 [16 each], previous stores)
     if (prev == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -788,13 +796,14 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
     static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
     ktile(0, std::true_type{});
     for (int kt = 1; kt < ktiles; ++kt) ktile(kt, std::false_type{});
+    if (tq && tid == 0) *reinterpret_cast<int*>(smem + SMEM) = claim;
     // every wave past its last LDS read before the stages are refilled
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if constexpr (STAMP) {
       tA = stamp();
       st_loop += tA - tB;
     }
-    const int nidx = idx + G8;
+    const int nidx = tq ? G8 + __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + SMEM)) : idx + G8;
     const bool more = nidx < xcnt;
     int nm0 = 0, nn0 = 0;
     if (more) coords(nidx, nm0, nn0);
@@ -821,6 +830,14 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
     m0 = nm0;
     n0 = nn0;
     idx = nidx;
+  }
+  if (tq && tid == 0) {
+    // every workgroup's last claim precedes its arrival here: the last to arrive resets the
+    // queue for the next launch on this stream (graph replays included)
+    if (atomicAdd(tq + 8, 1) == static_cast<int>(gridDim.x) - 1) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) tq[i] = 0;
+    }
   }
   if constexpr (STAMP) {
     if (lane == 0 && blockIdx.x < 2048) {
@@ -1133,6 +1150,15 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
   // stagger of the persistent kernel's workgroups: a quarter tile in s_sleep 127 units (~8k
   // cycles each), from the K-tile count (~3k cycles per K-tile + the epilogue)
   const int stag = g4_stagger() ? std::max(1, ((K / 64) * 3000 + 20000) / 4 / 8128) : 0;
+  // the persistent kernel's tile queue: the stream's counter buffer (gemm_conv.h tile_counters),
+  // last 16 ints, shared with gemm256p_kernel (same-stream launches never overlap; each launch
+  // leaves it zeroed). TTD_G4_QUEUE=0: static tile shares.
+  static const int queue = getenv_int("TTD_G4_QUEUE", 1);
+  int* tq = nullptr;
+  if (queue && g4_cus() % 8 == 0) {
+    int* c = big::tile_counters(st, 0);
+    if (c) tq = c + big::kMaxCtr - 16;
+  }
 #define TTDK_G4(EKV)                                                                                        \
   case EKV:                                                                                                 \
     switch (sched) {                                                                                        \
@@ -1158,7 +1184,7 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
         const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
         if (grid < 8) return hipErrorInvalidValue;                                                          \
         hipLaunchKernelGGL((g4::gemm4p_kernel<EKV, true>), dim3(grid), dim3(g4::T), 0, st, A, lda, B, ldb, pe, \
-                           M, N, K, tm, tn, group, stag);                                                   \
+                           M, N, K, tm, tn, group, stag, tq);                                               \
         break;                                                                                              \
       }                                                                                                     \
       case 30: {                                                                                          \
@@ -1169,7 +1195,7 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
           break;                                                                                            \
         }                                                                                                   \
         hipLaunchKernelGGL((g4::gemm4p_kernel<EKV>), dim3(grid), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M, N,  \
-                           K, tm, tn, group, stag);                                                         \
+                           K, tm, tn, group, stag, tq);                                                     \
         break;                                                                                              \
       }                                                                                                     \
       case 20: if (K % 128) return hipErrorInvalidValue;                                                   \

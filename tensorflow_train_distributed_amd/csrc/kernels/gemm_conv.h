@@ -853,8 +853,18 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
 
 template <int BM, int BN, class LA, class LB>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(typename LA::Params pa, typename LB::Params pb, EpiParams pe,
-                                                      int M, int N, int K, int tiles_m, int tiles_n, int kt_per_split) {
+                                                      int M, int N, int K, int tiles_m, int tiles_n, int kt_per_split,
+                                                      long long bsa = 0, long long bsb = 0, long long bso = 0) {
   __shared__ __attribute__((aligned(16))) char smem[2 * (LA::BYTES + LB::BYTES)];
+  // strided batch on grid z (dense operands only; element strides, output stride in elements of
+  // the epilogue's output type): one launch for a batched MatMul
+  if constexpr (std::is_same_v<typename LA::Params, DenseParams> && std::is_same_v<typename LB::Params, DenseParams>) {
+    if (gridDim.z > 1) {
+      pa.p += blockIdx.z * bsa;
+      pb.p += blockIdx.z * bsb;
+      pe.out = static_cast<char*>(pe.out) + blockIdx.z * bso * (pe.mode == 0 ? 2 : 4);
+    }
+  }
   const int nblk = tiles_m * tiles_n;
   // split-K (gridDim.y > 1): the XCD-aware order runs over (tile, split) so the output tiles of
   // one K-split — which read the same K rows of both operands (a weight gradient's dy and
@@ -2573,6 +2583,16 @@ hipError_t launch(const typename LA::Params& pa, const typename LB::Params& pb, 
   splits = ceil_div(ktiles, per);
   dim3 grid(tm * tn, splits);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB>), grid, dim3(NTHR), 0, st, pa, pb, pe, M, N, K, tm, tn, per);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, class LA, class LB>
+hipError_t launch_batched(const typename LA::Params& pa, const typename LB::Params& pb, const EpiParams& pe, int M,
+                          int N, int K, int batch, long long sa, long long sb, long long so, hipStream_t st) {
+  const int tm = ceil_div(M, BM), tn = ceil_div(N, BN);
+  const int ktiles = ceil_div(K, BK);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB>), dim3(tm * tn, 1, batch), dim3(NTHR), 0, st, pa, pb, pe, M, N, K, tm,
+                     tn, ktiles, sa, sb, so);
   return hipGetLastError();
 }
 

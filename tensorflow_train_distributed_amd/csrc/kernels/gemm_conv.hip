@@ -51,6 +51,51 @@ TTDK_EXPORT int ttdk_gemm_bf16(const bf16_t* A, long long lda, int a_kmajor, con
   return dispatch<MNDenseS, MNDenseS>(&pa, &pb, pe, M, N, K, splits, bm, bn, st);
 }
 
+// Strided-batched GEMM: C_z[M,N] = alpha * op(A_z) . op(B_z) for z < batch in ONE launch (batch on
+// grid z; A_z = A + z*sa, B_z = B + z*sb, C_z = out + z*so, element strides), bf16 operands in
+// either layout, bf16 (out_fp32 = 0) or fp32 output. The batched MatMul of ttd.nn.matmul
+// (tf.matmul on rank > 2 operands; per-entry launches before).
+TTDK_EXPORT int ttdk_gemm_bf16_batched(const bf16_t* A, long long lda, long long sa, int a_kmajor, const bf16_t* B,
+                                       long long ldb, long long sb, int b_kmajor, void* out, long long ldo,
+                                       long long so, int out_fp32, int M, int N, int K, int batch, hipStream_t st) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || batch > 65535) return hipErrorInvalidValue;
+  const bool vec = al(A) && al(B) && lda % 8 == 0 && ldb % 8 == 0 && sa % 8 == 0 && sb % 8 == 0 &&
+                   (a_kmajor ? K % 8 == 0 : M % 8 == 0) && (b_kmajor ? K % 8 == 0 : N % 8 == 0);
+  TtdkEpilogue te{};
+  te.mode = out_fp32 ? 2 : 0;
+  te.out = out;
+  te.ldo = ldo;
+  EpiParams pe = to_epi(&te);
+  DenseParams pa{A, lda, M, K};
+  DenseParams pb{B, ldb, N, K};
+  int bm = 0, bn = 0;
+  pick_tile(M, N, &bm, &bn);
+#define TTDK_BCASE(BM_, BN_, LA_, LB_)                                                                            \
+  if (bm == BM_ && bn == BN_) return launch_batched<BM_, BN_, LA_<BM_>, LB_<BN_>>(pa, pb, pe, M, N, K, batch, sa, sb, so, st);
+#define TTDK_BLAYOUT(LA_, LB_) \
+  {                            \
+    TTDK_BCASE(128, 128, LA_, LB_) \
+    TTDK_BCASE(128, 64, LA_, LB_)  \
+    TTDK_BCASE(64, 128, LA_, LB_)  \
+    TTDK_BCASE(64, 64, LA_, LB_)   \
+  }
+  if (vec) {
+    if (a_kmajor && b_kmajor) TTDK_BLAYOUT(KDense, KDense)
+    if (a_kmajor && !b_kmajor) TTDK_BLAYOUT(KDense, MNDense)
+    if (!a_kmajor && b_kmajor) TTDK_BLAYOUT(MNDense, KDense)
+    if (!a_kmajor && !b_kmajor) TTDK_BLAYOUT(MNDense, MNDense)
+  } else {
+    if (a_kmajor && b_kmajor) TTDK_BLAYOUT(KDenseS, KDenseS)
+    if (a_kmajor && !b_kmajor) TTDK_BLAYOUT(KDenseS, MNDenseS)
+    if (!a_kmajor && b_kmajor) TTDK_BLAYOUT(MNDenseS, KDenseS)
+    if (!a_kmajor && !b_kmajor) TTDK_BLAYOUT(MNDenseS, MNDenseS)
+  }
+#undef TTDK_BLAYOUT
+#undef TTDK_BCASE
+  return hipErrorInvalidValue;
+}
+
 // Split-K GEMM into an fp32 output: C (+)= alpha * A.B over `splits` K-slices with fp32 slabs in
 // `ws` [splits][M][N]. On the 256-row kernel the launch folds its own slabs (EpiParams mode 3);
 // elsewhere a fold pass follows.

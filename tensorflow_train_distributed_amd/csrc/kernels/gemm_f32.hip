@@ -30,7 +30,12 @@ __device__ __forceinline__ float ld_op(const float* __restrict__ p, long long ld
 __global__ __launch_bounds__(F_THR) void gemm_f32_kernel(const float* __restrict__ A, long long lda, int ta,
                                                           const float* __restrict__ B, long long ldb, int tb,
                                                           float* __restrict__ C, long long ldc, const float* __restrict__ bias,
-                                                          int beta, int M, int N, int K) {
+                                                          int beta, int M, int N, int K, long long sa = 0,
+                                                          long long sb = 0, long long sc = 0) {
+  // strided batch (tf.matmul on rank > 2 operands): entry blockIdx.z at element offsets z * s*
+  A += blockIdx.z * sa;
+  B += blockIdx.z * sb;
+  C += blockIdx.z * sc;
   __shared__ float sA[F_BK][F_BM + 1];
   __shared__ float sB[F_BK][F_BN + 1];
   const int m0 = blockIdx.y * F_BM, n0 = blockIdx.x * F_BN;
@@ -93,5 +98,17 @@ TTDK_EXPORT int ttdk_gemm_f32(const float* A, long long lda, int ta, const float
   if (M <= 0 || N <= 0 || K < 0) return hipErrorInvalidValue;
   dim3 grid(ceil_div(N, F_BN), ceil_div(M, F_BM));
   hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(F_THR), 0, st, A, lda, ta, B, ldb, tb, C, ldc, bias, beta, M, N, K);
+  return hipGetLastError();
+}
+
+// Strided-batched form: `batch` GEMMs in one launch (entry z reads A + z*sa, B + z*sb, writes
+// C + z*sc; element strides). The batched MatMul of ttd.nn.matmul on rank > 2 fp32 operands.
+TTDK_EXPORT int ttdk_gemm_f32_batched(const float* A, long long lda, long long sa, int ta, const float* B, long long ldb,
+                                      long long sb, int tb, float* C, long long ldc, long long sc, int M, int N, int K,
+                                      int batch, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K < 0 || batch <= 0 || batch > 65535) return hipErrorInvalidValue;
+  dim3 grid(ceil_div(N, F_BN), ceil_div(M, F_BM), batch);
+  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(F_THR), 0, st, A, lda, ta, B, ldb, tb, C, ldc, nullptr, 0, M, N, K, sa,
+                     sb, sc);
   return hipGetLastError();
 }

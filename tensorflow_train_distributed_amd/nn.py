@@ -262,22 +262,24 @@ def dense(x, kernel, bias=None, activation=None):
     return _act_ref(y, activation)
 
 
-def _mm(a, b, ta=False, tb=False):
-    """2-D GEMM on the matching MFMA kernel: exact fp32 for fp32 operands, else bf16 -> fp32."""
-    from .ops import gemm as G
-    if a.dtype == torch.float32 and b.dtype == torch.float32:
-        return G.gemm_f32(a, b, trans_a=ta, trans_b=tb)
-    return G.gemm(a.to(torch.bfloat16), b.to(torch.bfloat16), trans_a=ta, trans_b=tb, out_dtype=torch.float32)
-
-
 class _MatMul(torch.autograd.Function):
-    """[..., M, K] @ [..., K, N] with identical leading (batch) shapes, one GEMM per batch entry."""
+    """[..., M, K] @ [..., K, N] with identical leading (batch) shapes: ONE strided-batched GEMM
+    launch per product (ops.gemm.gemm_batched: batch index on the grid), forward and backward.
+    fp32 operands stay exact fp32 (f32 MFMA); otherwise bf16 operands with fp32 accumulation."""
+
+    @staticmethod
+    def _bmm(a, b, ta=False, tb=False):
+        from .ops import gemm as G
+        if a.dtype == torch.float32 and b.dtype == torch.float32:
+            return G.gemm_batched(a, b, trans_a=ta, trans_b=tb)
+        return G.gemm_batched(a.to(torch.bfloat16), b.to(torch.bfloat16), trans_a=ta, trans_b=tb,
+                              out_dtype=torch.float32)
 
     @staticmethod
     def forward(ctx, a, b):
         a3 = a.reshape(-1, a.shape[-2], a.shape[-1]).contiguous()
         b3 = b.reshape(-1, b.shape[-2], b.shape[-1]).contiguous()
-        out = torch.stack([_mm(a3[i], b3[i]) for i in range(a3.shape[0])])
+        out = _MatMul._bmm(a3, b3)
         ctx.save_for_backward(a3, b3)
         ctx.shapes = (a.shape, b.shape, a.dtype, b.dtype)
         return out.reshape(*a.shape[:-1], b.shape[-1]).to(a.dtype)
@@ -291,9 +293,9 @@ class _MatMul(torch.autograd.Function):
             d3 = d3.float()
         da = db = None
         if ctx.needs_input_grad[0]:
-            da = torch.stack([_mm(d3[i], b3[i], tb=True) for i in range(a3.shape[0])]).reshape(sa).to(da_t)
+            da = _MatMul._bmm(d3, b3, tb=True).reshape(sa).to(da_t)
         if ctx.needs_input_grad[1]:
-            db = torch.stack([_mm(a3[i], d3[i], ta=True) for i in range(a3.shape[0])]).reshape(sb).to(db_t)
+            db = _MatMul._bmm(a3, d3, ta=True).reshape(sb).to(db_t)
         return da, db
 
 

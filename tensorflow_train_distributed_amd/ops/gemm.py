@@ -194,6 +194,42 @@ def gemm4w(a, b, *, out=None, bias=None, act=ACT_NONE, residual=None, beta=0, al
     return out
 
 
+_lib.register({"ttdk_gemm_bf16_batched": [_lib.P, _lib.L, _lib.L, _lib.I, _lib.P, _lib.L, _lib.L, _lib.I, _lib.P,
+                                          _lib.L, _lib.L, _lib.I, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P],
+               "ttdk_gemm_f32_batched": [_lib.P, _lib.L, _lib.L, _lib.I, _lib.P, _lib.L, _lib.L, _lib.I, _lib.P,
+                                         _lib.L, _lib.L, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P]})
+
+
+def gemm_batched(a, b, *, trans_a=False, trans_b=False, out_dtype=torch.float32):
+    """Strided-batched C[z] = op(a[z]) @ op(b[z]) for every z in ONE kernel launch (batch index on
+    the grid's z). a: [Bt, M, K] ([Bt, K, M] with trans_a), b: [Bt, K, N] ([Bt, N, K] with trans_b),
+    contiguous 3-D. bf16 operands -> bf16 / fp32 output on the MFMA GEMM; fp32 operands -> exact
+    fp32 (f32 MFMA). The batched MatMul of tf.matmul on rank > 2 operands."""
+    if a.dim() != 3 or b.dim() != 3 or a.shape[0] != b.shape[0]:
+        raise ValueError("gemm_batched needs [B, ., .] operands with equal batch, got %s and %s"
+                         % (tuple(a.shape), tuple(b.shape)))
+    a = a.contiguous()
+    b = b.contiguous()
+    Bt = a.shape[0]
+    M, K = (a.shape[2], a.shape[1]) if trans_a else (a.shape[1], a.shape[2])
+    Kb, N = (b.shape[2], b.shape[1]) if trans_b else (b.shape[1], b.shape[2])
+    if K != Kb:
+        raise ValueError("gemm_batched inner dims differ: %d vs %d" % (K, Kb))
+    _log("gemm_batched", M, N, K, Bt)
+    if a.dtype == torch.float32 and b.dtype == torch.float32:
+        out = torch.empty((Bt, M, N), dtype=torch.float32, device=a.device)
+        _lib.call("ttdk_gemm_f32_batched", a.data_ptr(), a.stride(1), a.stride(0), int(trans_a), b.data_ptr(),
+                  b.stride(1), b.stride(0), int(trans_b), out.data_ptr(), N, M * N, M, N, K, Bt, _lib.stream())
+        return out
+    _check(a, torch.bfloat16, "a")
+    _check(b, torch.bfloat16, "b")
+    out = torch.empty((Bt, M, N), dtype=out_dtype, device=a.device)
+    _lib.call("ttdk_gemm_bf16_batched", a.data_ptr(), a.stride(1), a.stride(0), 0 if trans_a else 1, b.data_ptr(),
+              b.stride(1), b.stride(0), 1 if trans_b else 0, out.data_ptr(), N, M * N,
+              1 if out_dtype == torch.float32 else 0, M, N, K, Bt, _lib.stream())
+    return out
+
+
 def wgrad_bias_ok(M, N, K, splits) -> bool:
     """Whether gemm_wgrad_bias takes this weight gradient (dW[M,N] over K tokens, `splits`
     K-slices): the 256-wide ping-pong kernel with >= 16 K-tiles per split."""
