@@ -1,0 +1,429 @@
+// 4-wave 256 x 256 weight-gradient GEMM on MN-major operands: dW[M,N] (+)= alpha * A^T . B with
+// A [K][M] (row stride lda) and B [K][N] (ldb), K = tokens / pixels, both operands read in their
+// stored layout — the reduction runs down the rows, so neither operand is K-contiguous.
+//
+// Reference op: the kernel gradients of tf.layers.dense (/root/reference/distribute_training.py:54,61,
+// taken by the optimizer's compute_gradients at :152).
+//
+// Why a second 4-wave kernel (gemm4w.hip is the K-major one): the 8-wave 256-row loop ran BERT's
+// weight gradients at 29-32 % MFMA utilisation with 41-43 % of wave cycles waiting
+// (profiles/r4_bert_wgrad_pmc_s2.txt), plus a split-K fold pass over fp32 slabs (~17-22 ms per
+// BERT-Large step). Here:
+//  * operand tiles [64 k-rows][256 columns] reach LDS by LDS-DMA (16 B per lane) in their HBM
+//    layout; the MFMA fragments (8 consecutive k of one column per lane) come out of LDS with the
+//    CDNA4 transposing read ds_read_b64_tr_b16 (4 k-rows x 16 columns per 16-lane group, two
+//    reads per 16x32 fragment) — no transpose pass, no VALU shuffles;
+//  * LDS rows are 512 B; the 32-B slot of columns 16j..16j+15 in k-row r sits at slot
+//    j ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2: the 8 k-rows one half-wave's transposed
+//    read touches (rows 8g + q, g = the half's two groups, q = 0..3) land on 8 different bank
+//    groups (conflict-free); the DMA applies the same XOR when choosing which global chunk each
+//    lane fetches, so the LDS side stays lane-linear;
+//  * accumulators: 64 AGPR tiles per wave (inline-asm MFMA, "+a"), the schedule of gemm4w's
+//    SCHED 2 (two barriers per K-tile, DMA of K-tile kt + 2 under K-step 1's MFMAs);
+//  * split-K without a fold pass: every split stores its fp32 partial tile lane-linear (1 KB per
+//    store instruction), the LAST split of a tile to arrive (per-tile counter) sums the tile's
+//    partials in split order (deterministic) and writes dW (+= with beta);
+//  * RS: the bias gradient rowsum(A^T) = column sums of dY from the A fragments already in
+//    registers, as an MFMA against a ones operand (D = 1 . A): 4 extra MFMAs per K-step and wave
+//    on 1 / tiles_n of the K-tiles (spread over the tile columns).
+#include "gemm_conv.h"
+
+#include <type_traits>
+
+typedef __attribute__((ext_vector_type(4))) int ttd_i32x4_t;
+typedef __attribute__((ext_vector_type(4))) short ttd_s16x4_t;
+
+namespace ttdk {
+namespace {
+namespace g4t {
+
+constexpr int T = 256;
+constexpr int OPB = 64 * 512;    // one operand's K-tile image: 64 k-rows x 256 bf16 columns
+constexpr int SB = 2 * OPB;      // A stages at 0 / OPB, B stages at SB / SB + OPB
+constexpr int SMEM = 4 * OPB;    // 128 KB
+constexpr int SLAB = 256 * 256;  // floats of one split's partial tile
+constexpr int kLgkm0 = 0xC07F;   // s_waitcnt encoding: lgkmcnt(0), vmcnt / expcnt not waited
+
+typedef __attribute__((address_space(3))) char lds_char_t;
+typedef __attribute__((address_space(3))) ttd_s16x4_t lds_s4_t;
+
+__device__ __forceinline__ ttd_i32x4_t make_srd(const void* p, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  ttd_i32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane(static_cast<int>(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane(static_cast<int>((a >> 32) & 0xffffu));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
+  r[3] = 0x00020000;
+  return r;
+}
+
+__device__ __forceinline__ void dma_piece(uint32_t m0v, uint32_t voff, const ttd_i32x4_t& srd, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(m0v), "v"(voff), "s"(srd), "s"(soff)
+      : "memory");
+}
+
+template <int N, class F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+
+// MN-major operand loader: K-tile image [64 k-rows][512 B]; piece i (0..7) of thread tid fills
+// LDS chunk i * 256 + tid = k-row i * 8 + tid / 32, physical 16-B chunk tid % 32, i.e. 32-B slot
+// (tid % 32) / 2, which holds logical slot ((tid % 32) / 2) ^ f(row). f depends on the piece only
+// through i & 1, so two per-lane offsets cover the 8 pieces; the k-row step (i * 8 rows) and the
+// K-tile offset are scalar (soffset). Columns past the operand's end are clamped to its last 8
+// (their outputs are never stored).
+struct LoadMN {
+  ttd_i32x4_t srd;
+  uint32_t voff[2];
+  int row8;  // bytes of 8 k-rows
+  __device__ __forceinline__ void init(const bf16_t* p, long long ld, int K, int cols, int col0, int tid) {
+    srd = make_srd(p, static_cast<uint32_t>(static_cast<long long>(K) * ld * 2));
+    row8 = static_cast<int>(ld * 16);
+    const int pc = tid & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int f = ((tid >> 5) & 3) | (i << 2);
+      const int col = min(col0 + (((pc >> 1) ^ f) << 4) + (pc & 1) * 8, cols - 8);
+      voff[i] = static_cast<uint32_t>((static_cast<long long>(tid >> 5) * ld + col) * 2);
+    }
+  }
+};
+
+__device__ __forceinline__ ttd_s16x4_t trd(const lds_char_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)p);
+}
+
+__device__ __forceinline__ bf16x8_t cat(const ttd_s16x4_t& lo, const ttd_s16x4_t& hi) {
+  return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// acc (+)= x . y^T, accumulator an AGPR operand (FIRST: C = 0). "memory": keeps the compiler's
+// LDS reads where the schedule puts them (between MFMAs) instead of hoisting / sinking them.
+template <bool FIRST>
+__device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& x, const bf16x8_t& y) {
+  if constexpr (FIRST)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(y), "v"(x) : "memory");
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(y), "v"(x) : "memory");
+}
+// column sums of a fragment: c[.][col] += sum_k x[k][col] (D = ones . x). Wait states hipcc does
+// not insert around asm: the leading s_nop 1 (hipcc may rematerialise `ones` or zero `c` — VALU
+// writes — right before; a VALU-written MFMA operand needs 2), and after the LAST of a group
+// (TAIL) s_nop 11: the VGPR result may be read or moved by compiler code next, and an 8-pass
+// MFMA's D needs 12 states before any reader but a chained MFMA (a missing tail read stale sums
+// of the group's last block).
+template <bool TAIL>
+__device__ __forceinline__ void mfma_rs(f32x4_t& c, const bf16x8_t& ones, const bf16x8_t& x) {
+  if constexpr (TAIL)
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\ts_nop 11" : "+v"(c) : "v"(ones), "v"(x)
+                 : "memory");
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(ones), "v"(x) : "memory");
+}
+
+__device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int group, int& tm, int& tn) {
+  const int per = group * tiles_n;
+  const int g0 = (t / per) * group;
+  const int gm = min(tiles_m - g0, group);
+  const int r = t - (t / per) * per;
+  tm = g0 + r % gm;
+  tn = r / gm;
+}
+
+// fragment read order of a K-step (first use in the a-major MFMA sweep): 0: A0, 1..8: B0..B7,
+// 9..15: A1..A7; two transposed reads (k-rows +0..3, +4..7 of each lane group) per fragment
+constexpr bool fr_is_a(int r) { return r == 0 || r >= 9; }
+constexpr int fr_blk(int r) { return r == 0 ? 0 : (r <= 8 ? r - 1 : r - 8); }
+
+template <bool RS>
+__global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__ A, long long lda,
+                                                     const bf16_t* __restrict__ B, long long ldb, int M, int N, int K,
+                                                     int tiles_m, int tiles_n, int splits, int kt_per,
+                                                     float* __restrict__ ws, float* __restrict__ out, int beta,
+                                                     float alpha, int* __restrict__ ctr, float* __restrict__ rsw) {
+  // 1 KB aligned: the read bases' bits 5..9 are the lane's own, so a column block is one XOR
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM + 16];
+  // the epilogue's arguments into SGPRs now: loaded lazily behind the main loop's first K-tile,
+  // a pending scalar load at the loop header makes hipcc's LDS-read waits there lgkmcnt(0)
+  // (scalar loads complete out of order)
+  asm volatile("" : "+s"(out), "+s"(ws), "+s"(ctr), "+s"(rsw), "+s"(beta), "+s"(alpha));
+  const int tiles = tiles_m * tiles_n;
+  // XCD-contiguous work index, split-major: the ~32 workgroups of one XCD share a K range and a
+  // block of 8 tile rows (tile_of), so their A / B panels are read once into that XCD's L2
+  const int w = xcd_remap(blockIdx.x, tiles * splits);
+  const int split = w / tiles, t = w - split * tiles;
+  int tm, tn;
+  tile_of(t, tiles_m, tiles_n, 8, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kt0 = split * kt_per;
+  const int nk = min(kt_per, K / 64 - kt0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int i16 = lane & 15, g = lane >> 4, q = i16 >> 2, p = i16 & 3;
+  const int f = q | ((g & 1) << 2);
+
+  lds_char_t* const lds = (lds_char_t*)smem;
+  // per-lane read base of column block 0 of the wave's A / B columns per stage; block j is
+  // base ^ (32 j) (the slot XOR: 32 (j ^ f) = 32 j ^ 32 f), K-step and half are immediates
+  // (s * 16384 + h * 2048)
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
+  const uint32_t lanep = static_cast<uint32_t>((8 * g + q) * 512 + 8 * p + 32 * f);
+  const uint32_t bA0 = sb + lanep + wm * 256, bB0 = sb + SB + lanep + wn * 256;
+  const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
+  LoadMN la, lb;
+  la.init(A, lda, K, M, m0, tid);
+  lb.init(B, ldb, K, N, n0, tid);
+  const int kstride_a = static_cast<int>(lda * 128), kstride_b = static_cast<int>(ldb * 128);  // bytes per K-tile
+
+  f32x4_t acc[8][8];
+  ttd_s16x4_t fl[2][16], fh[2][16];  // [set][fragment: 0..7 A, 8..15 B] low / high k halves
+  f32x4_t rsacc[4];
+  bf16x8_t ones;
+  if constexpr (RS) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rsacc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    ones = __builtin_bit_cast(bf16x8_t, ttd_i32x4_t{0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80});
+  }
+
+  // read r (0..31) of K-step S of the image in stage st into fragment set SET
+  auto rd1 = [&](auto R, auto S, int st, auto SET) {
+    constexpr int r = decltype(R)::value, s = decltype(S)::value, set = decltype(SET)::value;
+    constexpr int fr = r / 2, h = r % 2, blk = fr_blk(fr);
+    constexpr int imm = s * 16384 + h * 2048;
+    const uint32_t base = (fr_is_a(fr) ? bA0 : bB0) + st * OPB;
+    const ttd_s16x4_t v = trd((const lds_char_t*)(uintptr_t)((blk ? (base ^ (32u * blk)) : base) + imm));
+    constexpr int slot = fr_is_a(fr) ? blk : 8 + blk;
+    if constexpr (h == 0) fl[set][slot] = v;
+    else fh[set][slot] = v;
+  };
+  auto dma1 = [&](auto Q, int st, int kt) {  // piece q (0..7 A, 8..15 B) of K-tile kt into stage st
+    constexpr int qq = decltype(Q)::value, i = qq & 7;
+    const LoadMN& L = qq < 8 ? la : lb;
+    dma_piece(ldsw + (qq < 8 ? 0 : SB) + st * OPB + i * 4096, L.voff[i & 1], L.srd,
+              (kt0 + kt) * (qq < 8 ? kstride_a : kstride_b) + i * L.row8);
+  };
+  auto fa = [&](int set, int a) { return cat(fl[set][a], fh[set][a]); };
+  auto fb = [&](int set, int b) { return cat(fl[set][8 + b], fh[set][8 + b]); };
+
+  auto ktile = [&](int kt, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
+    const bool has2 = kt + 2 < nk;
+    const int st = kt & 1;
+    const bool rs_on = RS && ((kt0 + kt) % tiles_n == tn);
+    // phase 0: K-step 0 (set 0) | reads of K-step 1 into set 1
+    static_for<64>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, std::integral_constant<int, 1>{}, st, std::integral_constant<int, 1>{});
+      mfma_acc<FIRST>(acc[i / 8][i % 8], fa(0, i / 8), fb(0, i % 8));
+    });
+    if constexpr (RS) {
+      if (rs_on) {  // (wave-uniform branches: no VALU-selected operand)
+        if (wn == 0) {
+          static_for<4>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            mfma_rs<j == 3>(rsacc[j], ones, fa(0, j));
+          });
+        } else {
+          static_for<4>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            mfma_rs<j == 3>(rsacc[j], ones, fa(0, 4 + j));
+          });
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(kLgkm0);  // (a real s_waitcnt: hipcc's own wait tracking sees it)
+    asm volatile("s_barrier" ::: "memory");
+    // phase 1a: first half of K-step 1 | A pieces of K-tile kt + 2 into the freed stage
+    static_for<32>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 4 == 0)
+        if (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
+      mfma_acc<false>(acc[i / 8][i % 8], fa(1, i / 8), fb(1, i % 8));
+    });
+    if constexpr (RS) {
+      if (rs_on) {  // (wave-uniform branches: no VALU-selected operand)
+        if (wn == 0) {
+          static_for<4>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            mfma_rs<j == 3>(rsacc[j], ones, fa(1, j));
+          });
+        } else {
+          static_for<4>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            mfma_rs<j == 3>(rsacc[j], ones, fa(1, 4 + j));
+          });
+        }
+      }
+    }
+    if (has2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    // phase 1b: second half of K-step 1 | B pieces of kt + 2 | reads of K-tile kt + 1, K-step 0
+    static_for<32>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 4 == 1)
+        if (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
+      rd1(std::integral_constant<int, i>{}, std::integral_constant<int, 0>{}, st ^ 1, std::integral_constant<int, 0>{});
+      mfma_acc<false>(acc[4 + i / 8][i % 8], fa(1, 4 + i / 8), fb(1, i % 8));
+    });
+  };
+
+  // prologue: K-tiles 0 and 1 into stages 0 and 1, K-step 0 fragments of K-tile 0
+  static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
+  static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  static_for<32>([&](auto R) { rd1(R, std::integral_constant<int, 0>{}, 0, std::integral_constant<int, 0>{}); });
+  ktile(0, std::true_type{});
+  for (int kt = 1; kt < nk; ++kt) ktile(kt, std::false_type{});
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+
+  // bias-gradient partials: rsw[(split * tiles_n + tn) * M + m] (folded by the host's reduce)
+  if constexpr (RS) {
+    if (g == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 128 + (wn * 4 + j) * 16 + i16;
+        if (m < M) rsw[static_cast<long long>(split * tiles_n + tn) * M + m] = rsacc[j][0];
+      }
+    }
+  }
+  // acc[a][b] = C[m0 + wm*128 + a*16 + i16][n0 + wn*128 + b*16 + 4g .. +3]
+  const bool whole = m0 + 256 <= M && n0 + 256 <= N;
+  auto store = [&](int a, int b, f32x4_t v) {
+    const int m = m0 + wm * 128 + a * 16 + i16, n = n0 + wn * 128 + b * 16 + 4 * g;
+    if (whole || (m < M && n < N)) {
+      f32x4_t* o = reinterpret_cast<f32x4_t*>(out + static_cast<long long>(m) * N + n);
+      if (beta) v += *o;
+      *o = v;
+    }
+  };
+  // rows a..7 re-pinned before row a is read: hipcc would otherwise move all 256 accumulator
+  // reads to the top (VGPR spills)
+  auto pin_from = [&](int a0) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+      if (a >= a0)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+  };
+  if (splits == 1) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      pin_from(a);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) store(a, b, acc[a][b] * alpha);
+    }
+    return;
+  }
+  // split-K: partial tile lane-linear into this split's slab (stored straight from the AGPRs),
+  // release, count arrivals
+  const long long lin = static_cast<long long>(wave * 64) * 64 * 4 + lane * 4;  // + (a * 8 + b) * 256
+  {
+    float* slab = ws + static_cast<long long>(split * tiles + t) * SLAB + lin;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(slab + (a * 8 + b) * 256), "a"(acc[a][b])
+                     : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __threadfence();
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem + SMEM);
+  if (tid == 0) *flag = atomicAdd(ctr + t, 1) == splits - 1;
+  __syncthreads();
+  if (!*flag) return;
+  __threadfence();  // acquire: the other splits' partials
+  // last split of this tile: sum the partials in split order, its own re-read from the slab it
+  // just wrote (deterministic whoever is last; no accumulator stays live through the fold)
+  const float* src0 = ws + static_cast<long long>(t) * SLAB + lin;
+  const long long sstride = static_cast<long long>(tiles) * SLAB;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    f32x4_t v[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v[b] = *reinterpret_cast<const f32x4_t*>(src0 + (a * 8 + b) * 256);
+    for (int s = 1; s < splits; ++s) {
+      const float* src = src0 + s * sstride + a * 8 * 256;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) v[b] += *reinterpret_cast<const f32x4_t*>(src + b * 256);
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) store(a, b, v[b] * alpha);
+  }
+  if (tid == 0) ctr[t] = 0;  // ready for the next launch on this counter block
+}
+
+}  // namespace g4t
+}  // namespace
+}  // namespace ttdk
+
+static int g4t_enabled() {
+  static const int v = ttdk::getenv_int("TTD_G4T", 1);
+  return v;
+}
+
+// floats of workspace ttdk_gemm4t_wgrad needs: split partial tiles + bias-gradient partials
+TTDK_EXPORT long long ttdk_gemm4t_ws(int M, int N, int K, int splits) {
+  using namespace ttdk;
+  const int ktiles = K / 64;
+  if (ktiles < 2) return -1;
+  splits = std::max(1, std::min(splits, ktiles / 2));
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256);
+  return static_cast<long long>(splits) * tiles_m * tiles_n * g4t::SLAB + static_cast<long long>(splits) * tiles_n * M;
+}
+
+// dW[M,N] (+)= alpha * A^T . B, A [K][M] (lda), B [K][N] (ldb) bf16 MN-major, out fp32 contiguous
+// [M][N]; rowsum (optional): bias gradient sum_k A[k][m], written. ws: ttdk_gemm4t_ws floats.
+// Returns hipErrorInvalidValue for shapes this kernel does not take (the caller keeps another path).
+TTDK_EXPORT int ttdk_gemm4t_wgrad(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                                  int splits, float* ws, float* out, int beta, float alpha, float* rowsum,
+                                  hipStream_t st) {
+  using namespace ttdk;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const long long lim = 1LL << 31;
+  if (!g4t_enabled() || K % 64 || K < 128 || M < 8 || N < 8 || M % 8 || N % 8 || lda % 8 || ldb % 8 || lda < M ||
+      ldb < N || !al16(A) || !al16(B) || !al16(out) || static_cast<long long>(K) * lda * 2 >= lim ||
+      static_cast<long long>(K) * ldb * 2 >= lim)
+    return hipErrorInvalidValue;
+  const int ktiles = K / 64;
+  splits = std::max(1, std::min(splits, ktiles / 2));
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
+  int* ctr = nullptr;
+  if (splits > 1) {
+    ctr = big::tile_counters(st, tiles);
+    if (!ctr || !ws) return hipErrorInvalidValue;
+  }
+  if (rowsum && !ws) return hipErrorInvalidValue;
+  float* rsw = rowsum ? ws + static_cast<long long>(splits) * tiles * g4t::SLAB : nullptr;
+  const dim3 grid(tiles * splits);
+  if (rowsum)
+    hipLaunchKernelGGL((g4t::gemm4t_kernel<true>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
+                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw);
+  else
+    hipLaunchKernelGGL((g4t::gemm4t_kernel<false>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
+                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !rowsum) return e;
+  return splitk_reduce(rsw, splits * tiles_n, M, rowsum, 0, st);
+}

@@ -1,6 +1,10 @@
 // Dense bf16 GEMM entry point (+ split-K reduce); kernels in gemm_conv.h.
 #include "gemm_conv.h"
 
+extern "C" int ttdk_gemm4t_wgrad(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                                 int splits, float* ws, float* out, int beta, float alpha, float* rowsum,
+                                 hipStream_t st);
+extern "C" long long ttdk_gemm4t_ws(int M, int N, int K, int splits);
 extern "C" int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                                 const TtdkEpilogue* epi, hipStream_t st);
 
@@ -117,6 +121,12 @@ TTDK_EXPORT int ttdk_gemm_bf16_splitk(const bf16_t* A, long long lda, int a_kmaj
   // a forced tile (tile_m / tile_n != 0, tests and benches) always takes the slab + fold path,
   // which honours it; the in-kernel fold exists for the 256-row kernel at its own BN only
   const bool forced = tile_m != 0 || tile_n != 0;
+  // MN-major operands (weight gradients): the 4-wave transposed-read kernel (gemm4t.hip), its
+  // split-K summed by the last split of each tile
+  if (!forced && !a_kmajor && !b_kmajor && ttdk_gemm4t_ws(M, N, K, splits) <= static_cast<long long>(splits) * M * N) {
+    const int rc = ttdk_gemm4t_wgrad(A, lda, B, ldb, M, N, K, splits, ws, out, beta, alpha, nullptr, st);
+    if (rc != hipErrorInvalidValue) return rc;
+  }
   if (!forced && splits > 1 && vec && bbn && (a_kmajor || M % 8 == 0) && big::inkernel_fold() && ktiles >= splits) {
     int* ctr = big::tile_counters(st, ceil_div(M, big::BM) * ceil_div(N, bbn));
     if (ctr) {
@@ -140,17 +150,22 @@ TTDK_EXPORT int ttdk_gemm_bf16_splitk(const bf16_t* A, long long lda, int a_kmaj
 // splits * ceil(N / 256) * M floats (row-sum partials). Returns hipErrorInvalidValue when the
 // shape does not take the 256-row ping-pong kernel (the caller keeps its column-sum pass).
 TTDK_EXPORT long long ttdk_gemm_wgrad_bias_ws(int M, int N, int K, int splits) {
-  if (big_bn(M, N, K) != 256) return -1;
+  const long long w4 = ttdk_gemm4t_ws(M, N, K, splits);
+  if (big_bn(M, N, K) != 256) return w4;
   const int ktiles = K / 64;
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles;
   splits = ceil_div(ktiles, ceil_div(ktiles, splits));
-  return static_cast<long long>(splits) * M * N + static_cast<long long>(splits) * ceil_div(N, 256) * M;
+  return std::max(w4, static_cast<long long>(splits) * M * N + static_cast<long long>(splits) * ceil_div(N, 256) * M);
 }
 
 TTDK_EXPORT int ttdk_gemm_wgrad_bias(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                                      int splits, float* ws, float* out, int beta, float alpha, float* rowsum,
                                      hipStream_t st) {
+  {
+    const int rc = ttdk_gemm4t_wgrad(A, lda, B, ldb, M, N, K, splits, ws, out, beta, alpha, rowsum, st);
+    if (rc != hipErrorInvalidValue) return rc;
+  }
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!al(A) || !al(B) || lda % 8 || ldb % 8 || M % 8 || N % 8 || K % 64 || big_bn(M, N, K) != 256 || !rowsum)
     return hipErrorInvalidValue;

@@ -53,6 +53,8 @@ _SIGS = {
     "ttdk_gemm_bf16_splitk": [P, L, I, P, L, I, I, I, I, I, P, P, I, F, I, I, P],
     "ttdk_gemm_wgrad_bias": [P, L, P, L, I, I, I, I, P, P, I, F, P, P],
     "ttdk_gemm_wgrad_bias_ws": [I, I, I, I],
+    "ttdk_gemm4t_wgrad": [P, L, P, L, I, I, I, I, P, P, I, F, P, P],
+    "ttdk_gemm4t_ws": [I, I, I, I],
     "ttdk_conv_fwd": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad_bnpro": [P, P, G, P, P, P, E, P],
@@ -139,7 +141,7 @@ def register(sigs: dict):
 
 
 _RESTYPE = {"ttdk_conv_dgrad_subpixel_stat_rows": c_longlong, "ttdk_colsum_ws_floats": c_longlong,
-            "ttdk_gemm_wgrad_bias_ws": c_longlong}
+            "ttdk_gemm_wgrad_bias_ws": c_longlong, "ttdk_gemm4t_ws": c_longlong}
 
 
 def fn(name):

@@ -269,6 +269,34 @@ def gemm_wgrad_bias(dy, x, out, bias_out, splits=1, beta=0, alpha=1.0):
     return out, bias_out
 
 
+def gemm4t(dy, x, out=None, bias_out=None, *, splits=1, beta=0, alpha=1.0):
+    """Weight gradient out[M,N] (+)= alpha * dy^T . x (fp32) on the 4-wave transposed-read kernel
+    (gemm4t.hip), dy [K, M] and x [K, N] bf16 row-major (K = tokens), split-K summed inside the
+    launch; bias_out[M] (optional) = column sums of dy, written. Raises when the kernel does not
+    take the shape (no silent fallback: this entry exists to pin that path)."""
+    _check2d(dy, torch.bfloat16, "dy")
+    _check2d(x, torch.bfloat16, "x")
+    K, M = dy.shape
+    K2, N = x.shape
+    if K != K2:
+        raise ValueError("gemm4t: token dims differ (%d vs %d)" % (K, K2))
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=dy.device)
+    if tuple(out.shape) != (M, N) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("gemm4t: out must be a contiguous fp32 [%d, %d]" % (M, N))
+    if bias_out is not None and (bias_out.numel() != M or bias_out.dtype != torch.float32
+                                 or not bias_out.is_contiguous()):
+        raise ValueError("gemm4t: bias_out must be a contiguous fp32 [%d]" % M)
+    nws = int(_lib.query("ttdk_gemm4t_ws", M, N, K, int(splits)))
+    if nws < 0:
+        raise ValueError("gemm4t: K=%d needs >= 2 K-tiles of 64" % K)
+    ws = torch.empty(max(nws, 1), dtype=torch.float32, device=dy.device)
+    _log("gemm4t", M, N, K, splits)
+    _lib.call("ttdk_gemm4t_wgrad", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K, int(splits),
+              ws.data_ptr(), out.data_ptr(), int(beta), float(alpha), _lib.ptr(bias_out), _lib.stream())
+    return out
+
+
 _C3 = _os.environ.get("TTD_CONV3", "1") != "0"
 
 

@@ -32,6 +32,84 @@ def meta(text, name):
     return out
 
 
+def _regs(tok):
+    """set of (kind, index) for a register operand like v[4:7], v12, a[0:3]"""
+    m = re.match(r"([va])\[(\d+):(\d+)\]", tok)
+    if m:
+        return {(m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.match(r"([va])(\d+)$", tok)
+    return {(m.group(1), int(m.group(2)))} if m else set()
+
+
+def valu_to_mfma(lines):
+    """VALU (or v_accvgpr_write) results read as an A/B operand by an MFMA within the next 2
+    instructions: the hazard needs 2 wait states, which hipcc does not pad for asm MFMAs."""
+    real = []
+    for l in lines:
+        t = l.strip()
+        if not t or t.startswith(";") or t.startswith(".") or t.endswith(":"):
+            continue
+        real.append(t)
+    bad = []
+    for i, t in enumerate(real):
+        if not t.startswith("v_mfma"):
+            continue
+        ops = [o.strip() for o in t.split(None, 1)[1].split(",")]
+        srcs = _regs(ops[1]) | _regs(ops[2])
+        nops = 0
+        for back in range(1, 4):
+            if i - back < 0:
+                break
+            u = real[i - back]
+            if u.startswith("s_nop"):
+                nops += int(u.split()[1]) + 1
+                continue
+            if nops >= 2 or back - 1 + nops >= 2:
+                break
+            if u.startswith("v_") and not u.startswith("v_mfma") and not u.startswith("v_cmp"):
+                dst = u.split(None, 1)[1].split(",")[0].strip() if " " in u else ""
+                if _regs(dst) & srcs:
+                    bad.append(u + "  ->  " + t)
+    return bad
+
+
+def mfma_d_to_reader(lines, states=12):
+    """Non-MFMA instructions that touch a VGPR MFMA result within `states` wait states of the
+    MFMA (8-pass XDL: 12), counting s_nop N as N + 1 states and other instructions as 1."""
+    real = []
+    for l in lines:
+        t = l.strip()
+        if not t or t.startswith(";") or t.startswith(".") or t.endswith(":"):
+            continue
+        real.append(t)
+    bad = []
+    for i, t in enumerate(real):
+        if not t.startswith("v_mfma"):
+            continue
+        dst = _regs(t.split(None, 1)[1].split(",")[0].strip())
+        if not dst or next(iter(dst))[0] != "v":
+            continue
+        n = 0
+        for u in real[i + 1:i + 1 + states]:
+            if n >= states:
+                break
+            if u.startswith("s_nop"):
+                n += int(u.split()[1]) + 1
+                continue
+            if u.startswith("v_mfma"):
+                ops = [o.strip() for o in u.split(None, 1)[1].split(",")]
+                if _regs(ops[3]) == dst:
+                    break  # accumulate chain: no wait states
+            regs = set()
+            for tok in re.split(r"[\s,]+", u.split(None, 1)[1] if " " in u else ""):
+                regs |= _regs(tok)
+            if regs & dst:
+                bad.append(t + "  ->  " + u)
+                break
+            n += 1
+    return bad
+
+
 def audit(body):
     lines = body.splitlines()
     idx = [i for i, l in enumerate(lines) if "v_mfma" in l]
@@ -50,8 +128,9 @@ def audit(body):
             bad.append(l.strip())
         if lo <= i <= hi and "scratch_" in l:
             scratch += 1
+    haz = valu_to_mfma(lines) + mfma_d_to_reader(lines)
     return {"mfma": len(idx), "compiler_accvgpr_in_mfma_region": len(bad), "scratch_ops_in_mfma_region": scratch,
-            "examples": bad[:3]}
+            "valu_to_mfma_hazards": len(haz), "examples": bad[:3] + haz[:3]}
 
 
 def main():
@@ -65,7 +144,7 @@ def main():
         print(name[:90], m, {k: v for k, v in a.items() if k != "examples"})
         for e in a.get("examples", []):
             print("    ", e)
-        if a.get("compiler_accvgpr_in_mfma_region") or (m.get("vgpr_spill_count") or 0):
+        if a.get("compiler_accvgpr_in_mfma_region") or a.get("valu_to_mfma_hazards") or (m.get("vgpr_spill_count") or 0):
             ok = False
     sys.exit(0 if ok else 1)
 
