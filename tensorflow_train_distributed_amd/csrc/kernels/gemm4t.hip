@@ -25,7 +25,9 @@
 //    partials in split order (deterministic) and writes dW (+= with beta);
 //  * RS: the bias gradient rowsum(A^T) = column sums of dY from the A fragments already in
 //    registers, as an MFMA against a ones operand (D = 1 . A): 4 extra MFMAs per K-step and wave
-//    on 1 / tiles_n of the K-tiles (spread over the tile columns).
+//    on 1 / tiles_n of the K-tiles (spread over the tile columns); the last workgroup of a tile
+//    row to finish sums the row's partials (no separate reduce launch: on the side stream of the
+//    BERT step a tiny reduce kernel waited ~200 us per call for a free CU).
 #include "gemm_conv.h"
 
 #include <type_traits>
@@ -149,13 +151,14 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
                                                      const bf16_t* __restrict__ B, long long ldb, int M, int N, int K,
                                                      int tiles_m, int tiles_n, int splits, int kt_per,
                                                      float* __restrict__ ws, float* __restrict__ out, int beta,
-                                                     float alpha, int* __restrict__ ctr, float* __restrict__ rsw) {
+                                                     float alpha, int* __restrict__ ctr, float* __restrict__ rsw,
+                                                     float* __restrict__ rowsum) {
   // 1 KB aligned: the read bases' bits 5..9 are the lane's own, so a column block is one XOR
   __shared__ __attribute__((aligned(1024))) char smem[SMEM + 16];
   // the epilogue's arguments into SGPRs now: loaded lazily behind the main loop's first K-tile,
   // a pending scalar load at the loop header makes hipcc's LDS-read waits there lgkmcnt(0)
   // (scalar loads complete out of order)
-  asm volatile("" : "+s"(out), "+s"(ws), "+s"(ctr), "+s"(rsw), "+s"(beta), "+s"(alpha));
+  asm volatile("" : "+s"(out), "+s"(ws), "+s"(ctr), "+s"(rsw), "+s"(rowsum), "+s"(beta), "+s"(alpha));
   const int tiles = tiles_m * tiles_n;
   // XCD-contiguous work index, split-major: the ~32 workgroups of one XCD share a K range and a
   // block of 8 tile rows (tile_of), so their A / B panels are read once into that XCD's L2
@@ -292,7 +295,8 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
 
-  // bias-gradient partials: rsw[(split * tiles_n + tn) * M + m] (folded by the host's reduce)
+  // bias-gradient partials: rsw[(split * tiles_n + tn) * M + m], summed below by the last of the
+  // splits * tiles_n workgroups of tile row tm to arrive
   if constexpr (RS) {
     if (g == 0) {
 #pragma unroll
@@ -321,6 +325,7 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
 #pragma unroll
         for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
   };
+  const long long lin = static_cast<long long>(wave * 64) * 64 * 4 + lane * 4;  // + (a * 8 + b) * 256
   if (splits == 1) {
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
@@ -328,12 +333,9 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
 #pragma unroll
       for (int b = 0; b < 8; ++b) store(a, b, acc[a][b] * alpha);
     }
-    return;
-  }
-  // split-K: partial tile lane-linear into this split's slab (stored straight from the AGPRs),
-  // release, count arrivals
-  const long long lin = static_cast<long long>(wave * 64) * 64 * 4 + lane * 4;  // + (a * 8 + b) * 256
-  {
+    if constexpr (!RS) return;
+  } else {
+    // split-K: partial tile lane-linear into this split's slab (stored straight from the AGPRs)
     float* slab = ws + static_cast<long long>(split * tiles + t) * SLAB + lin;
 #pragma unroll
     for (int a = 0; a < 8; ++a)
@@ -342,14 +344,32 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
         asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(slab + (a * 8 + b) * 256), "a"(acc[a][b])
                      : "memory");
   }
+  // release the partials, count arrivals: per tile (ctr[t], splits) and per tile row for the
+  // bias gradient (ctr[tiles + tm], splits * tiles_n)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __threadfence();
   __syncthreads();
   int* flag = reinterpret_cast<int*>(smem + SMEM);
-  if (tid == 0) *flag = atomicAdd(ctr + t, 1) == splits - 1;
+  if (tid == 0) {
+    flag[0] = splits > 1 && atomicAdd(ctr + t, 1) == splits - 1;
+    flag[1] = RS && atomicAdd(ctr + tiles + tm, 1) == splits * tiles_n - 1;
+  }
   __syncthreads();
-  if (!*flag) return;
-  __threadfence();  // acquire: the other splits' partials
+  const bool last_tile = flag[0], last_row = flag[1];
+  if (!last_tile && !last_row) return;
+  __threadfence();  // acquire: the other workgroups' partials
+  if constexpr (RS) {
+    if (last_row) {
+      const int m = m0 + tid;
+      if (m < M) {
+        float sum = 0.f;  // fixed order (deterministic whoever is last)
+        for (int q = 0; q < splits * tiles_n; ++q) sum += rsw[static_cast<long long>(q) * M + m];
+        rowsum[m] = sum;
+      }
+      if (tid == 0) ctr[tiles + tm] = 0;
+    }
+  }
+  if (!last_tile) return;
   // last split of this tile: sum the partials in split order, its own re-read from the slab it
   // just wrote (deterministic whoever is last; no accumulator stays live through the fold)
   const float* src0 = ws + static_cast<long long>(t) * SLAB + lin;
@@ -410,20 +430,17 @@ TTDK_EXPORT int ttdk_gemm4t_wgrad(const bf16_t* A, long long lda, const bf16_t* 
   splits = ceil_div(ktiles, per);
   const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
   int* ctr = nullptr;
-  if (splits > 1) {
-    ctr = big::tile_counters(st, tiles);
+  if (splits > 1 || rowsum) {
+    ctr = big::tile_counters(st, tiles + tiles_m);
     if (!ctr || !ws) return hipErrorInvalidValue;
   }
-  if (rowsum && !ws) return hipErrorInvalidValue;
   float* rsw = rowsum ? ws + static_cast<long long>(splits) * tiles * g4t::SLAB : nullptr;
   const dim3 grid(tiles * splits);
   if (rowsum)
     hipLaunchKernelGGL((g4t::gemm4t_kernel<true>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
-                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw);
+                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum);
   else
     hipLaunchKernelGGL((g4t::gemm4t_kernel<false>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
-                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !rowsum) return e;
-  return splitk_reduce(rsw, splits * tiles_n, M, rowsum, 0, st);
+                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum);
+  return hipGetLastError();
 }

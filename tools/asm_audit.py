@@ -14,7 +14,7 @@ import sys
 def kernels(text):
     for m in re.finditer(r"^(_Z\S+):(?:\s*;.*)?$", text, re.M):
         name = m.group(1)
-        end = text.find("s_endpgm", m.end())
+        end = text.find(".Lfunc_end", m.end())  # (a kernel can have several s_endpgm)
         yield name, text[m.end():end]
 
 
@@ -112,7 +112,10 @@ def mfma_d_to_reader(lines, states=12):
 
 def audit(body):
     lines = body.splitlines()
-    idx = [i for i, l in enumerate(lines) if "v_mfma" in l]
+    # the region the AGPR accumulators are live in: first .. last MFMA writing an AGPR
+    idx = [i for i, l in enumerate(lines) if "v_mfma" in l and l.split(None, 1)[1].lstrip().startswith("a")]
+    if not idx:
+        idx = [i for i, l in enumerate(lines) if "v_mfma" in l]
     if not idx:
         return {"mfma": 0}
     lo, hi = idx[0], idx[-1]
@@ -129,7 +132,7 @@ def audit(body):
         if lo <= i <= hi and "scratch_" in l:
             scratch += 1
     haz = valu_to_mfma(lines) + mfma_d_to_reader(lines)
-    return {"mfma": len(idx), "compiler_accvgpr_in_mfma_region": len(bad), "scratch_ops_in_mfma_region": scratch,
+    return {"mfma": sum("v_mfma" in l for l in lines), "compiler_accvgpr_in_mfma_region": len(bad), "scratch_ops_in_mfma_region": scratch,
             "valu_to_mfma_hazards": len(haz), "examples": bad[:3] + haz[:3]}
 
 
