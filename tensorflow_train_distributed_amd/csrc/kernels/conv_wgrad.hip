@@ -1,6 +1,11 @@
 // Convolution weight gradient (split-K); kernels in gemm_conv.h.
 #include "gemm_conv.h"
 
+extern "C" int ttdk_gemm4t_wgrad(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                                 int splits, float* ws, float* out, int beta, float alpha, float* rowsum,
+                                 hipStream_t st);
+extern "C" long long ttdk_gemm4t_ws(int M, int N, int K, int splits);
+
 // dw[K,R,S,C] (fp32) = sum over pixels of dy ⊗ im2col(x). `ws` is a split-K workspace of
 // splits*K*R*S*C floats (may be null when splits == 1, then dw is written directly).
 TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkConv* g, float* dw, float* ws,
@@ -15,6 +20,13 @@ TTDK_EXPORT int ttdk_conv_wgrad(const bf16_t* x, const bf16_t* dy, const TtdkCon
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);
   if (splits > 1 && !ws) return hipErrorInvalidValue;
+  // unit-stride 1x1 convs with >= 256 output and input channels: the 4-wave transposed-read
+  // kernel (gemm4t.hip), split-K summed by the last split of each tile
+  if (bbn && is_pointwise(g) && M >= 256 && N >= 256 &&
+      (splits == 1 || ttdk_gemm4t_ws(M, N, K, splits) <= static_cast<long long>(splits) * M * N)) {
+    const int rc = ttdk_gemm4t_wgrad(dy, g->K, x, g->C, M, N, K, splits, ws, dw, beta, 1.f, nullptr, st);
+    if (rc != hipErrorInvalidValue) return rc;
+  }
   EpiParams pe{};
   pe.alpha = 1.f;
   pe.ldo = N;

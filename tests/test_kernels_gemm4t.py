@@ -73,3 +73,19 @@ def test_wgrad_bias_entry_takes_gemm4t():
     G.gemm_wgrad_bias(dy, x, out, bias, splits=splits)
     assert _rel(out, dy.float().t() @ x.float()) < 1e-5
     assert _rel(bias, dy.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("beta", [0, 1])
+def test_conv_wgrad_1x1_takes_gemm4t(beta):
+    """ops.gemm.conv_wgrad of a unit-stride 1x1 conv with >= 256 input and output channels (the
+    ResNet-50 stage 3/4 weight gradients) runs on the 4-wave transposed-read kernel."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(13)
+    x = (torch.rand(8, 16, 16, 256, device="cuda") * 2 - 1).bfloat16()
+    dy = (torch.rand(8, 16, 16, 512, device="cuda") * 2 - 1).bfloat16()
+    ref = dy.reshape(-1, 512).float().t() @ x.reshape(-1, 256).float()
+    out = torch.randn(512, 1, 1, 256, device="cuda")
+    old = out.clone()
+    G.conv_wgrad(x, dy, (512, 1, 1, 256), out=out, beta=beta, splits=4)
+    want = ref + (old.view(512, 256) if beta else 0)
+    assert _rel(out.view(512, 256), want) < 1e-5
