@@ -53,10 +53,9 @@ def build_resnet(args, dev, rank, world):
     else:
         opt = FlatSGD(model.params, Schedule(kind=2, base_lr=0.1 * B * world / 256, warmup_steps=5, end_lr=0.0,
                                              power=2.0, total_steps=10000), momentum=0.9, weight_decay=5e-5)
-    # the collectives hide under the backward: ~44 ms at 1024 images on one MI355X,
-    # the CTA-budget probe of the native engine weighs the gradient bytes against it
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16,
-                                 overlap_ms=44.0 * B / 1024 * (args.image_size / 224) ** 2)
+    # the backward window the collectives hide under is measured on a warm-up step (main) and
+    # fed to the native engine's CTA-budget choice (BucketedAllReducer.retune)
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
     g = torch.Generator(device=dev)
     g.manual_seed(rank)
     S = args.image_size
@@ -103,9 +102,8 @@ def build_bert(args, dev, rank, world):
     broadcast_flat_(model.params)
     opt = FlatLAMB(model.params, Schedule(kind=2, base_lr=4e-3, warmup_steps=100, end_lr=0.0, power=1.0,
                                           total_steps=10000), weight_decay=0.01, max_grad_norm=1.0)
-    # backward ~120 ms at 128 sequences of 512
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16,
-                                 overlap_ms=120.0 * B / 128 * S / 512)
+    # (overlap window: measured on a warm-up step, see main)
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
     batch = synthetic_batch(cfg, B, S, max_predictions=80 if S >= 512 else 20, device=dev, seed=rank)
 
     def step():
@@ -280,6 +278,21 @@ def main():
     # stream has been exercised on one-rank communicators but never across real ranks (no
     # multi-GPU box is reachable from the build loop), so N > 1 stays eager until a two-rank
     # replay has been checked against eager; --graph 1 / TTD_BENCH_GRAPH=1 opt in.
+    red_m = getattr(step, "reducer", None)
+    window_ms = None
+    if world > 1 and not on_cpu and getattr(red_m, "comm", None) is not None:
+        # the overlap window the collectives hide under, MEASURED on one eager warm-up step (the
+        # backward after the first bucket is ready, max over ranks), re-decides the engine's CTA
+        # budget from its start-up probe table (rccl.retune) instead of a per-model constant
+        red_m.measure_window()
+        step()
+        sync()
+        w = red_m.window_ms()
+        wt = torch.tensor([w if w is not None else -1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
+        window_ms = float(wt.item())
+        if window_ms > 0:
+            red_m.retune(window_ms)
     auto_graph = 1 if world == 1 else int(os.environ.get("TTD_BENCH_GRAPH", "0"))
     use_graph = args.graph if args.graph >= 0 else auto_graph
     red0 = getattr(step, "reducer", None)
@@ -459,6 +472,13 @@ def main():
             dinfo["buckets"] = len(red.buckets)
             dinfo["allreduce_dtype"] = "bf16" if red.compress else "fp32"
             dinfo["collective_engine"] = red.engine
+            if world > 1:
+                # per bucket: bytes and the path it took (direct xGMI one-/two-shot or RCCL)
+                dinfo["bucket_bytes"] = [(e - s_) * (2 if red.compress else 4) for s_, e in red.buckets]
+                dinfo["bucket_paths"] = red.bucket_paths
+                if red.ipc is None and red.ipc_reason:
+                    dinfo["ipc_allreduce_unavailable"] = red.ipc_reason
+                dinfo["overlap_window_ms"] = round(window_ms, 3) if window_ms else None
             if world > 1 and red.comm is None and backend == "nccl":
                 from tensorflow_train_distributed_amd.parallel import rccl
                 dinfo["native_engine_unavailable"] = rccl.failure_reason() or os.environ.get("TTD_COLLECTIVE")

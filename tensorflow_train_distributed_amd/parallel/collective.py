@@ -104,11 +104,95 @@ class BucketedAllReducer:
         if self.comm is not None and compress_bf16 and self.buckets:
             # the bf16 staging buffer at its final size before any step can be graph-captured
             self.comm.reserve(max(e - s for s, e in self.buckets))
+        # direct xGMI all-reduce (parallel/ipc.py) for the first and last buckets of a
+        # single-node group: one-shot <= 1 MB, two-shot <= 8 MB; RCCL keeps the rest
+        self.ipc = None
+        self.ipc_reason = None
+        self._paths = [0] * len(self.buckets)
+        if self.comm is not None and self.world > 1 and not compress_bf16 and flat.grad.is_cuda:
+            from . import ipc as ipcm
+            if not ipcm.enabled():
+                self.ipc_reason = "disabled (TTD_IPC_AR=0)"
+            else:
+                same = ipcm.group_same_node(group)
+                paths = ipcm.plan_paths([(e - s) * 4 for s, e in self.buckets], self.world, same)
+                # whole 16-B vectors at 16-B aligned offsets only (same layout on every rank)
+                paths = [p if (s % 4 == 0 and (e - s) % 4 == 0) else ipcm.RCCL
+                         for p, (s, e) in zip(paths, self.buckets)]
+                if not same:
+                    self.ipc_reason = "group spans several nodes"
+                elif any(p != ipcm.RCCL for p in paths):
+                    try:
+                        self.ipc = ipcm.IpcAllReducer(group)
+                    except Exception as e:  # noqa: BLE001 - every rank raised together: all use RCCL
+                        self.ipc_reason = "%s: %s" % (type(e).__name__, e)
+                    if self.ipc is not None:
+                        why = self._ipc_selfcheck()
+                        if why:
+                            self.ipc.destroy()
+                            self.ipc, self.ipc_reason = None, why
+                        else:
+                            self._paths = paths
         self._next = 0
         self._works = []
         self._keep = []
         self._timed = None
+        self._window = None
         self.launch_log: List[int] = []
+
+    def _ipc_selfcheck(self) -> Optional[str]:
+        """Both direct paths on a known pattern (sum of rank + 1), every rank voting: the paths
+        are used only if they return the right sum without a barrier timeout on EVERY rank."""
+        from . import ipc as ipcm
+        why = ""
+        try:
+            r = dist.get_rank(self.group)
+            want = self.world * (self.world + 1) / 2
+            for path, n in ((ipcm.ONE_SHOT, 64 * 1024), (ipcm.TWO_SHOT, 768 * 1024)):
+                t = torch.full((n,), float(r + 1), dtype=torch.float32, device=self.flat.grad.device)
+                self.ipc.all_reduce_(t, path)
+                if not bool(torch.all(t == want).item()):
+                    why = "self-check: %s returned a wrong sum" % ipcm.PATH_NAMES[path]
+            if not why and self.ipc.timed_out():
+                why = "self-check: a barrier timed out"
+        except Exception as e:  # noqa: BLE001 - voted below
+            why = "self-check: %s: %s" % (type(e).__name__, e)
+        flag = torch.tensor([0 if why else 1], dtype=torch.int32, device=self.flat.grad.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 1:
+            return None
+        return why or "self-check failed on another rank"
+
+    @property
+    def bucket_paths(self) -> List[str]:
+        """Path of every bucket: "ipc_oneshot" / "ipc_twoshot" (direct xGMI), "rccl" (native
+        engine), or the torch backend's name."""
+        from .ipc import PATH_NAMES
+        if self.comm is None:
+            return [self.engine] * len(self.buckets)
+        return [PATH_NAMES[p] for p in self._paths]
+
+    def measure_window(self):
+        """Record, in the next step, how long the backward runs on after the first bucket is
+        ready (the window the collectives can hide under): `window_ms()` afterwards."""
+        if self.flat.grad.is_cuda:
+            self._window = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), False]
+
+    def window_ms(self) -> Optional[float]:
+        w, self._window = self._window, None
+        if w is None or not w[2]:
+            return None
+        w[1].synchronize()
+        return float(w[0].elapsed_time(w[1]))
+
+    def retune(self, overlap_ms: float):
+        """Re-decide the native engine's CTA budget from a measured overlap window (collective:
+        every rank calls it with the same value, e.g. the MAX over ranks of window_ms())."""
+        if self.comm is None:
+            return
+        from . import rccl
+        self.comm = rccl.retune(self.group, self.comm, float(overlap_ms),
+                                [(e - s) * (2 if self.compress else 4) for s, e in self.buckets])
 
     def _make_buckets(self):
         """Greedy buckets on variable boundaries: the first `first_bucket_mb` (communication
@@ -181,11 +265,18 @@ class BucketedAllReducer:
             # from the first bucket on, RCCL CTAs may hold CUs: persistent grids launched from
             # here to finish() use the remaining ones
             self._reserve(True)
+            if self._window is not None:
+                self._window[0].record()
         if self.comm is not None:
             # in place on the communicator stream, ordered after the current (producing) stream;
             # under a segmented hipGraph capture the fork is an event node pair and the
             # communicator stream records its own linear graph segments (utils/graphs.py)
             from ..utils import graphs
+            if self.ipc is not None and self._paths[i] != 0:
+                # direct xGMI one-/two-shot on the communicator stream (same ordering as RCCL)
+                graphs.fork(torch.cuda.current_stream(), self.comm.stream)
+                self.ipc.all_reduce_(t, self._paths[i], stream=self.comm.stream)
+                return
             if graphs.capturing_segmented():
                 graphs.fork(torch.cuda.current_stream(), self.comm.stream)
                 self.comm.bucket(t, algorithm=self.algorithm, compress=self.compress, fork=False)
@@ -244,6 +335,9 @@ class BucketedAllReducer:
             self._launch(self._next)
             self._next += 1
         self._reserve(False)
+        if self._window is not None:
+            self._window[1].record()  # the backward's last queued work
+            self._window[2] = True
         if self.comm is not None:
             if self._timed is not None:
                 self._timed[0].record()  # the backward's last queued work

@@ -498,6 +498,32 @@ def for_group(group=None, required: bool = False, overlap_ms=None, bucket_bytes=
     return None
 
 
+def retune(group, comm: RcclCommunicator, overlap_ms: float, bucket_bytes) -> RcclCommunicator:
+    """Re-decide the CTA budget with a MEASURED overlap window (the warm-up step's backward,
+    collective.BucketedAllReducer.window_ms, MAX over ranks so every rank decides alike) from the
+    start-up probe table already held in `comm.policy`; when the budget changes, a communicator
+    with the new budget replaces `comm` (collective: every rank of `group` calls it with the same
+    arguments). Returns the communicator to use."""
+    pol = getattr(comm, "policy", None) or {}
+    probes = pol.get("probe")
+    if not probes:
+        return comm  # fixed budget (TTD_RCCL_MAX_CTAS / TTD_RCCL_PROBE=0): nothing to re-decide
+    new = choose_cta_budget({int(k): v for k, v in probes.items()}, bucket_bytes or [32 << 20],
+                            dist.get_world_size(group), overlap_ms)
+    new["overlap_source"] = "measured (warm-up step backward, max over ranks)"
+    if int(new["cta_budget"]) == int(comm.max_ctas):
+        comm.policy = new
+        return comm
+    (uid,) = broadcast_unique_ids(group, 1, comm.device)
+    fresh = RcclCommunicator(uid, dist.get_world_size(group), dist.get_rank(group), comm.device,
+                             max_ctas=int(new["cta_budget"]))
+    fresh.policy = new
+    comm.synchronize()
+    comm.destroy(abort=False)
+    _COMMS[_key(group)] = fresh
+    return fresh
+
+
 def failure_reason(group=None) -> Optional[str]:
     return _FAILED.get(_key(group))
 
