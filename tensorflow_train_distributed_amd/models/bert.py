@@ -149,6 +149,9 @@ class BertPretraining:
         # CUs leave room for the data-gradient chain's kernels (b128: 180.0 -> 176.8 ms/step over
         # two A/B pairs; 128: 177.4); TTD_BERT_WGRAD_WGS
         self.wgrad_wgs = int(os.environ.get("TTD_BERT_WGRAD_WGS", "192"))
+        # side-stream weight gradients that would overlap a LayerNorm backward start after it
+        # (TTD_BERT_LN_YIELD=0: as soon as their operands exist)
+        self.ln_yield = os.environ.get("TTD_BERT_LN_YIELD", "1") != "0"
         # encoder weight gradients on a second HIP stream (TTD_WGRAD_STREAM=0: single stream)
         self.wgrad_stream = os.environ.get("TTD_WGRAD_STREAM", "1") != "0" and self.device.type == "cuda"
         # data-gradient GEMMs read [in][out] copies of the encoder weights (K-major B: ~10 % faster
@@ -345,16 +348,36 @@ class BertPretraining:
             if bout is not None:
                 K.colsum(dy, out=bout)
 
-        def wgrad_bias(dy, x, wout, bout):
+        deferred = []
+
+        def wgrad_bias(dy, x, wout, bout, defer=False):
             """weight gradient (+ bias column sum unless bout is None: the producer's epilogue
-            already emitted it) on the side stream"""
+            already emitted it) on the side stream. defer=True: queued until flush_wgrads(),
+            called right after the next LayerNorm backward is enqueued — the side stream then
+            starts it only once that LN backward has finished, instead of holding CUs the
+            LN backward needs (TTD_BERT_LN_YIELD)."""
             if side is None:
                 wgrad_and_bias(dy, x, wout, bout)
+                return
+            keep.extend((dy, x))  # alive until the streams join (no deferred record_stream frees)
+            if defer and self.ln_yield:
+                deferred.append((dy, x, wout, bout))
                 return
             graphs.fork(torch.cuda.current_stream(), side)
             with torch.cuda.stream(side):
                 wgrad_and_bias(dy, x, wout, bout)
-            keep.extend((dy, x))  # alive until the streams join (no deferred record_stream frees)
+
+        def flush_wgrads():
+            if not deferred:
+                return
+            graphs.fork(torch.cuda.current_stream(), side)
+            with torch.cuda.stream(side):
+                for a in deferred:
+                    if isinstance(a, str):
+                        hook(a)  # a gradient-ready hook queued behind the deferred work
+                    else:
+                        wgrad_and_bias(*a)
+            deferred.clear()
 
         wt_ready = None
         if self.transposed_dgrad:
@@ -369,6 +392,8 @@ class BertPretraining:
         def layer_hook(name):
             if side is None:
                 hook(name)
+            elif deferred:
+                deferred.append(name)  # after the deferred weight gradients it covers
             else:
                 with torch.cuda.stream(side):
                     hook(name)
@@ -484,6 +509,7 @@ class BertPretraining:
                                        g[self._ln(l, "output/LayerNorm/gamma")],
                                        g[self._ln(l, "output/LayerNorm/beta")], ds_out=G1, want_dx=True, p_in=hd,
                                        site_in=site(l, 2), rng=rng, work=ln_work)
+            flush_wgrads()
             del dy
             wgrad_bias(dout2, inter, g[self._ln(l, "output/dense/kernel")], g[self._ln(l, "output/dense/bias")])
             b_inter = g[self._ln(l, "intermediate/dense/bias")]
@@ -497,7 +523,7 @@ class BertPretraining:
             else:
                 dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre)
             del dout2, inter, pre
-            wgrad_bias(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")], b_inter)
+            wgrad_bias(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")], b_inter, defer=True)
             self._dgrad(dpre, l, 2, out=G1, beta=1)
             del dpre
             layer_hook(self._ln(l, "intermediate/dense/bias"))
@@ -506,6 +532,7 @@ class BertPretraining:
                                        g[self._ln(l, "attention/output/LayerNorm/gamma")],
                                        g[self._ln(l, "attention/output/LayerNorm/beta")], ds_out=G0, want_dx=True,
                                        p_in=hd, site_in=site(l, 1), rng=rng, work=ln_work)
+            flush_wgrads()
             del G1
             wgrad_bias(dproj, ao, g[self._ln(l, "attention/output/dense/kernel")],
                        g[self._ln(l, "attention/output/dense/bias")])
@@ -516,12 +543,13 @@ class BertPretraining:
                             dqkv[:, H:2 * H], dqkv[:, 2 * H:], B, NH, S, delta=delta, seqlen=seqlen, p_drop=ad,
                             rng=rng, site=site(l, 0))
             del dao, ao, qkv
-            wgrad_bias(dqkv, x, self._fused(l, "gw"), self._fused(l, "gb"))
+            wgrad_bias(dqkv, x, self._fused(l, "gw"), self._fused(l, "gb"), defer=l > 0)
             self._dgrad(dqkv, l, 0, out=G0, beta=1)
             del dqkv
             layer_hook(self._ln(l, "attention/self/value/bias"))
             dy = G0
         if side is not None:
+            flush_wgrads()
             graphs.join(torch.cuda.current_stream(), side)
         keep.clear()
 
