@@ -151,7 +151,8 @@ class BertPretraining:
         self.wgrad_wgs = int(os.environ.get("TTD_BERT_WGRAD_WGS", "192"))
         # side-stream weight gradients that would overlap a LayerNorm backward start after it
         # (TTD_BERT_LN_YIELD=0: as soon as their operands exist)
-        self.ln_yield = os.environ.get("TTD_BERT_LN_YIELD", "1") != "0"
+        # (2: also the attention backward)
+        self.ln_yield = int(os.environ.get("TTD_BERT_LN_YIELD", "1"))
         # encoder weight gradients on a second HIP stream (TTD_WGRAD_STREAM=0: single stream)
         self.wgrad_stream = os.environ.get("TTD_WGRAD_STREAM", "1") != "0" and self.device.type == "cuda"
         # data-gradient GEMMs read [in][out] copies of the encoder weights (K-major B: ~10 % faster
@@ -360,7 +361,7 @@ class BertPretraining:
                 wgrad_and_bias(dy, x, wout, bout)
                 return
             keep.extend((dy, x))  # alive until the streams join (no deferred record_stream frees)
-            if defer and self.ln_yield:
+            if defer and self.ln_yield > 0:
                 deferred.append((dy, x, wout, bout))
                 return
             graphs.fork(torch.cuda.current_stream(), side)
@@ -532,16 +533,19 @@ class BertPretraining:
                                        g[self._ln(l, "attention/output/LayerNorm/gamma")],
                                        g[self._ln(l, "attention/output/LayerNorm/beta")], ds_out=G0, want_dx=True,
                                        p_in=hd, site_in=site(l, 1), rng=rng, work=ln_work)
-            flush_wgrads()
+            if self.ln_yield != 2:
+                flush_wgrads()
             del G1
             wgrad_bias(dproj, ao, g[self._ln(l, "attention/output/dense/kernel")],
-                       g[self._ln(l, "attention/output/dense/bias")])
+                       g[self._ln(l, "attention/output/dense/bias")], defer=self.ln_yield == 2)
             dao = self._dgrad(dproj, l, 1)
             del dproj
             dqkv = torch.empty((Tk, 3 * H), dtype=bf, device=dev)
             T.attention_bwd(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], ao, dao, lse, dqkv[:, :H],
                             dqkv[:, H:2 * H], dqkv[:, 2 * H:], B, NH, S, delta=delta, seqlen=seqlen, p_drop=ad,
                             rng=rng, site=site(l, 0))
+            if self.ln_yield == 2:
+                flush_wgrads()  # (mode 2: the attention backward runs without side-stream GEMMs too)
             del dao, ao, qkv
             wgrad_bias(dqkv, x, self._fused(l, "gw"), self._fused(l, "gb"), defer=l > 0)
             self._dgrad(dqkv, l, 0, out=G0, beta=1)
