@@ -59,14 +59,17 @@ __device__ __forceinline__ ttd_i32x4_t make_srd(const void* p, uint32_t bytes) {
   return r;
 }
 
-__device__ __forceinline__ void dma_piece(uint32_t m0v, uint32_t voff, const ttd_i32x4_t& srd, int soff) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(m0v), "v"(voff), "s"(srd), "s"(soff)
-      : "memory");
+// LDS-DMA piece with M0 already holding its LDS base; sets M0 for the next piece right after
+// issuing (MFMAs separate it from the next piece: no s_nop for the M0 hazard). Nothing else
+// writes M0 in this kernel (ds_* need no M0 on gfx950; every LDS-DMA is this asm).
+__device__ __forceinline__ void dma_chain(uint32_t voff, const ttd_i32x4_t& srd, int soff, uint32_t next_m0) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_mov_b32 m0, %3"
+               :
+               : "v"(voff), "s"(srd), "s"(soff), "s"(next_m0)
+               : "memory");
+}
+__device__ __forceinline__ void m0_init(uint32_t v) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(v) : "memory");
 }
 
 template <int N, class F, int I = 0>
@@ -209,18 +212,26 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
     if constexpr (h == 0) fl[set][slot] = v;
     else fh[set][slot] = v;
   };
-  auto dma1 = [&](auto Q, int st, int kt) {  // piece q (0..7 A, 8..15 B) of K-tile kt into stage st
+  // LDS base of piece q (0..7 A, 8..15 B) in stage st; pieces go out in the order (stage st:
+  // 0..15), (stage st ^ 1: 0..15), ..., each setting M0 for its successor
+  auto m0_of = [&](int q, int st) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<int>(ldsw + (q < 8 ? 0 : SB) + st * OPB + (q & 7) * 4096)));
+  };
+  auto dma1 = [&](auto Q, int st, int kt) {  // piece q of K-tile kt into stage st (M0 = its base)
     constexpr int qq = decltype(Q)::value, i = qq & 7;
     const LoadMN& L = qq < 8 ? la : lb;
-    dma_piece(ldsw + (qq < 8 ? 0 : SB) + st * OPB + i * 4096, L.voff[i & 1], L.srd,
-              (kt0 + kt) * (qq < 8 ? kstride_a : kstride_b) + i * L.row8);
+    dma_chain(L.voff[i & 1], L.srd, (kt0 + kt) * (qq < 8 ? kstride_a : kstride_b) + i * L.row8,
+              qq < 15 ? m0_of(qq + 1, st) : m0_of(0, st ^ 1));
   };
   auto fa = [&](int set, int a) { return cat(fl[set][a], fh[set][a]); };
   auto fb = [&](int set, int b) { return cat(fl[set][8 + b], fh[set][8 + b]); };
 
-  auto ktile = [&](int kt, auto first) {
+  // HAS2 (K-tile kt + 2 exists) is compile-time: no branch around the 16 DMA pieces in the
+  // steady-state loop
+  auto ktile = [&](int kt, auto first, auto has2c) {
     constexpr bool FIRST = decltype(first)::value;
-    const bool has2 = kt + 2 < nk;
+    constexpr bool has2 = decltype(has2c)::value;
     const int st = kt & 1;
     const bool rs_on = RS && ((kt0 + kt) % tiles_n == tn);
     // phase 0: K-step 0 (set 0) | reads of K-step 1 into set 1
@@ -250,7 +261,7 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
     static_for<32>([&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i % 4 == 0)
-        if (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
+        if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
       mfma_acc<false>(acc[i / 8][i % 8], fa(1, i / 8), fb(1, i % 8));
     });
     if constexpr (RS) {
@@ -268,27 +279,35 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
         }
       }
     }
-    if (has2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (has2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
     // phase 1b: second half of K-step 1 | B pieces of kt + 2 | reads of K-tile kt + 1, K-step 0
     static_for<32>([&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i % 4 == 1)
-        if (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
+        if constexpr (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
       rd1(std::integral_constant<int, i>{}, std::integral_constant<int, 0>{}, st ^ 1, std::integral_constant<int, 0>{});
       mfma_acc<false>(acc[4 + i / 8][i % 8], fa(1, 4 + i / 8), fb(1, i % 8));
     });
   };
 
   // prologue: K-tiles 0 and 1 into stages 0 and 1, K-step 0 fragments of K-tile 0
+  m0_init(m0_of(0, 0));
   static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
   static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   static_for<32>([&](auto R) { rd1(R, std::integral_constant<int, 0>{}, 0, std::integral_constant<int, 0>{}); });
-  ktile(0, std::true_type{});
-  for (int kt = 1; kt < nk; ++kt) ktile(kt, std::false_type{});
+  if (nk >= 3) {
+    ktile(0, std::true_type{}, std::true_type{});
+    for (int kt = 1; kt < nk - 2; ++kt) ktile(kt, std::false_type{}, std::true_type{});
+    ktile(nk - 2, std::false_type{}, std::false_type{});
+    ktile(nk - 1, std::false_type{}, std::false_type{});
+  } else {
+    ktile(0, std::true_type{}, std::false_type{});
+    if (nk == 2) ktile(1, std::false_type{}, std::false_type{});
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 #pragma unroll
   for (int a = 0; a < 8; ++a)

@@ -402,24 +402,6 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
   static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
-  if constexpr (SCHED >= 6) {
-    // DIAGNOSTIC schedules (wrong results; timing only, tools/g4_bench.py): 9 = the 128 MFMAs
-    // per K-tile alone, 8 = MFMAs + the 32 fragment reads, 7 = MFMAs + the 16 DMA pieces,
-    // 6 = MFMAs + reads + DMA without any barrier (waits lag one K-tile / one half)
-    for (int kt = 0; kt < ktiles; ++kt) {
-      const int st = kt & 1;
-      static_for<128>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        if constexpr ((SCHED == 8 || SCHED == 6) && i % 4 == 0)
-          rd1(std::integral_constant<int, (i / 4) % 16>{}, va[st][i / 64], vb[st][i / 64], fa[1 - i / 64], fb[1 - i / 64]);
-        if constexpr ((SCHED == 7 || SCHED == 6) && i % 8 == 2) dma1(std::integral_constant<int, i / 8>{}, st, kt);
-        if constexpr ((SCHED == 8 || SCHED == 6) && i == 63) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-        mfma1((i / 8) % 8, i % 8, fa[i / 64][(i / 8) % 8], fb[i / 64][i % 8], F{});
-      });
-      if constexpr (SCHED == 8 || SCHED == 6) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-      if constexpr (SCHED == 7 || SCHED == 6) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    }
-  } else {
   auto ktile = [&](int kt, auto first) {
     const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
     const int st = kt & 1;
@@ -428,7 +410,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
       constexpr int i = decltype(I)::value, a = i / 8, b = i % 8;
       if constexpr (i % 4 == 0) rd1(std::integral_constant<int, i / 4>{}, va[st][1], vb[st][1], fa[1], fb[1]);
       if constexpr (i == 0 || need0(i) > need0(i - 1 < 0 ? 0 : i - 1))
-        if constexpr (SCHED != 5) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(lgk0(i)) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(lgk0(i)) : "memory");
       mfma1(a, b, fa[0][a], fb[0][b], first);
     });
     if constexpr (SCHED == 3) {
@@ -444,14 +426,11 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
         mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
       });
     } else {
-      if constexpr (SCHED == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      else if constexpr (SCHED == 5) asm volatile("s_barrier" ::: "memory");
-      else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       // phase 1a: K-tile kt + 2 into this stage (the MFMA sequence is never duplicated per
       // branch: with the MFMAs inside if / else copies hipcc allocated the accumulators
       // differently per copy and shuffled them with unpadded v_accvgpr_mov between).
       // SCHED 1: all 16 pieces in the first 32 MFMAs; SCHED 2: 8 here, 8 in phase 1b.
-      // (diagnostics: 4 = SCHED 2 without barriers, 5 = SCHED 2 without LDS-read waits)
       constexpr int DSTEP = SCHED == 1 ? 2 : 4;
       static_for<32>([&](auto I) {
         constexpr int i = decltype(I)::value;
@@ -465,7 +444,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if constexpr (SCHED != 4) asm volatile("s_barrier" ::: "memory");
+      asm volatile("s_barrier" ::: "memory");
       // phase 1b: K-step-0 fragments of K-tile kt + 1 (read unconditionally: past the last
       // K-tile they are never used)
       static_for<32>([&](auto I) {
@@ -478,7 +457,6 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
     }
   };
   for (int kt = 0; kt < ktiles; ++kt) ktile(kt, F{});
-  }
   }
   // the last MFMAs' results -> the epilogue's v_accvgpr_read: XDL write -> read wait states
   // (hipcc pads nothing after asm); the empty "+a" statements order every read after the pad
@@ -493,10 +471,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   else epilogue<EK, true>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
 }
 
-// DIAGNOSTIC (timing only, wrong results): the 4-wave tile on v_mfma_f32_32x32x16_bf16 (4 x 4
-// tiles of 32 x 32 per wave, 16 accumulator AGPRs each; per K-tile 64 MFMAs of 32 cycles, 32
-// fragment reads, 16 DMA pieces). MODE 9: MFMAs only; 8: + reads (one per 2 MFMAs); 7: + DMA
-// (one per 4 MFMAs); 6: both. Measures whether the wider MFMA gaps hide the reads / DMA.
+// 32x32x16 MFMA with an AGPR accumulator, and the VGPR-staged loader pieces of gemm4v
 __device__ __forceinline__ void mfma32(f32x16_t& c, const bf16x8_t& x, const bf16x8_t& y) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(y), "v"(x));
 }
@@ -508,118 +483,6 @@ __device__ __forceinline__ void buf_ld16(ttd_i32x4_t& d, uint32_t voff, const tt
   asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(srd), "s"(soff));
 }
 
-template <int MODE>
-__global__ __launch_bounds__(T, 1) void g4diag32_kernel(const bf16_t* __restrict__ A, long long lda,
-                                                       const bf16_t* __restrict__ B, long long ldb, bf16_t* out,
-                                                       int M, int N, int K, int tiles_m, int tiles_n, int group) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int nblk = tiles_m * tiles_n;
-  const int t = xcd_remap(blockIdx.x, nblk);
-  int tm_, tn_;
-  tile_of(t, tiles_m, tiles_n, group, tm_, tn_);
-  const int m0 = tm_ * BM, n0 = tn_ * BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int ktiles = K / 64;
-  LoadK la, lb;
-  la.init(A, lda, M, m0, tid);
-  lb.init(B, ldb, N, n0, tid);
-  const int r32 = lane & 31, h = lane >> 5;
-  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
-  uint32_t vk[4];  // per K-step s: lane offset of chunk 2s + h in row r32 (block offsets immediate)
-#pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4) vk[s4] = sb + r32 * 128 + ((((2 * s4 + h) ^ ((r32 >> 1) & 7))) << 4);
-  const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
-  f32x16_t acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      acc[a][b] = f32x16_t{};
-      asm volatile("" : "+a"(acc[a][b]));
-    }
-  bf16x8_t fa[2][4], fb[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      fa[j][a] = bf16x8_t{};
-      fb[j][a] = bf16x8_t{};
-    }
-  auto dma1 = [&](auto Q, int st, int kt) {
-    constexpr int q = decltype(Q)::value;
-    const LoadK& L = q < 8 ? la : lb;
-    const uint32_t m0v = ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096;
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(m0v), "v"(L.voff[q & 7]), "s"(L.srd), "s"(kt * 128)
-        : "memory");
-  };
-  ttd_i32x4_t stg[4] = {};
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const int st = kt & 1;
-    if constexpr (MODE == 17) asm volatile("s_waitcnt vmcnt(0)" ::"v"(stg[0]), "v"(stg[1]), "v"(stg[2]), "v"(stg[3]) : "memory");
-    if constexpr (MODE >= 10) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    static_for<64>([&](auto I) {
-      constexpr int i = decltype(I)::value, s4 = i / 16, a = (i / 4) % 4, b = i % 4;
-      // reads per burst: 1 (modes 8, 6, 10: one every 2 MFMAs), 2 (11), 4 (12), 8 (13)
-      constexpr int BURST = MODE == 11 ? 2 : (MODE == 12 ? 4 : (MODE >= 13 ? 8 : 1));
-      constexpr bool RD = (MODE == 6 || MODE == 8 || MODE >= 10) && (i % (2 * BURST)) < BURST;
-      if constexpr (RD) {
-        constexpr int r = ((i / (2 * BURST)) * BURST + (i % (2 * BURST))) % 8;  // A blocks 0..3, B 0..3
-        constexpr int nxt = (s4 + 1) & 3;
-        const uint32_t base = vk[nxt] + st * STAGE + (r < 4 ? wm * 16384 : OPB + wn * 16384);
-        if constexpr (r < 4)
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[(s4 + 1) & 1][r]) : "v"(base), "i"(r * 4096));
-        else
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[(s4 + 1) & 1][r - 4]) : "v"(base), "i"((r - 4) * 4096));
-      }
-      if constexpr ((MODE == 7 || MODE == 6 || MODE == 15) && i % 4 == 1) dma1(std::integral_constant<int, i / 4>{}, st, kt);
-      // 16: + 4 ds_write_b128 per K-step (burst, register data): LDS write contention alone
-      if constexpr (MODE == 16 && i % 16 == 7) {
-        static_for<4>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          const uint32_t wa = sb + st * STAGE + ((i / 16) * 4 + j) * 4096 + tid * 16;
-          ds_w128(wa, stg[j]);
-        });
-      }
-      // 17: + 4 buffer_load_dwordx4 into registers per K-step (burst): the VMEM issue alone
-      if constexpr (MODE == 17 && i % 16 == 7) {
-        static_for<4>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          constexpr int q = (i / 16) * 4 + j;
-          const LoadK& L = q < 8 ? la : lb;
-          buf_ld16(stg[j], L.voff[q & 7], L.srd, kt * 128);
-        });
-      }
-      // 14: 4 DMA pieces in a burst right after each K-step's read burst
-      if constexpr (MODE == 14 && i % 16 == 7) {
-        dma1(std::integral_constant<int, (i / 16) * 4 + 0>{}, st, kt);
-        dma1(std::integral_constant<int, (i / 16) * 4 + 1>{}, st, kt);
-        dma1(std::integral_constant<int, (i / 16) * 4 + 2>{}, st, kt);
-        dma1(std::integral_constant<int, (i / 16) * 4 + 3>{}, st, kt);
-      }
-      if constexpr ((MODE == 8 || MODE == 6) && i % 16 == 15) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-      mfma32(acc[a][b], fa[s4 & 1][a], fb[s4 & 1][b]);
-    });
-    if constexpr (MODE == 7 || MODE == 6 || MODE == 14 || MODE == 15) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  float sum = 0.f;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      asm volatile("" : "+a"(acc[a][b]));
-#pragma unroll
-      for (int j = 0; j < 16; ++j) sum += acc[a][b][j];
-    }
-  if (sum == 12345.f) out[0] = 1;  // keep the accumulators live
-}
 
 // ============================================================================================
 // gemm4p: the production form — persistent 4-wave 256 x 256 kernel on the SCHED 2 main loop
@@ -642,6 +505,20 @@ __device__ __forceinline__ void dma_piece(uint32_t m0v, uint32_t voff, const ttd
       : "=&s"(keep)
       : "s"(m0v), "v"(voff), "s"(srd), "s"(soff)
       : "memory");
+}
+// LDS-DMA piece with M0 already holding its LDS base; sets M0 for the NEXT piece right after
+// issuing (the next piece is MFMAs away, so the SALU-write -> LDS-DMA-read hazard needs no
+// s_nop): 2 issue slots per piece instead of a save / set / nop / restore sequence. Only valid
+// where nothing else writes M0 (the compiler does not use it in these kernels: ds_* need no M0
+// on gfx950 and every LDS-DMA here is this asm).
+__device__ __forceinline__ void dma_chain(uint32_t voff, const ttd_i32x4_t& srd, int soff, uint32_t next_m0) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_mov_b32 m0, %3"
+               :
+               : "v"(voff), "s"(srd), "s"(soff), "s"(next_m0)
+               : "memory");
+}
+__device__ __forceinline__ void m0_init(uint32_t v) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(v) : "memory");
 }
 template <int OFF>
 __device__ __forceinline__ void ds_rd(bf16x8_t& d, uint32_t base) {
@@ -703,10 +580,14 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
     if constexpr (rd_is_a(r)) ds_rd<rd_blk(r) * 2048>(xa[rd_blk(r)], a_base);
     else ds_rd<rd_blk(r) * 2048>(xb[rd_blk(r)], b_base);
   };
-  auto dma1 = [&](auto Q, int st, int kt) {  // piece q (0..7 A, 8..15 B) of K-tile kt into stage st
+  // LDS base of piece q (0..7 A, 8..15 B) in stage st; pieces are issued in the order
+  // (stage st: 0..15), (stage st ^ 1: 0..15), ... so each sets M0 for its successor
+  auto m0_of = [&](int q, int st) { return ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096; };
+  auto dma1 = [&](auto Q, int st, int kt) {  // piece q of K-tile kt into stage st (M0 = its base)
     constexpr int q = decltype(Q)::value;
     const LoadK& L = q < 8 ? la : lb;
-    dma_piece(ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096, L.voff[q & 7], L.srd, kt * 128);
+    const uint32_t nxt = q < 15 ? m0_of(q + 1, st) : m0_of(0, st ^ 1);
+    dma_chain(L.voff[q & 7], L.srd, kt * 128, static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(nxt))));
   };
   auto mfma1 = [&](int a, int b, const bf16x8_t& x, const bf16x8_t& y, auto first) {
     mfma_acc<decltype(first)::value>(acc[a][b], x, y);
@@ -720,12 +601,15 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
   auto prologue = [&](int m0, int n0) {  // K-tiles 0 and 1 of tile (m0, n0) into stages 0 and 1
     la.init(A, lda, M, m0, tid);
     lb.init(B, ldb, N, n0, tid);
+    m0_init(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m0_of(0, 0)))));
     static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
     if (ktiles > 1) static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
   };
-  // one K-tile of the SCHED 2 schedule (see gemm4w_kernel); FIRST: phase 0 with C = 0
-  auto ktile = [&](int kt, auto first) {
-    const bool has2 = kt + 2 < ktiles;
+  // one K-tile of the SCHED 2 schedule (see gemm4w_kernel); FIRST: phase 0 with C = 0; HAS2:
+  // K-tile kt + 2 exists (compile-time: the steady-state loop body has no branch around its 16
+  // DMA pieces — as run-time tests they were 16 scalar branches per K-tile)
+  auto ktile = [&](int kt, auto first, auto has2c) {
+    constexpr bool has2 = decltype(has2c)::value;
     const int st = kt & 1;
     static_for<64>([&](auto I) {
       constexpr int i = decltype(I)::value, a = i / 8, b = i % 8;
@@ -738,16 +622,16 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
     static_for<32>([&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i % 4 == 0)
-        if (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
+        if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
       mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], std::false_type{});
     });
-    if (has2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (has2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
     static_for<32>([&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i % 4 == 1)
-        if (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
+        if constexpr (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
       if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
       mfma1(4 + i / 8, i % 8, fa[1][4 + i / 8], fb[1][i % 8], std::false_type{});
     });
@@ -794,8 +678,15 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
       st_land += tB - tA;
     }
     static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
-    ktile(0, std::true_type{});
-    for (int kt = 1; kt < ktiles; ++kt) ktile(kt, std::false_type{});
+    if (ktiles >= 3) {
+      ktile(0, std::true_type{}, std::true_type{});
+      for (int kt = 1; kt < ktiles - 2; ++kt) ktile(kt, std::false_type{}, std::true_type{});
+      ktile(ktiles - 2, std::false_type{}, std::false_type{});
+      ktile(ktiles - 1, std::false_type{}, std::false_type{});
+    } else {
+      ktile(0, std::true_type{}, std::false_type{});
+      if (ktiles == 2) ktile(1, std::false_type{}, std::false_type{});
+    }
     if (tq && tid == 0) *reinterpret_cast<int*>(smem + SMEM) = claim;
     // every wave past its last LDS read before the stages are refilled
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1088,7 +979,7 @@ __global__ __launch_bounds__(T, 1) void gemm4v_kernel(const bf16_t* __restrict__
 
 // TTD_G4_SCHED: main-loop form. 30 (default) = persistent SCHED-2 kernel (gemm4p); 0-3 the
 // one-tile-per-workgroup forms (0 compiler-scheduled, 1-3 hand-ordered asm), 20 the VGPR-staged
-// 32x32x16 form, 31 = 30 with phase stamps, 4-9 / d32 diagnostics (wrong results, timing only)
+// 32x32x16 form, 31 = 30 with phase stamps
 static int& g4_sched() {
   static int v = ttdk::getenv_int("TTD_G4_SCHED", 30);
   return v;
@@ -1168,18 +1059,6 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
       case 3: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 3>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 4: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 4>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                   \
-      case 5: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 5>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                   \
-      case 6: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 6>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 7: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 7>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 8: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 8>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 9: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 9>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
       case 31: {                                                                                          \
         const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
         if (grid < 8) return hipErrorInvalidValue;                                                          \
@@ -1215,29 +1094,6 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
   }
 #undef TTDK_G4
   return hipErrorInvalidValue;
-}
-
-// diagnostic entry (tools/g4_bench.py arms d32:MODE): the 32x32x16 MFMA form of the main loop
-TTDK_EXPORT int ttdk_g4diag32(int mode, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* out,
-                              int M, int N, int K, hipStream_t st) {
-  using namespace ttdk;
-  const int tm = ceil_div(M, g4::BM), tn = ceil_div(N, g4::BN);
-  const int group = g4_group();
-  switch (mode) {
-    case 6: hipLaunchKernelGGL((g4::g4diag32_kernel<6>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 7: hipLaunchKernelGGL((g4::g4diag32_kernel<7>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 10: hipLaunchKernelGGL((g4::g4diag32_kernel<10>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 11: hipLaunchKernelGGL((g4::g4diag32_kernel<11>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 12: hipLaunchKernelGGL((g4::g4diag32_kernel<12>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 13: hipLaunchKernelGGL((g4::g4diag32_kernel<13>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 14: hipLaunchKernelGGL((g4::g4diag32_kernel<14>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 15: hipLaunchKernelGGL((g4::g4diag32_kernel<15>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 16: hipLaunchKernelGGL((g4::g4diag32_kernel<16>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 17: hipLaunchKernelGGL((g4::g4diag32_kernel<17>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    case 8: hipLaunchKernelGGL((g4::g4diag32_kernel<8>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-    default: hipLaunchKernelGGL((g4::g4diag32_kernel<9>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, out, M, N, K, tm, tn, group); break;
-  }
-  return hipGetLastError();
 }
 
 // diagnostic: copy the per-wave phase stamps of the last TTD_G4_SCHED=31 launch (2048 x 4 x 4 u64)

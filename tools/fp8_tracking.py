@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Loss tracking of the fp8 ResNet-50 path against bf16 (BASELINE config 5 quality check).
 
-Trains ResNet-50 v1.5 at the bench's shape (b1024, 224^2, synthetic batch, LAMB large-batch
-recipe as bench.py --optimizer lamb) for --steps steps in bf16 and in --precision fp8 from the
-same initial weights and data, and reports both loss curves and the relative gap of the mean
-loss over the second half of the run (the acceptance line: within 15 %; windowed means reported).
+Trains ResNet-50 v1.5 at the bench's shape (b1024, 224^2, LAMB large-batch recipe as bench.py
+--optimizer lamb) for --steps steps in bf16 and in --precision fp8 from the same initial weights,
+cycling over --batches distinct synthetic batches (default 8: the model has to fit 8192 images,
+not memorise one batch), and reports both loss curves and the relative gap of the mean loss over
+the second half of the run (the acceptance line: within 10 %; windowed means reported).
 
     python tools/fp8_tracking.py --steps 200 --out gpurun_out/fp8_tracking.json
 """
@@ -19,7 +20,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(precision, steps, B, S, log_every):
+def run(precision, steps, B, S, log_every, nbatches=8):
     from tensorflow_train_distributed_amd.models.resnet import resnet50
     from tensorflow_train_distributed_amd.train.flat import FlatLAMB, Schedule
     dev = torch.device("cuda", 0)
@@ -28,11 +29,14 @@ def run(precision, steps, B, S, log_every):
                                           power=2.0, total_steps=10000), weight_decay=5e-5)
     g = torch.Generator(device=dev)
     g.manual_seed(0)
-    images = torch.randn((B, S, S, 3), generator=g, device=dev).to(torch.bfloat16)
-    labels = torch.randint(0, 1000, (B,), generator=g, device=dev, dtype=torch.int32)
+    data = []
+    for _ in range(nbatches):
+        data.append((torch.randn((B, S, S, 3), generator=g, device=dev).to(torch.bfloat16),
+                     torch.randint(0, 1000, (B,), generator=g, device=dev, dtype=torch.int32)))
     losses = []
     t0 = time.time()
     for i in range(steps):
+        images, labels = data[i % nbatches]
         sums = model.forward_backward(images, labels, grad_scale=1.0 / B)
         opt.step()
         losses.append(sums[0:1].clone())
@@ -47,20 +51,22 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--out", default="gpurun_out/fp8_tracking.json")
     a = ap.parse_args()
     torch.cuda.set_device(0)
-    res = {"steps": a.steps, "batch": a.batch, "optimizer": "LAMB (bench.py --optimizer lamb)"}
+    res = {"steps": a.steps, "batch": a.batch, "distinct_batches": a.batches,
+           "optimizer": "LAMB (bench.py --optimizer lamb)"}
     for p in ("bf16", "fp8"):
-        res[p] = run(p, a.steps, a.batch, a.image_size, log_every=25)
+        res[p] = run(p, a.steps, a.batch, a.image_size, log_every=25, nbatches=a.batches)
         torch.cuda.empty_cache()
     k = min(10, a.steps)
     mb = sum(res["bf16"][-k:]) / k
     m8 = sum(res["fp8"][-k:]) / k
     res["mean_last10"] = {"bf16": round(mb, 5), "fp8": round(m8, 5)}
-    # once the batch is memorised the per-step loss oscillates between ~0.02 and ~0.1 (LAMB on one
-    # synthetic batch), so a 10-step mean is noise-dominated: the acceptance line compares the
-    # mean over the second half of the run (within 15 %) and the windowed means are reported
+    # per-step losses differ batch to batch, so a 10-step mean is noise-dominated: the acceptance
+    # line compares the mean over the second half of the run (within 10 %) and the windowed means
+    # are reported
     h = a.steps // 2
     hb = sum(res["bf16"][h:]) / (a.steps - h)
     h8 = sum(res["fp8"][h:]) / (a.steps - h)
@@ -69,11 +75,11 @@ def main():
                                           "fp8": round(sum(res["fp8"][w0:w1]) / (w1 - w0), 5)}
                       for w0, w1 in ((0, a.steps // 4), (a.steps // 4, h), (h, a.steps)) if w1 > w0}
     res["rel_gap"] = round((h8 - hb) / hb, 4)
-    res["within_15pct"] = abs(h8 - hb) <= 0.15 * abs(hb)
+    res["within_10pct"] = abs(h8 - hb) <= 0.10 * abs(hb)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f)
-    print(json.dumps({k2: res[k2] for k2 in ("mean_last10", "mean_second_half", "windows", "rel_gap", "within_15pct")}),
+    print(json.dumps({k2: res[k2] for k2 in ("mean_last10", "mean_second_half", "windows", "rel_gap", "within_10pct")}),
           flush=True)
 
 

@@ -62,12 +62,6 @@ def main():
             else (lambda: torch.mm(a, b.t(), out=out)),
         }
         for k in ARMS:
-            if k.startswith("d32:"):  # diagnostic 32x32x16 main loop (timing only)
-                from tensorflow_train_distributed_amd.ops import _lib
-                _lib.register({"ttdk_g4diag32": [_lib.I, _lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.I, _lib.I,
-                                                 _lib.I, _lib.P]})
-                arms[k] = (lambda v: lambda: _lib.call("ttdk_g4diag32", v, a.data_ptr(), K, b.data_ptr(), K,
-                                                       out.data_ptr(), M, N, K, _lib.stream()))(int(k[4:]))
             if k.startswith("g4:"):  # g4:SCHED[/GROUP[/STAGGER]]
                 sv, _, rest = k[3:].partition("/")
                 gv, _, stv = rest.partition("/")
