@@ -97,6 +97,20 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// LDS-DMA piece with M0 already holding its LDS base; sets M0 for the NEXT piece right after
+// issuing (the next piece is MFMAs away, so the SALU-write -> LDS-DMA-read hazard needs no
+// s_nop): 2 issue slots per piece instead of a save / set / nop / restore sequence. Only valid
+// where nothing else writes M0 (the compiler does not use it in these kernels: ds_* need no M0
+// on gfx950 and every LDS-DMA here is this asm).
+__device__ __forceinline__ void dma_chain(uint32_t voff, const ttd_i32x4_t& srd, int soff, uint32_t next_m0) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_mov_b32 m0, %3"
+               :
+               : "v"(voff), "s"(srd), "s"(soff), "s"(next_m0)
+               : "memory");
+}
+__device__ __forceinline__ void m0_init(uint32_t v) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(v) : "memory");
+}
 using big::kEkBias;
 using big::kEkDGelu;
 using big::kEkBeta;
@@ -377,23 +391,23 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
     else
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(xb[rd_blk(r)]) : "v"(b_base), "i"(rd_blk(r) * 2048));
   };
-  // DMA piece q (0..7 A, 8..15 B) of K-tile kt into stage st
+  // DMA piece q (0..7 A, 8..15 B) of K-tile kt into stage st, M0 = its LDS base (chained: every
+  // piece sets M0 for its successor; the issue order is stage st 0..15, stage st ^ 1 0..15, ...
+  // — SCHED 1 / 3 issue A and B of a K-tile in the same 0..15 order)
+  auto m0_of = [&](int q, int st) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<int>(ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096)));
+  };
   auto dma1 = [&](auto Q, int st, int kt) {
     constexpr int q = decltype(Q)::value;
     const LoadK& L = q < 8 ? la : lb;
-    const uint32_t m0v = ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096;
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(m0v), "v"(L.voff[q & 7]), "s"(L.srd), "s"(kt * 128)
-        : "memory");
+    dma_chain(L.voff[q & 7], L.srd, kt * 128, q < 15 ? m0_of(q + 1, st) : m0_of(0, st ^ 1));
   };
   auto mfma1 = [&](int a, int b, const bf16x8_t& x, const bf16x8_t& y, auto first) {
     mfma_acc<decltype(first)::value>(acc[a][b], x, y);
   };
   // prologue: K-tiles 0 and 1, wait for 0, K-step-0 fragments of K-tile 0
+  m0_init(m0_of(0, 0));
   static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
   if (ktiles > 1) {
     static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
@@ -402,8 +416,10 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
   static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
-  auto ktile = [&](int kt, auto first) {
-    const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
+  // HAS2 (K-tile kt + 2 exists) compile-time: no branch around the DMA pieces in the steady loop
+  auto ktile = [&](int kt, auto first, auto has2c) {
+    constexpr bool has2 = decltype(has2c)::value;
+    const bool has1 = kt + 1 < ktiles;
     const int st = kt & 1;
     // phase 0
     static_for<64>([&](auto I) {
@@ -420,7 +436,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
       static_for<64>([&](auto I) {
         constexpr int i = decltype(I)::value;
         if constexpr (i % 4 == 0)
-          if (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
+          if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
         if constexpr (i % 4 == 2)
           rd1(std::integral_constant<int, i / 4>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
         mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
@@ -435,10 +451,10 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
       static_for<32>([&](auto I) {
         constexpr int i = decltype(I)::value;
         if constexpr (i % DSTEP == 0)
-          if (has2) dma1(std::integral_constant<int, i / DSTEP>{}, st, kt + 2);
+          if constexpr (has2) dma1(std::integral_constant<int, i / DSTEP>{}, st, kt + 2);
         mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
       });
-      if (has2) {
+      if constexpr (has2) {
         if constexpr (SCHED == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
@@ -450,13 +466,14 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
       static_for<32>([&](auto I) {
         constexpr int i = decltype(I)::value;
         if constexpr (SCHED != 1 && i % 4 == 1)
-          if (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
+          if constexpr (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
         if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
         mfma1(4 + i / 8, i % 8, fa[1][4 + i / 8], fb[1][i % 8], F{});
       });
     }
   };
-  for (int kt = 0; kt < ktiles; ++kt) ktile(kt, F{});
+  for (int kt = 0; kt < ktiles - 2; ++kt) ktile(kt, F{}, Tr{});
+  for (int kt = ktiles - 2 < 0 ? 0 : ktiles - 2; kt < ktiles; ++kt) ktile(kt, F{}, F{});
   }
   // the last MFMAs' results -> the epilogue's v_accvgpr_read: XDL write -> read wait states
   // (hipcc pads nothing after asm); the empty "+a" statements order every read after the pad
@@ -505,20 +522,6 @@ __device__ __forceinline__ void dma_piece(uint32_t m0v, uint32_t voff, const ttd
       : "=&s"(keep)
       : "s"(m0v), "v"(voff), "s"(srd), "s"(soff)
       : "memory");
-}
-// LDS-DMA piece with M0 already holding its LDS base; sets M0 for the NEXT piece right after
-// issuing (the next piece is MFMAs away, so the SALU-write -> LDS-DMA-read hazard needs no
-// s_nop): 2 issue slots per piece instead of a save / set / nop / restore sequence. Only valid
-// where nothing else writes M0 (the compiler does not use it in these kernels: ds_* need no M0
-// on gfx950 and every LDS-DMA here is this asm).
-__device__ __forceinline__ void dma_chain(uint32_t voff, const ttd_i32x4_t& srd, int soff, uint32_t next_m0) {
-  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_mov_b32 m0, %3"
-               :
-               : "v"(voff), "s"(srd), "s"(soff), "s"(next_m0)
-               : "memory");
-}
-__device__ __forceinline__ void m0_init(uint32_t v) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(v) : "memory");
 }
 template <int OFF>
 __device__ __forceinline__ void ds_rd(bf16x8_t& d, uint32_t base) {
@@ -977,11 +980,13 @@ __global__ __launch_bounds__(T, 1) void gemm4v_kernel(const bf16_t* __restrict__
 }  // namespace
 }  // namespace ttdk
 
-// TTD_G4_SCHED: main-loop form. 30 (default) = persistent SCHED-2 kernel (gemm4p); 0-3 the
-// one-tile-per-workgroup forms (0 compiler-scheduled, 1-3 hand-ordered asm), 20 the VGPR-staged
-// 32x32x16 form, 31 = 30 with phase stamps
+// TTD_G4_SCHED: main-loop form. 2 (default) = one tile per workgroup, hand-ordered SCHED 2;
+// 30 = the persistent SCHED-2 kernel (gemm4p, next tile's DMA under this tile's epilogue);
+// 0 / 1 / 3 other one-tile forms (0 compiler-scheduled), 20 the VGPR-staged 32x32x16 form,
+// 31 = 30 with phase stamps. With the branch-free steady loop (same box, tools/g4_bench.py):
+// 8192^3 1515 (2) vs 1301 (30) TF/s, hipBLASLt 1650; BERT-Large step 154.8 / 156.2 vs 158.7 ms
 static int& g4_sched() {
-  static int v = ttdk::getenv_int("TTD_G4_SCHED", 30);
+  static int v = ttdk::getenv_int("TTD_G4_SCHED", 2);
   return v;
 }
 static int g4_cus() { return ttdk::big::device_cus(); }

@@ -170,8 +170,9 @@ def set_g4_group(v: int) -> int:
 
 
 def set_g4_sched(v: int) -> int:
-    """Main-loop schedule of the 4-wave GEMM: 1 = hand-ordered inline asm (default), 0 = the
-    compiler-scheduled form (A/B and tests). Returns the previous setting."""
+    """Main-loop schedule of the 4-wave GEMM (gemm4w.hip g4_sched): 2 = hand-ordered inline asm,
+    one tile per workgroup (default), 30 = persistent, 0 = compiler-scheduled (A/B and tests).
+    Returns the previous setting."""
     return int(_lib.query("ttdk_set_g4_sched", int(v)))
 
 

@@ -3,7 +3,8 @@
 Pins the kernel that carries BERT's dense layers (tf.layers.dense MatMul,
 /root/reference/distribute_training.py:54,61): the plain store, the bias, bias + GELU + pre-activation
 (aux) copy, dGELU and accumulate (beta) epilogues, at BERT-Large shapes and at edge shapes
-(M and N not multiples of 256, rows past M / N read as zeros by the buffer loads)."""
+(M and N not multiples of 256, rows past M / N read as zeros by the buffer loads) and at ResNet-50
+1x1-conv GEMM shapes."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -16,10 +17,12 @@ def _rel(a, b):
 
 
 SHAPES = [(256, 256, 128), (512, 512, 128), (1000, 264, 384), (300, 1000, 1024), (4096, 4096, 1024),
-          (2048, 1024, 4096), (65, 8, 128)]
+          (2048, 1024, 4096), (65, 8, 128),
+          # ResNet-50 b256 1x1 convs as GEMMs (pixels x Cout x Cin): stage-4 c3, stage-5 c1
+          (12544, 1024, 256), (3136, 512, 2048)]
 
 
-@pytest.fixture(params=[30, 20, 1, 2, 3, 0], ids=["persistent", "vstage32", "asm_sched1", "asm_sched2", "asm_sched3", "compiler_sched"])
+@pytest.fixture(params=[2, 30, 20, 1, 3, 0], ids=["asm_sched2", "persistent", "vstage32", "asm_sched1", "asm_sched3", "compiler_sched"])
 def sched(request):
     from tensorflow_train_distributed_amd.ops import gemm as G
     old = G.set_g4_sched(request.param)
