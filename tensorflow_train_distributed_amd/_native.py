@@ -103,6 +103,12 @@ def hip_sources():
     return sorted(glob.glob(os.path.join(_CSRC, "kernels", "*.hip")))
 
 
+# Per-file extra flags. attention.hip: no SLP vectorisation — -O3 packs adjacent f32 multiplies /
+# FMAs of the softmax into v_pk_*_f32, which beside MFMAs cost more issue cycles than the scalar
+# pair (cdna_hip_programming.md, attention prefill pitfalls).
+_FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+
+
 def build_hip(force: bool = False) -> str:
     """Cross-compile every HIP kernel for gfx950 into libttd_hip.so (no GPU needed)."""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
@@ -113,7 +119,8 @@ def build_hip(force: bool = False) -> str:
     if force:
         shutil.rmtree(_OBJDIR, ignore_errors=True)
     objs, changed = _build_objects(
-        srcs, hdrs, lambda s, o: [hipcc, *flags, "-c", s, "-o", o], ".hip.o")
+        srcs, hdrs, lambda s, o: [hipcc, *flags, *_FILE_FLAGS.get(os.path.basename(s), []), "-c", s, "-o", o],
+        ".hip.o")
     if changed or not os.path.exists(HIP_LIB) or os.path.getmtime(HIP_LIB) < _newest_mtime(objs):
         # librccl.so.1: the native collective engine (collective.hip). At run time the soname
         # resolves to the RCCL torch already loaded, so the process holds one RCCL.
@@ -135,6 +142,8 @@ def _src_hash(kind):
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update(HIP_ARCH.encode())
+    if kind == "hip":
+        h.update(repr(sorted(_FILE_FLAGS.items())).encode())
     return h.hexdigest()
 
 

@@ -203,23 +203,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       m[qb] = mnew;
       float rs = 0.f;
       const int qrow = q0 + qb * 16 + i16;
-      // hash input of key pair (kbase + kb*16 + 4g)/2 + j: a per-tile base plus constants
-      const uint32_t hbase = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) +
-                                        (static_cast<uint32_t>(kbase >> 1) + 2u * g) * kAttnPairMul
-                                  : 0u;
+      // keys kbase + kb*16 + 4g + i: pair kbase/2 + (kb >> 1)*16 + 4g + i, half kb & 1 — the
+      // hash input is a per-tile base plus constants
+      uint32_t hp[2][4] = {};
+      if constexpr (DROP) {
+        const uint32_t hbase = attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) +
+                               (static_cast<uint32_t>(kbase >> 1) + 4u * g) * kAttnPairMul;
+#pragma unroll
+        for (int kp = 0; kp < 2; ++kp)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) hp[kp][i] = attn_hash_input(key, hbase + (16u * kp + i) * kAttnPairMul);
+      }
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
-        uint32_t hp[2] = {0u, 0u};
-        if constexpr (DROP) {  // keys kbase + kb*16 + 4g + {0,1 | 2,3}: two key pairs
-          hp[0] = attn_hash_input(key, hbase + (8u * kb) * kAttnPairMul);
-          hp[1] = attn_hash_input(key, hbase + (8u * kb + 1u) * kAttnPairMul);
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float p = fast_exp2(__builtin_fmaf(s[qb][kb][i], P.scale_log2, -msub));
           rs += p;
           float pd = p;
-          if constexpr (DROP) pd = attn_keep(hp[i >> 1], static_cast<uint32_t>(i), P.drop_thr) ? p : 0.f;
+          if constexpr (DROP) pd = attn_keep_half(hp[kb >> 1][i], kb & 1, P.drop_thr) ? p : 0.f;
           s[qb][kb][i] = pd;
         }
       }
@@ -266,10 +268,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
 }
 
 // ------------------------------------------------------------------------------ bwd dK, dV
-template <bool DROP>
+// Per 64-query tile, four phases that each put one wave's MFMA work beside independent VALU
+// work of the same wave (sched_barrier-separated, so the scheduler interleaves within a phase):
+// S/dP of query rows 0-31 | S/dP of rows 32-63 + P/dS of rows 0-31 | dV/dK over rows 0-31 + P/dS
+// of rows 32-63 | dV/dK over rows 32-63. The previous loop ran all of S/dP, then all P/dS, then
+// all dV/dK per wave: 20 % MFMA busy, 50 % of wave cycles waiting at BERT-Large b128
+// (profiles/r5_attn_bwd_pmc_before.txt). Two LDS buffers with compile-time offsets (the loop
+// handles two tiles per trip), register-staged global loads one tile ahead, one barrier per tile.
+// MODE (diagnostics, TTD_ATTN_KV_DIAG; 0 in production): bit 0 skips the elementwise P / dS,
+// bit 1 the per-tile Q / dO reloads, bit 2 the per-tile barrier (only with bit 1) — wrong
+// results, for attributing the kernel's time; bit 3 writes per-workgroup clock stamps (entry,
+// prologue done, loop done, exit as s_memtime; entry / exit as s_memrealtime) over dV as
+// int64[grid][8] instead of dV (tools/attn_kv_stamps.py).
+template <bool DROP, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TILE_BYTES + 2 * KT * 4)];
   constexpr int BUF = 2 * TILE_BYTES + 2 * KT * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int kblocks = P.S / QBLK;
   const int t = tile::xcd_remap(blockIdx.x, gridDim.x);
   const int bh = t / kblocks, kblk = t - bh * kblocks;
@@ -279,6 +293,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
   const int k0 = kblk * QBLK + wave * 32;
   const int len = P.seqlen ? min(P.seqlen[b], P.S) : P.S;
   const long long tok0 = static_cast<long long>(b) * P.S;
+  long long stamp[6] = {};
+  if constexpr ((MODE & 8) != 0) {
+    stamp[0] = __builtin_amdgcn_s_memtime();
+    stamp[4] = __builtin_amdgcn_s_memrealtime();
+  }
 
   f32x4_t dk[2][4], dv[2][4];
 #pragma unroll
@@ -300,36 +319,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
     TileLoader lq, ld;
     lq.init(P.q + tok0 * P.ldq + h * D, P.ldq, tid);
     ld.init(P.dout + tok0 * P.lddo + h * D, P.lddo, tid);
-    const float* lse_row = P.lse + static_cast<long long>(bh) * P.S;
-    const float* del_row = P.delta + static_cast<long long>(bh) * P.S;
+    // per-tile statistics, staged with the dropout scale folded in: lse2 - log2(1/(1-p)) (exp2
+    // then gives P / (1-p), a kept probability's value) and delta * (1-p) (the product P * delta
+    // unchanged). Thread t < 64 moves lse of query t, 64 <= t < 128 delta of query t - 64.
+    const float* st_src = (tid < KT ? P.lse : P.delta) + static_cast<long long>(bh) * P.S + (tid & (KT - 1));
+    const float st_add = tid < KT && DROP ? -__builtin_amdgcn_logf(P.drop_scale) : 0.f;
+    const float st_mul = tid >= KT && DROP ? 1.f / P.drop_scale : 1.f;
+    float stv = 0.f;
     const uint32_t key = DROP ? drop_key(P.rng, P.site) : 0u;
-    const int ntiles = P.S / KT;
-    auto stage_stats = [&](char* buf, int qt) {
-      float* st = reinterpret_cast<float*>(buf + 2 * TILE_BYTES);
-      if (tid < KT) st[tid] = lse_row[qt * KT + tid];
-      else if (tid < 2 * KT) st[tid] = del_row[qt * KT + tid - KT];
+    const int ntiles = P.S / KT;  // even: S is a multiple of QBLK = 2 * KT
+
+    auto load = [&](int qt) {
+      lq.load(qt * KT, P.S);
+      ld.load(qt * KT, P.S);
+      if (tid < 2 * KT) stv = st_src[qt * KT];
     };
-    lq.load(0, P.S);
-    ld.load(0, P.S);
-    lq.store(smem);
-    ld.store(smem + TILE_BYTES);
-    stage_stats(smem, 0);
-    __syncthreads();
-    int cur = 0;
-    for (int qt = 0; qt < ntiles; ++qt) {
-      const bool nxt = qt + 1 < ntiles;
-      if (nxt) {
-        lq.load((qt + 1) * KT, P.S);
-        ld.load((qt + 1) * KT, P.S);
-      }
-      const char* sQ = smem + cur * BUF;
+    auto store = [&](char* nb) {
+      lq.store(nb);
+      ld.store(nb + TILE_BYTES);
+      if (tid < 2 * KT) reinterpret_cast<float*>(nb + 2 * TILE_BYTES)[tid] = (stv + st_add) * st_mul;
+    };
+    // S[q][key] and dP[q][key] for the query rows of half hq (qb = 2 hq, 2 hq + 1) of the tile
+    // image sQ: lane holds q = qb*16 + 4g + i, key = kb*16 + i16
+    auto sdp = [&](const char* sQ, int hq, f32x4_t (&sc)[4][2], f32x4_t (&dp)[4][2]) {
       const char* sD = sQ + TILE_BYTES;
-      const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE_BYTES);
-      const float* sDel = sL + KT;
-      // S[q][key] and dP[q][key]: lane holds q = qb*16 + 4g + i, key = kb*16 + i16
-      f32x4_t sc[4][2], dp[4][2];
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb) {
+      for (int qb = 2 * hq; qb < 2 * hq + 2; ++qb) {
         const bf16x8_t q0f = rd_row(sQ, qb * 16 + i16, g), q1f = rd_row(sQ, qb * 16 + i16, 4 + g);
         const bf16x8_t d0f = rd_row(sD, qb * 16 + i16, g), d1f = rd_row(sD, qb * 16 + i16, 4 + g);
 #pragma unroll
@@ -340,95 +355,153 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnParams P) {
           dp[qb][kb] = mfma(d1f, vf[kb][1], dp[qb][kb]);
         }
       }
-      // dropout hashes: lanes i16 and i16 ^ 1 hold keys 2j and 2j + 1 (one pair, one hash) of
-      // the same query rows, for kb = 0 and kb = 1: the even lane hashes the kb = 0 pairs, the
-      // odd lane the kb = 1 pairs, and they swap (16 hashes per lane instead of 32)
-      uint32_t hk[4][4][2];  // the 16-bit hash half of (query row, key kb) in the low bits
-      if constexpr (DROP) {
-        const bool odd = (i16 & 1) != 0;
-        // v_perm_b32 selectors (bytes of {other, mine}; 0x0c = zero byte): key parity = lane
-        // parity, so the even lane takes low halves, the odd lane high halves — one perm per
-        // element instead of a swap select, a shift / mask and a half select
-        const uint32_t sel0 = odd ? 0x0c0c0706u : 0x0c0c0100u, sel1 = odd ? 0x0c0c0302u : 0x0c0c0504u;
-        const uint32_t pair = static_cast<uint32_t>(k0 + (odd ? 16 : 0) + i16) >> 1;
+    };
+    // P_d and dS in place for half hq (sc <- P_d = P * keep / (1-p); dp <- dS = P * (keep * dP /
+    // (1-p) - delta) = P_d * dP - (P / (1-p)) * (delta * (1-p))): exp2, and per element one keep
+    // test, one select, one multiply and one FMA. Keys >= len are not masked here: a key's P and
+    // dS feed only its own dK / dV rows (the key is the MFMA column), which are zeroed at the
+    // store. Dropout: keys k0 + i16 and k0 + 16 + i16 (kb = 0, 1) are the halves of pair
+    // k0/2 + i16 — one hash per query row, no lane exchange.
+    auto hashes = [&](uint32_t hrow, int hq, uint32_t (&hh)[2][4]) {
+      if constexpr (DROP)
 #pragma unroll
-        for (int qb = 0; qb < 4; ++qb)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int ql = qb * 16 + 4 * g + i;
-            const uint32_t mine =
-                attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * P.S + qt * KT + ql)), pair);
-            // lane ^ 1 on the VALU (DPP quad_perm [1,0,3,2]), not an LDS bpermute round trip
-            const uint32_t other = __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);
-            hk[qb][i][0] = __builtin_amdgcn_perm(other, mine, sel0);
-            hk[qb][i][1] = __builtin_amdgcn_perm(other, mine, sel1);
-          }
-      }
-      // P, dS (in place: sc <- P*keep*scale, dp <- dS). (Specialising the loop on the wave's key
-      // mask, as bwd_q and fwd do, made this kernel spill 63 VGPRs.)
+          for (int i = 0; i < 4; ++i)
+            hh[u][i] = attn_hash_input(key, hrow + static_cast<uint32_t>((2 * hq + u) * 16 + i) * 0x9E3779B1u);
+    };
+    auto pds = [&](const float* sL, const uint32_t (&hq_hash)[2][4], int hq, f32x4_t (&sc)[4][2], f32x4_t (&dp)[4][2]) {
+      const float* sDel = sL + KT;
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb)
+      for (int qb = 2 * hq; qb < 2 * hq + 2; ++qb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int ql = qb * 16 + 4 * g + i;
           const float lse2 = sL[ql], del = sDel[ql];
+          const uint32_t hh = hq_hash[qb - 2 * hq][i];
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) {
-            const int kcol = k0 + kb * 16 + i16;
-            float p = kcol < len ? fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2) : 0.f;
-            float dpv = dp[qb][kb][i];
-            float pd = p;
-            if constexpr (DROP) {  // one select for both: keep factor 1/(1-p) or 0
-              const uint32_t h = hk[qb][i][kb];
-              const float kf = h >= P.drop_thr ? P.drop_scale : 0.f;
-              pd = p * kf;
-              dpv = dpv * kf;
+            const float p = fast_exp2(__builtin_fmaf(sc[qb][kb][i], P.scale_log2, -lse2));
+            const float dpv = dp[qb][kb][i];
+            if constexpr (DROP) {
+              const float pd = attn_keep_half(hh, kb, P.drop_thr) ? p : 0.f;
+              sc[qb][kb][i] = pd;
+              dp[qb][kb][i] = __builtin_fmaf(pd, dpv, -(p * del));
+            } else {
+              sc[qb][kb][i] = p;
+              dp[qb][kb][i] = p * (dpv - del);
             }
-            sc[qb][kb][i] = pd;
-            dp[qb][kb][i] = p * (dpv - del);
           }
         }
-      // dV^T += dO^T P_d ; dK^T += Q^T dS   (contraction over the 64 queries in 2 chunks)
+    };
+    // dV^T += dO^T P_d ; dK^T += Q^T dS over the 32 queries of half ks
+    auto pv = [&](const char* sQ, int ks, const f32x4_t (&sc)[4][2], const f32x4_t (&dp)[4][2]) {
+      const char* sD = sQ + TILE_BYTES;
+      bf16x8_t pfr[2], sfr[2];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t pfr[2], sfr[2];
+      for (int kb = 0; kb < 2; ++kb) {
+        pfr[kb] = pack_frag(sc[2 * ks][kb], sc[2 * ks + 1][kb]);
+        sfr[kb] = pack_frag(dp[2 * ks][kb], dp[2 * ks + 1][kb]);
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8_t dof = rd_col(sD, ks * 32, ks * 32 + 16, db * 16, lane);
+        const bf16x8_t qcf = rd_col(sQ, ks * 32, ks * 32 + 16, db * 16, lane);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-          pfr[kb] = pack_frag(sc[2 * ks][kb], sc[2 * ks + 1][kb]);
-          sfr[kb] = pack_frag(dp[2 * ks][kb], dp[2 * ks + 1][kb]);
-        }
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const bf16x8_t dof = rd_col(sD, ks * 32, ks * 32 + 16, db * 16, lane);
-          const bf16x8_t qcf = rd_col(sQ, ks * 32, ks * 32 + 16, db * 16, lane);
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
-            dv[kb][db] = mfma(dof, pfr[kb], dv[kb][db]);
-            dk[kb][db] = mfma(qcf, sfr[kb], dk[kb][db]);
-          }
+          dv[kb][db] = mfma(dof, pfr[kb], dv[kb][db]);
+          dk[kb][db] = mfma(qcf, sfr[kb], dk[kb][db]);
         }
       }
-      if (nxt) {
-        char* nb = smem + (cur ^ 1) * BUF;
-        lq.store(nb);
-        ld.store(nb + TILE_BYTES);
-        stage_stats(nb, qt + 1);
+    };
+    // one tile from LDS buffer BUFI (compile-time: every LDS address is a lane base plus an
+    // immediate); the next tile's global loads are in flight meanwhile and stored into the other
+    // buffer at the end
+    f32x4_t sc[4][2], dp[4][2];
+    auto tile = [&](int qt, auto bufi_c) {
+      constexpr int BUFI = decltype(bufi_c)::value;
+      const bool nxt = qt + 1 < ntiles && !(MODE & 2);
+      if (nxt) load(qt + 1);
+      const char* sQ = smem + BUFI * BUF;
+      const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE_BYTES);
+      const uint32_t hrow = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qt * KT + 4 * g)) +
+                                       (static_cast<uint32_t>(k0 >> 1) + i16) * kAttnPairMul
+                                 : 0u;
+      // four phases, MFMA work beside independent VALU work of the same wave, spread one MFMA per
+      // few VALU instructions by sched_group_barrier:
+      //   S/dP(rows 0-31) + hashes(rows 0-31) | S/dP(rows 32-63) + P/dS(rows 0-31) + hashes(rows
+      //   32-63) | dV/dK(rows 0-31) + P/dS(rows 32-63) | dV/dK(rows 32-63)
+      uint32_t h0[2][4] = {}, h1[2][4] = {};
+      sdp(sQ, 0, sc, dp);
+      hashes(hrow, 0, h0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, DROP ? 3 : 0, 0);
       }
-      __syncthreads();
-      cur ^= 1;
+      __builtin_amdgcn_sched_barrier(0);
+      sdp(sQ, 1, sc, dp);
+      if constexpr (!(MODE & 1)) pds(sL, h0, 0, sc, dp);
+      hashes(hrow, 1, h1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 12, 1);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x002, DROP ? 10 : 6, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      pv(sQ, 0, sc, dp);
+      if constexpr (!(MODE & 1)) pds(sL, h1, 1, sc, dp);
+      __builtin_amdgcn_sched_group_barrier(0x100, 20, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, 8, 2);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+        __builtin_amdgcn_sched_group_barrier(0x002, DROP ? 8 : 5, 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      pv(sQ, 1, sc, dp);
+      if (nxt) store(smem + (BUFI ^ 1) * BUF);
+      if constexpr (!(MODE & 4)) __syncthreads();
+    };
+    load(0);
+    store(smem);
+    __syncthreads();
+    if constexpr ((MODE & 8) != 0) stamp[1] = __builtin_amdgcn_s_memtime();
+    for (int qt = 0; qt < ntiles; qt += 2) {  // ntiles is even
+      tile(qt, std::integral_constant<int, 0>{});
+      tile(qt + 1, std::integral_constant<int, 1>{});
     }
+    if constexpr ((MODE & 8) != 0) stamp[2] = __builtin_amdgcn_s_memtime();
   }
-  // store dK (scaled by 1/sqrt(D)) and dV: lane holds key kb*16 + i16, d = db*16 + 4g + i
+  // store dK (scaled by 1/sqrt(D)) and dV: lane holds key kb*16 + i16, d = db*16 + 4g + i; keys
+  // >= len get zeros (their accumulators saw unmasked probabilities)
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
     const long long row = tok0 + k0 + kb * 16 + i16;
     bf16_t* pk = P.out + row * P.ld_out + h * D + 4 * g;
     bf16_t* pv = P.out2 + row * P.ld_out2 + h * D + 4 * g;
+    const bool valid = k0 + kb * 16 + i16 < len;
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      const f32x4_t a = dk[kb][db] * P.scale, c = dv[kb][db];
+      const f32x4_t zero = {0.f, 0.f, 0.f, 0.f};
+      const f32x4_t a = valid ? dk[kb][db] * P.scale : zero, c = valid ? dv[kb][db] : zero;
       *reinterpret_cast<uint2*>(pk + db * 16) = make_uint2(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]));
-      *reinterpret_cast<uint2*>(pv + db * 16) = make_uint2(pack_bf16x2(c[0], c[1]), pack_bf16x2(c[2], c[3]));
+      if constexpr ((MODE & 8) == 0)
+        *reinterpret_cast<uint2*>(pv + db * 16) = make_uint2(pack_bf16x2(c[0], c[1]), pack_bf16x2(c[2], c[3]));
+    }
+  }
+  if constexpr ((MODE & 8) != 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp[3] = __builtin_amdgcn_s_memtime();
+    stamp[5] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      long long* o = reinterpret_cast<long long*>(P.out2) + static_cast<long long>(blockIdx.x) * 8;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) o[j] = stamp[j];
+      o[6] = t;
+      o[7] = __smid();
     }
   }
 }
@@ -518,23 +591,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const int qrow = q0 + qb * 16 + i16;
-      const uint32_t hbase = DROP ? attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) +
-                                        (static_cast<uint32_t>(kbase >> 1) + 2u * g) * kAttnPairMul
-                                  : 0u;
+      uint32_t hp[2][4] = {};  // pairs as in the forward kernel
+      if constexpr (DROP) {
+        const uint32_t hbase = attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) +
+                               (static_cast<uint32_t>(kbase >> 1) + 4u * g) * kAttnPairMul;
+#pragma unroll
+        for (int kp = 0; kp < 2; ++kp)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) hp[kp][i] = attn_hash_input(key, hbase + (16u * kp + i) * kAttnPairMul);
+      }
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
-        uint32_t hp[2] = {0u, 0u};
-        if constexpr (DROP) {
-          hp[0] = attn_hash_input(key, hbase + (8u * kb) * kAttnPairMul);
-          hp[1] = attn_hash_input(key, hbase + (8u * kb + 1u) * kAttnPairMul);
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int kcol = kbase + kb * 16 + 4 * g + i;
           float p = fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2[qb]);
           if constexpr (MASK) p = kcol < len ? p : 0.f;
           float dpv = dp[qb][kb][i];
-          if constexpr (DROP) dpv = attn_keep(hp[i >> 1], static_cast<uint32_t>(i), P.drop_thr) ? dpv * P.drop_scale : 0.f;
+          if constexpr (DROP) dpv = attn_keep_half(hp[kb >> 1][i], kb & 1, P.drop_thr) ? dpv * P.drop_scale : 0.f;
           sc[qb][kb][i] = p * (dpv - del[qb]);
         }
       }
@@ -694,12 +768,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P
           dp[qb][j] = mfma(df[qb][1], vf[2 * pp + j][1], dp[qb][j]);
         }
       }
-      // P, dS in place (sc <- P * keep * scale, dp <- dS). Dropout: lanes i16, i16 ^ 1 hold the
-      // two keys of one pair for j = 0 and j = 1; the even lane hashes the j = 0 pair, the odd
-      // lane the j = 1 pair, and they swap (one hash per lane per (query, pair of tiles))
-      const bool odd = (i16 & 1) != 0;
-      const uint32_t sel0 = odd ? 0x0c0c0706u : 0x0c0c0100u, sel1 = odd ? 0x0c0c0302u : 0x0c0c0504u;
-      const uint32_t pair = static_cast<uint32_t>(k0 + (odd ? 16 : 0) + i16) >> 1;
+      // P, dS in place (sc <- P * keep * scale, dp <- dS). Dropout: keys k0 + i16 and k0 + 16 + i16
+      // (j = 0, 1) are the two halves of pair k0/2 + i16: one hash per lane per query row
+      const uint32_t pair = static_cast<uint32_t>(k0 >> 1) + i16;
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         // this lane's query rows qb*16 + 4g + i: lse2 and delta
@@ -707,14 +778,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P
         const f32x4_t dl = *reinterpret_cast<const f32x4_t*>(sL + QS + qb * 16 + 4 * g);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          uint32_t hk[2] = {0u, 0u};
+          uint32_t hh = 0u;
           if constexpr (DROP) {
             const int qg = s * QS + qb * 16 + 4 * g + i;
-            const uint32_t mine = attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * SK + qg)), pair);
-            // lane ^ 1 on the VALU (DPP quad_perm [1,0,3,2]), not an LDS bpermute round trip
-            const uint32_t other = __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);
-            hk[0] = __builtin_amdgcn_perm(other, mine, sel0);  // 16-bit halves, as in bwd_kv
-            hk[1] = __builtin_amdgcn_perm(other, mine, sel1);
+            hh = attn_pair_hash(key, attn_row_term(static_cast<uint32_t>(bh * SK + qg)), pair);
           }
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
@@ -723,7 +790,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(AttnParams P
             float dpv = dp[qb][j][i];
             float pd = p;
             if constexpr (DROP) {
-              const bool kp = hk[j] >= P.drop_thr;
+              const bool kp = attn_keep_half(hh, j, P.drop_thr);
               pd = kp ? p * P.drop_scale : 0.f;
               dpv = kp ? dpv * P.drop_scale : 0.f;
             }
@@ -891,7 +958,22 @@ TTDK_EXPORT int ttdk_attn_bwd(const bf16_t* q, long long ldq, const bf16_t* k, l
   if (p_drop > 0.f) hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, block, 0, st, P);
   else hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, block, 0, st, P);
   P.out = dk; P.ld_out = lddk; P.out2 = dv; P.ld_out2 = lddv;
-  if (p_drop > 0.f) hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, block, 0, st, P);
-  else hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, block, 0, st, P);
+  static const int kv_diag = [] {
+    const char* e = getenv("TTD_ATTN_KV_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  if (p_drop > 0.f) {
+    switch (kv_diag) {
+      case 1: hipLaunchKernelGGL((attn_bwd_kv_kernel<true, 1>), grid, block, 0, st, P); break;
+      case 2: hipLaunchKernelGGL((attn_bwd_kv_kernel<true, 2>), grid, block, 0, st, P); break;
+      case 6: hipLaunchKernelGGL((attn_bwd_kv_kernel<true, 6>), grid, block, 0, st, P); break;
+      case 7: hipLaunchKernelGGL((attn_bwd_kv_kernel<true, 7>), grid, block, 0, st, P); break;
+      case 8: hipLaunchKernelGGL((attn_bwd_kv_kernel<true, 8>), grid, block, 0, st, P); break;
+      case 15: hipLaunchKernelGGL((attn_bwd_kv_kernel<true, 15>), grid, block, 0, st, P); break;
+      default: hipLaunchKernelGGL((attn_bwd_kv_kernel<true, 0>), grid, block, 0, st, P);
+    }
+  } else {
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, block, 0, st, P);
+  }
   return hipGetLastError();
 }

@@ -5,10 +5,13 @@
 // lane l holds acc[i] = sum_k X[4 * (l >> 4) + i][k] * Y[l & 15][k], i = 0..3 — i.e. the
 // X index runs over 4 consecutive values per lane, the Y index lies on lane & 15.
 //
-// LDS images are 64-element (128-B) rows with the 16-B chunk index XOR-swizzled by
-// (row >> 1) & 7: b128 row reads (K-major fragments) are conflict-free, and
-// ds_read_b64_tr_b16 (column fragments: 4 consecutive rows x 4 columns per 16 lanes) reads
-// the same image, so one copy of a tile serves both orientations.
+// LDS images are 64-element (128-B) rows with the 16-B chunk index XOR-swizzled by row & 7:
+// b128 row reads (K-major fragments, 16 rows per lane group), ds_read_b64_tr_b16 column reads
+// (8 consecutive rows x 2 chunks per 32-lane half) and the fused backward's b64 dS stores
+// (16 rows, one chunk) are all conflict-free, so one copy of a tile serves both orientations.
+// (The previous XOR, (row >> 1) & 7, put rows r and r + 2 of a column read on the same two
+// slots: a 2-way conflict on every transposed read — 28M conflict cycles per BERT-Large
+// attn_bwd_kv launch, profiles/r5_attn_bwd_pmc_before.txt.)
 #pragma once
 #include "common.h"
 
@@ -16,7 +19,7 @@ namespace ttdk {
 namespace tile {
 
 __device__ __forceinline__ int off64(int row, int col) {  // byte offset of element (row, col), col % 4 == 0 ok
-  return row * 128 + ((((col >> 3) ^ ((row >> 1) & 7))) << 4) + ((col & 7) << 1);
+  return row * 128 + ((((col >> 3) ^ (row & 7))) << 4) + ((col & 7) << 1);
 }
 
 __device__ __forceinline__ bf16x8_t rd_row(const char* lds, int row, int kchunk) {
@@ -104,15 +107,18 @@ __device__ __forceinline__ bool drop_keep(uint32_t key, unsigned long long idx, 
   return h >= thr;
 }
 
-// Attention-probability dropout: one hash per PAIR of adjacent keys of a query row, each key
-// taking one 16-bit half (keep iff half >= thr16 = floor(p * 2^16)). The hash input is
-// rowid * C1 + (key >> 1) * C2 with rowid = (b*H + h)*S + q, so a lane derives its row term
-// once and pays one fmix32 per two probabilities (the per-element 64-bit index + hash made
-// the dropout variant of the kernels VALU-bound). ops/transformer.attention_keep_mask mirrors it.
+// Attention-probability dropout: one hash per PAIR of keys of a query row, each key taking one
+// 16-bit half (keep iff half >= thr16 = floor(p * 2^16)). Key k belongs to pair
+// ((k >> 5) << 4) | (k & 15) and takes half (k >> 4) & 1: keys k and k + 16 of an aligned 32-key
+// block share a hash, and every kernel's lane layout holds both in ONE lane (fwd / bwd_q: key
+// tiles kb and kb + 1 at the same i; bwd_kv / fused: the two 16-key tiles of a 32-key block at
+// the same lane), so no lane exchange is needed. (Adjacent-key pairs sat in lanes l and l ^ 1 of
+// the backward layouts: a DPP move and two byte permutes per hash.) The hash input is
+// rowid * C1 + pair * C2 with rowid = (b*H + h)*S + q, so a lane derives its row term once and
+// pays one mix per two probabilities. ops/transformer.attention_keep_mask mirrors it.
 constexpr uint32_t kAttnPairMul = 0x7FEB352Du;
 __device__ __forceinline__ uint32_t attn_row_term(uint32_t rowid) { return rowid * 0x9E3779B1u; }
-// hash of a precomputed input row_term + pair * kAttnPairMul (kernels walking consecutive pairs
-// form it incrementally instead of multiplying per pair)
+__device__ __forceinline__ uint32_t attn_pair_of(uint32_t k) { return ((k >> 5) << 4) | (k & 15u); }
 // One multiply-xorshift round (not murmur's two): the hash is regenerated for every probability
 // pair in both backward kernels, where its quarter-rate 32-bit multiplies were the dropout
 // variant's extra cost (bwd 864 vs 702 us per BERT-Large layer at p = 0.1 vs 0). The input is
@@ -125,12 +131,15 @@ __device__ __forceinline__ uint32_t attn_mix(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
+// hash of a precomputed input row_term + pair * kAttnPairMul (kernels walking consecutive pairs
+// form it incrementally instead of multiplying per pair)
 __device__ __forceinline__ uint32_t attn_hash_input(uint32_t key, uint32_t input) { return attn_mix(key ^ input); }
 __device__ __forceinline__ uint32_t attn_pair_hash(uint32_t key, uint32_t row_term, uint32_t pair) {
   return attn_hash_input(key, row_term + pair * kAttnPairMul);
 }
-__device__ __forceinline__ bool attn_keep(uint32_t h, uint32_t key_index, uint32_t thr16) {
-  return ((key_index & 1u) ? (h >> 16) : (h & 0xffffu)) >= thr16;
+// keep test of half `hi` ((key >> 4) & 1) of a pair hash
+__device__ __forceinline__ bool attn_keep_half(uint32_t h, bool hi, uint32_t thr16) {
+  return (hi ? (h >> 16) : (h & 0xffffu)) >= thr16;
 }
 
 inline uint32_t drop_threshold16(float p) {

@@ -235,14 +235,16 @@ def keep_mask(seed: int, step: int, site: int, p: float, idx) -> np.ndarray:
 
 def attention_keep_mask(seed: int, step: int, site: int, p: float, B: int, H: int, S: int) -> np.ndarray:
     """Keep mask [B, H, S(query), S(key)] of the attention-probability dropout (mirror of
-    tile_common.h attn_pair_hash / attn_keep: one hash per pair of adjacent keys, 16-bit halves)."""
+    tile_common.h attn_pair_hash / attn_keep_half: keys k and k + 16 of an aligned 32-key block
+    share one hash, pair ((k >> 5) << 4) | (k & 15), 16-bit half (k >> 4) & 1)."""
     key = np.uint64(drop_key(seed, step, site))
     thr = 0 if p <= 0 else (0x10000 if p >= 1 else int(float(np.float32(p)) * 65536.0))
     rowid = np.arange(B * H * S, dtype=np.uint64).reshape(B * H, S, 1)
     k = np.arange(S, dtype=np.uint64).reshape(1, 1, S)
-    mixed = ((rowid * np.uint64(0x9E3779B1)) + ((k >> np.uint64(1)) * np.uint64(0x7FEB352D))) & M32
+    pair = ((k >> np.uint64(5)) << np.uint64(4)) | (k & np.uint64(15))
+    mixed = ((rowid * np.uint64(0x9E3779B1)) + (pair * np.uint64(0x7FEB352D))) & M32
     h = _attn_mix(key ^ mixed)
-    half = np.where((k & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    half = np.where(((k >> np.uint64(4)) & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
     return (half >= np.uint64(thr)).reshape(B, H, S, S)
 
 

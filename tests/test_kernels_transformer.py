@@ -45,9 +45,12 @@ def _keep_tensor(rng_state, site, p, B, H, S, device):
 def test_attention_dropout_pair_hash_statistics():
     keep = T.attention_keep_mask(1234, 7, 3, 0.1, 2, 4, 256)
     assert abs(keep.mean() - 0.9) < 0.005
-    # the two keys of a pair use different halves of one hash: not correlated
-    a, b = keep[..., 0::2].ravel(), keep[..., 1::2].ravel()
-    assert abs(np.mean(a & b) - np.mean(a) * np.mean(b)) < 0.01
+    # the two keys of a pair (k and k + 16 of an aligned 32-key block) use different halves of
+    # one hash: not correlated; nor are adjacent keys (different hashes)
+    kk = keep.reshape(*keep.shape[:-1], -1, 2, 16)
+    for a, b in ((kk[..., 0, :], kk[..., 1, :]), (keep[..., 0::2], keep[..., 1::2])):
+        a, b = a.ravel(), b.ravel()
+        assert abs(np.mean(a & b) - np.mean(a) * np.mean(b)) < 0.01
     # neighbouring pairs of a row, the same key in neighbouring rows, and the same (query, key)
     # of neighbouring heads are independent too (one multiply-xorshift round per pair hash)
     for u, v in ((keep[..., 0:-2:2], keep[..., 2::2]), (keep[..., :-1, :], keep[..., 1:, :]),
