@@ -542,6 +542,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
     const long long srow = static_cast<long long>(bh) * P.S + q0 + qb * 16 + i16;
     lse2[qb] = P.lse[srow];
     if (g == 0) P.delta[srow] = acc;
+    if constexpr (DROP) {
+      // dS = P * (keep * dP / (1-p) - delta) = P_d' * dP - P' * (delta * (1-p)) with P' = P / (1-p)
+      // = exp2(s - (lse2 - log2(1/(1-p)))) and P_d' = keep ? P' : 0
+      lse2[qb] -= __builtin_amdgcn_logf(P.drop_scale);
+      del[qb] *= 1.f / P.drop_scale;
+    }
   }
   f32x4_t dq[2][4];
 #pragma unroll
@@ -561,18 +567,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
     lv.store(smem + TILE_BYTES);
   }
   __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const bool nxt = kt + 1 < ntiles;
-    if (nxt) {
-      lk.load((kt + 1) * KT, len);
-      lv.load((kt + 1) * KT, len);
-    }
-    const char* sK = smem + cur * 2 * TILE_BYTES;
+  // S, dP for the keys of half hk (kb = 2 hk, 2 hk + 1) of the tile: lane holds keys
+  // kb*16 + 4g + i of query qb*16 + i16
+  auto sdp = [&](const char* sK, int hk, f32x4_t (&sc)[2][4], f32x4_t (&dp)[2][4]) {
     const char* sV = sK + TILE_BYTES;
-    f32x4_t sc[2][4], dp[2][4];
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 2 * hk; kb < 2 * hk + 2; ++kb) {
       const bf16x8_t k0f = rd_row(sK, kb * 16 + i16, g), k1f = rd_row(sK, kb * 16 + i16, 4 + g);
       const bf16x8_t v0f = rd_row(sV, kb * 16 + i16, g), v1f = rd_row(sV, kb * 16 + i16, 4 + g);
 #pragma unroll
@@ -583,56 +583,96 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_kernel(AttnParams P) {
         dp[qb][kb] = mfma(v1f, df[qb][1], dp[qb][kb]);
       }
     }
-    const int kbase = kt * KT;
-    bf16x8_t sfr[2][2];
-    // key mask only on a tile that reaches past len (block-uniform)
-    auto pds = [&](auto maskc) {
-      constexpr bool MASK = decltype(maskc)::value;
+  };
+  // dropout pair hashes of the tile at kbase for key half hk (pairs as in the forward kernel:
+  // kb = 2 hk, 2 hk + 1 at the same i share one)
+  auto hashes = [&](int kbase, int hk, uint32_t (&hp)[2][4]) {
+    if constexpr (DROP)
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int qrow = q0 + qb * 16 + i16;
-      uint32_t hp[2][4] = {};  // pairs as in the forward kernel
-      if constexpr (DROP) {
-        const uint32_t hbase = attn_row_term(static_cast<uint32_t>(bh * P.S + qrow)) +
-                               (static_cast<uint32_t>(kbase >> 1) + 4u * g) * kAttnPairMul;
+      for (int qb = 0; qb < 2; ++qb) {
+        const uint32_t hbase = attn_row_term(static_cast<uint32_t>(bh * P.S + q0 + qb * 16 + i16)) +
+                               (static_cast<uint32_t>(kbase >> 1) + 4u * g + 16u * hk) * kAttnPairMul;
 #pragma unroll
-        for (int kp = 0; kp < 2; ++kp)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) hp[kp][i] = attn_hash_input(key, hbase + (16u * kp + i) * kAttnPairMul);
+        for (int i = 0; i < 4; ++i) hp[qb][i] = attn_hash_input(key, hbase + static_cast<uint32_t>(i) * kAttnPairMul);
       }
+  };
+  // dS in place for key half hk. (DROP: lse2 / del carry the dropout scale, p is P / (1-p) — see
+  // the prologue.) Keys >= len need no mask: their K rows are zero-filled in LDS, so whatever dS
+  // they get adds nothing to dQ = dS K (and their S = 0, dP = 0 keep dS finite).
+  auto pds = [&](int hk, const uint32_t (&hp)[2][4], f32x4_t (&sc)[2][4], const f32x4_t (&dp)[2][4]) {
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int kb = 2 * hk; kb < 2 * hk + 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int kcol = kbase + kb * 16 + 4 * g + i;
-          float p = fast_exp2(sc[qb][kb][i] * P.scale_log2 - lse2[qb]);
-          if constexpr (MASK) p = kcol < len ? p : 0.f;
-          float dpv = dp[qb][kb][i];
-          if constexpr (DROP) dpv = attn_keep_half(hp[kb >> 1][i], kb & 1, P.drop_thr) ? dpv * P.drop_scale : 0.f;
-          sc[qb][kb][i] = p * (dpv - del[qb]);
+          const float p = fast_exp2(__builtin_fmaf(sc[qb][kb][i], P.scale_log2, -lse2[qb]));
+          const float dpv = dp[qb][kb][i];
+          if constexpr (DROP) {
+            const float pd = attn_keep_half(hp[qb][i], kb & 1, P.drop_thr) ? p : 0.f;
+            sc[qb][kb][i] = __builtin_fmaf(pd, dpv, -(p * del[qb]));
+          } else {
+            sc[qb][kb][i] = p * (dpv - del[qb]);
+          }
         }
-      }
-      sfr[qb][0] = pack_frag(sc[qb][0], sc[qb][1]);
-      sfr[qb][1] = pack_frag(sc[qb][2], sc[qb][3]);
+  };
+  // dQ += dS K over the 32 keys of half ks
+  auto dqh = [&](const char* sK, int ks, const f32x4_t (&sc)[2][4]) {
+    bf16x8_t sfr[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) sfr[qb] = pack_frag(sc[qb][2 * ks], sc[qb][2 * ks + 1]);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const bf16x8_t kc = rd_col(sK, ks * 32, ks * 32 + 16, db * 16, lane);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) dq[qb][db] = mfma(kc, sfr[qb], dq[qb][db]);
     }
-    };
-    if (kbase + KT <= len) pds(std::false_type{});
-    else pds(std::true_type{});
+  };
+  // one 64-key tile in four phases (as attn_bwd_kv_kernel): S/dP(keys 0-31) + hashes | S/dP(keys
+  // 32-63) + dS(keys 0-31) | dQ(keys 0-31) + dS(keys 32-63) | dQ(keys 32-63)
+  int cur = 0;
+  f32x4_t sc[2][4], dp[2][4];
+  auto tile = [&](int kt) {
+    const bool nxt = kt + 1 < ntiles;
+    if (nxt) {
+      lk.load((kt + 1) * KT, len);
+      lv.load((kt + 1) * KT, len);
+    }
+    const char* sK = smem + cur * 2 * TILE_BYTES;
+    const int kbase = kt * KT;
+    uint32_t h0[2][4] = {}, h1[2][4] = {};
+    sdp(sK, 0, sc, dp);
+    hashes(kbase, 0, h0);
+    hashes(kbase, 1, h1);
+    __builtin_amdgcn_sched_barrier(0);
+    sdp(sK, 1, sc, dp);
+    pds(0, h0, sc, dp);
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int k = 0; k < 16; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x002, DROP ? 6 : 4, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dqh(sK, 0, sc);
+    pds(1, h1, sc, dp);
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 2);
+    __builtin_amdgcn_sched_group_barrier(0x002, 4, 2);
 #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const bf16x8_t kc = rd_col(sK, ks * 32, ks * 32 + 16, db * 16, lane);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) dq[qb][db] = mfma(kc, sfr[qb][ks], dq[qb][db]);
-      }
+    for (int k = 0; k < 8; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, DROP ? 12 : 8, 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dqh(sK, 1, sc);
     if (nxt) {
       lk.store(smem + (cur ^ 1) * 2 * TILE_BYTES);
       lv.store(smem + (cur ^ 1) * 2 * TILE_BYTES + TILE_BYTES);
     }
     __syncthreads();
     cur ^= 1;
-  }
+  };
+  for (int kt = 0; kt < ntiles; ++kt) tile(kt);
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     bf16_t* op = P.out + (tok0 + q0 + qb * 16 + i16) * P.ld_out + h * D + 4 * g;

@@ -119,15 +119,17 @@ __device__ __forceinline__ bool drop_keep(uint32_t key, unsigned long long idx, 
 constexpr uint32_t kAttnPairMul = 0x7FEB352Du;
 __device__ __forceinline__ uint32_t attn_row_term(uint32_t rowid) { return rowid * 0x9E3779B1u; }
 __device__ __forceinline__ uint32_t attn_pair_of(uint32_t k) { return ((k >> 5) << 4) | (k & 15u); }
-// One multiply-xorshift round (not murmur's two): the hash is regenerated for every probability
-// pair in both backward kernels, where its quarter-rate 32-bit multiplies were the dropout
-// variant's extra cost (bwd 864 vs 702 us per BERT-Large layer at p = 0.1 vs 0). The input is
-// already an odd-multiplier progression over (row, pair) xor a murmur-mixed key; statistics
-// (keep rate, pair-half / neighbour-pair / neighbour-row independence) are pinned by
-// tests/test_kernels_transformer.py::test_attention_dropout_pair_hash_statistics on the mirror.
+// One xorshift - 24-bit multiply - xorshift round: the hash is regenerated for every probability
+// pair in the forward and both backward kernels, whose VALU issue bounds them; v_mul_u32_u24 is a
+// full-rate instruction where the 32-bit v_mul_lo_u32 is quarter rate (16 of ~300 VALU
+// instructions per tile, ~15 % of the tile's VALU cycles). Bits 24-31 of the input reach the
+// product through the first xorshift (into bits 8-15). The input is already an odd-multiplier
+// progression over (row, pair) xor a murmur-mixed key; statistics (keep rate, pair-half /
+// neighbour-pair / neighbour-row / neighbour-head independence, same as the 32-bit multiply within
+// sampling noise) are pinned by tests/test_kernels_transformer.py on the mirror.
 __device__ __forceinline__ uint32_t attn_mix(uint32_t h) {
   h ^= h >> 16;
-  h *= 0x846CA68Bu;
+  h = __umul24(h, 0x9E3779u);
   h ^= h >> 16;
   return h;
 }
