@@ -487,15 +487,24 @@ __device__ __forceinline__ float fast_tanh(float u) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * 2.8853900817779268f));
 }
 
+// tanh-GELU as x * sigmoid(2u), u = k0 (x + k1 x^3): 0.5 x (1 + tanh u) = x / (1 + e^(-2u)), with
+// 2u log2(e) = x (c1 + c2 x^2) — five plain VALU ops + v_exp_f32 + v_rcp_f32 per element (the
+// 0.5 x (1 + tanh) form took ten plain ops; the GELU / dGELU GEMM epilogues run ~256 elements
+// per lane after the main loop). Saturates through exp2 -> inf / 0 (x -> -inf: 0, +inf: x).
+constexpr float kGeluC1 = 2.f * 0.7978845608028654f * 1.4426950408889634f;
+constexpr float kGeluC2 = kGeluC1 * 0.044715f;
 __device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + fast_tanh(k0 * (x + k1 * x * x * x)));
+  const float z = -x * __builtin_fmaf(kGeluC2, x * x, kGeluC1);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
 }
 
+// d/dx x s(x), s = sigmoid(2u): s + x s (1 - s) 2u' = s (1 + x (1 - s) 2 k0 (1 + 3 k1 x^2))
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float t = fast_tanh(k0 * (x + k1 * x * x * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  const float t = x * x;
+  const float sg = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * __builtin_fmaf(kGeluC2, t, kGeluC1)));
+  const float q = __builtin_fmaf(6.f * k0 * k1, t, 2.f * k0);
+  return __builtin_fmaf(sg, x * (1.f - sg) * q, sg);  // (1 - sg, not e * sg: inf * 0 at x -> -inf)
 }
 
 struct EpiParams {
