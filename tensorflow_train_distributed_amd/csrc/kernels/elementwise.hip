@@ -154,6 +154,49 @@ __global__ __launch_bounds__(256) void transpose8_bf16_kernel(const uint4* __res
   }
 }
 
+// bf16 [A][C] -> [C][A] for A, C multiples of 128: one workgroup per 128 x 128 tile. Thread
+// (ai, ci) = (tid / 16, tid % 16) loads its 8 x 8 block as 8 source-row pieces of 16 B (16 lanes
+// per 256-B row segment), transposes it in registers (v_perm_b32), and parks the 8 output pieces
+// in an LDS image of the output tile ([128 rows][256 B], 16-B chunk c at slot c ^ ((row >> 3) &
+// 15): the 8-lane ds_write_b128 groups hit 8 different slots); after one barrier every store
+// instruction writes 4 whole 256-B output row segments. transpose8_bf16_kernel stores each
+// lane's 16 B to a different output row (64 rows per instruction): 47 us for a 4096 x 1024 BERT
+// weight, ~0.35 TB/s.
+__global__ __launch_bounds__(256) void transpose128_bf16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                              int A, int C) {
+  __shared__ __attribute__((aligned(16))) uint4 img[128 * 16];
+  const int tiles_c = C / 128;
+  const int ta = blockIdx.x / tiles_c, tc = blockIdx.x - ta * tiles_c;
+  const int tid = threadIdx.x, ai = tid >> 4, ci = tid & 15;
+  const int cb = C / 8, ab = A / 8;
+  uint32_t r[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 v = src[(static_cast<long long>(ta) * 128 + ai * 8 + i) * cb + tc * 16 + ci];
+    r[i][0] = v.x;
+    r[i][1] = v.y;
+    r[i][2] = v.z;
+    r[i][3] = v.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t lo = r[2 * d][j >> 1], hi = r[2 * d + 1][j >> 1];
+      o[d] = (j & 1) ? __builtin_amdgcn_perm(hi, lo, 0x07060302u) : __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+    }
+    const int row = ci * 8 + j;  // output row within the tile; chunk = ai
+    img[row * 16 + (ai ^ ci)] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int row = it * 16 + (tid >> 4), c = tid & 15;
+    dst[(static_cast<long long>(tc) * 128 + row) * ab + ta * 16 + c] = img[row * 16 + (c ^ ((row >> 3) & 15))];
+  }
+}
+
 // fp32 [A][B][C] -> fp32 [C][B][A] (checkpoint layout conversions: KRSC <-> RSCK done as 2-D)
 __global__ void transpose2d_f32_kernel(const float* __restrict__ src, float* __restrict__ dst, int R, int C) {
   __shared__ float tile[32][33];
@@ -424,6 +467,12 @@ TTDK_EXPORT int ttdk_unpad_channels(const bf16_t* x, bf16_t* y, long long rows, 
 
 // [A][B][C] -> [C][B][A] bf16
 TTDK_EXPORT int ttdk_transpose_aca_bf16(const bf16_t* src, bf16_t* dst, int A, int B, int C, hipStream_t st) {
+  if (B == 1 && A % 128 == 0 && C % 128 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    hipLaunchKernelGGL(transpose128_bf16_kernel, dim3((A / 128) * (C / 128)), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), A, C);
+    return hipGetLastError();
+  }
   if (B == 1 && A % 8 == 0 && C % 8 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
     const long long nblk = static_cast<long long>(A / 8) * (C / 8);

@@ -345,10 +345,12 @@ def test_bf16_rounding_matches_torch_bitwise():
     assert int(((dev_ref != ref) & ~isnan).sum()) == 0
 
 
-@pytest.mark.parametrize("A,B,C", [(1024, 1, 4096), (4096, 1, 1024), (1000, 1, 24), (13, 1, 40), (64, 9, 128)])
+@pytest.mark.parametrize("A,B,C", [(1024, 1, 4096), (4096, 1, 1024), (3072, 1, 1024), (136, 1, 264), (1000, 1, 24),
+                                   (13, 1, 40), (64, 9, 128)])
 def test_weight_transpose_matches_torch(A, B, C):
-    """[A][B][C] -> [C][B][A] bf16: the 8 x 8 register-block kernel (B == 1, multiples of 8) and
-    the LDS-tile kernel (everything else) against torch's permute, bit for bit."""
+    """[A][B][C] -> [C][B][A] bf16: the 128 x 128 LDS-staged tile kernel (B == 1, multiples of
+    128), the 8 x 8 register-block kernel (B == 1, multiples of 8) and the LDS-tile kernel
+    (everything else) against torch's permute, bit for bit."""
     from tensorflow_train_distributed_amd.ops import kernels as K
     w = torch.randn(A, 1, B, C, device="cuda").to(torch.bfloat16)
     out = K.krsc_to_crsk(w)
