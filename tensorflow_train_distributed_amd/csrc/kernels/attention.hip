@@ -197,10 +197,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[qb][kb][i]);
       mx = tile::rows4_max(mx);
-      const float mnew = fmaxf(m[qb], mx * P.scale_log2);
-      const float msub = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = fast_exp2(m[qb] - msub);
-      m[qb] = mnew;
+      // lazy rescale: the running max moves (and O, l are rescaled) only when some row of the
+      // wave saw its max grow by more than 8 (log2 units) — otherwise P = exp2(s - m) stays
+      // below 2^8 (exact in fp32, in range for the bf16 P operand) and the 16 O multiplies and
+      // the alpha exp2 of the tile are skipped (wave-uniform branch; lse = m + log2 l either way)
+      const float mxs = mx * P.scale_log2;
+      float alpha = 1.f;
+      const bool grow = mxs > m[qb] + 8.f;
+      if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+        const float mnew = fmaxf(m[qb], mxs);
+        alpha = fast_exp2(m[qb] - (mnew == -INFINITY ? 0.f : mnew));
+        m[qb] = mnew;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[qb][db] *= alpha;
+      }
+      const float msub = m[qb] == -INFINITY ? 0.f : m[qb];
       float rs = 0.f;
       const int qrow = q0 + qb * 16 + i16;
       // keys kbase + kb*16 + 4g + i: pair kbase/2 + (kb >> 1)*16 + 4g + i, half kb & 1 — the
@@ -227,8 +238,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       }
       rs = tile::rows4_sum(rs);
       l[qb] = l[qb] * alpha + rs;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) o[qb][db] *= alpha;
       pf[qb][0] = pack_frag(s[qb][0], s[qb][1]);
       pf[qb][1] = pack_frag(s[qb][2], s[qb][3]);
     }
