@@ -162,11 +162,11 @@ __global__ __launch_bounds__(256) void transpose8_bf16_kernel(const uint4* __res
 // instruction writes 4 whole 256-B output row segments. transpose8_bf16_kernel stores each
 // lane's 16 B to a different output row (64 rows per instruction): 47 us for a 4096 x 1024 BERT
 // weight, ~0.35 TB/s.
-__global__ __launch_bounds__(256) void transpose128_bf16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                              int A, int C) {
+__device__ __forceinline__ void transpose128_tile(const uint4* __restrict__ src, uint4* __restrict__ dst, int A, int C,
+                                                  int tile) {
   __shared__ __attribute__((aligned(16))) uint4 img[128 * 16];
   const int tiles_c = C / 128;
-  const int ta = blockIdx.x / tiles_c, tc = blockIdx.x - ta * tiles_c;
+  const int ta = tile / tiles_c, tc = tile - ta * tiles_c;
   const int tid = threadIdx.x, ai = tid >> 4, ci = tid & 15;
   const int cb = C / 8, ab = A / 8;
   uint32_t r[8][4];
@@ -195,6 +195,32 @@ __global__ __launch_bounds__(256) void transpose128_bf16_kernel(const uint4* __r
     const int row = it * 16 + (tid >> 4), c = tid & 15;
     dst[(static_cast<long long>(tc) * 128 + row) * ab + ta * 16 + c] = img[row * 16 + (c ^ ((row >> 3) & 15))];
   }
+}
+
+__global__ __launch_bounds__(256) void transpose128_bf16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                              int A, int C) {
+  transpose128_tile(src, dst, A, C, blockIdx.x);
+}
+
+// Many [A][C] -> [C][A] transposes (all multiples of 128) in ONE launch: block b takes tile
+// b - tile_begin of the last entry whose tile_begin <= b (binary search). BERT refreshes 96
+// transposed weight copies per step; as separate launches of 64-256 workgroups each they ran
+// one after another between the forward GEMMs (each of which holds every CU's register file).
+struct TransposeEntry {
+  const uint4* src;
+  uint4* dst;
+  int A, C, tile_begin, pad;
+};
+__global__ __launch_bounds__(256) void transpose128_batch_kernel(const TransposeEntry* __restrict__ tab, int n) {
+  const int bid = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].tile_begin <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const TransposeEntry e = tab[lo];
+  transpose128_tile(e.src, e.dst, e.A, e.C, bid - e.tile_begin);
 }
 
 // fp32 [A][B][C] -> fp32 [C][B][A] (checkpoint layout conversions: KRSC <-> RSCK done as 2-D)
@@ -462,6 +488,14 @@ TTDK_EXPORT int ttdk_pad_channels(const bf16_t* x, bf16_t* y, long long rows, in
 
 TTDK_EXPORT int ttdk_unpad_channels(const bf16_t* x, bf16_t* y, long long rows, int Cp, int C, hipStream_t st) {
   hipLaunchKernelGGL(unpad_channels_kernel, dim3(grid_for(rows * C)), dim3(256), 0, st, x, y, rows, Cp, C);
+  return hipGetLastError();
+}
+
+// tab: n TransposeEntry rows (device memory, 32 B each; src / dst 16-B aligned, A and C
+// multiples of 128, tile_begin the running sum of (A/128)*(C/128)); tiles: the total
+TTDK_EXPORT int ttdk_transpose128_batch_bf16(const void* tab, int n, int tiles, hipStream_t st) {
+  if (n <= 0 || tiles <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(transpose128_batch_kernel, dim3(tiles), dim3(256), 0, st, static_cast<const TransposeEntry*>(tab), n);
   return hipGetLastError();
 }
 

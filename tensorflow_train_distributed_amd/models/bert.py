@@ -173,6 +173,9 @@ class BertPretraining:
         # GEMMs, 2 = also the plain / accumulating data gradients, 3 = the weight gradients too.
         self.blaslt = int(os.environ.get("TTD_BERT_BLASLT", "0")) if self.device.type == "cuda" else 0
         self._wt = None
+        self._wt_batch = None
+        # TTD_BERT_WT_BATCH=0: one transpose launch per weight copy instead of one batched launch
+        self.wt_batch = os.environ.get("TTD_BERT_WT_BATCH", "1") != "0"
         if self.device.type == "cuda":
             from ..ops.transformer import RngState
             self.rng = RngState(seed * 7919 + 17, self.device)
@@ -261,12 +264,21 @@ class BertPretraining:
             for l in range(L):
                 ws = [self._fused(l, "w")] + [P.c[self._ln(l, n)] for n in self._WT_NAMES]
                 self._wt.append([torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device) for w in ws])
+        pairs, rest = [], []
         for l in range(L):
             ws = [self._fused(l, "w")] + [P.c[self._ln(l, n)] for n in self._WT_NAMES]
             for i, (w, t) in enumerate(zip(ws, self._wt[l])):
                 if self.blaslt >= 2 and i != 3:
                     continue  # only the dGELU data gradient (FFN2's weight) still reads a copy
-                K.krsc_to_crsk(w.view(w.shape[0], 1, 1, w.shape[1]), out=t.view(t.shape[0], 1, 1, t.shape[1]))
+                (pairs if self.wt_batch and K.TransposeBatch.fits(w, t) else rest).append((w, t))
+        if pairs:
+            # every copy in one launch (96 separate launches ran one after another between the
+            # forward GEMMs); the pointer table is built once and re-checked per call
+            if self._wt_batch is None or len(self._wt_batch.pairs) != len(pairs):
+                self._wt_batch = K.TransposeBatch(pairs)
+            self._wt_batch.run(pairs)
+        for w, t in rest:
+            K.krsc_to_crsk(w.view(w.shape[0], 1, 1, w.shape[1]), out=t.view(t.shape[0], 1, 1, t.shape[1]))
 
     def _dgrad(self, dy, l, which, **kw):
         """dx = dy · W for encoder weight `which` (0 = fused QKV, 1.. = _WT_NAMES) of layer l."""

@@ -118,6 +118,7 @@ _SIGS = {
     "ttdk_pad_channels": [P, P, L, I, I, P],
     "ttdk_unpad_channels": [P, P, L, I, I, P],
     "ttdk_transpose_aca_bf16": [P, P, I, I, I, P],
+    "ttdk_transpose128_batch_bf16": [P, I, I, P],
     "ttdk_wprep": [P, P, P, I, I, P],
     "ttdk_transpose2d_f32": [P, P, I, I, P],
     "ttdk_bias_act_dropout_fwd": [P, P, P, L, I, I, F, U64, U64, I, P],

@@ -313,6 +313,54 @@ def subpixel_phases(s, pad, R, H):
     return out
 
 
+class TransposeBatch:
+    """bf16 [A][C] -> [C][A] for a fixed list of (src, dst) 2-D tensor pairs in ONE launch
+    (ttdk_transpose128_batch_bf16; A and C multiples of 128, 16-B aligned, contiguous rows).
+    The device table holds raw pointers: run() re-checks them against the tensors and rebuilds
+    the table when one moved (never inside a graph capture — there it raises)."""
+
+    _DT = np.dtype([("src", "<u8"), ("dst", "<u8"), ("A", "<i4"), ("C", "<i4"), ("tile_begin", "<i4"),
+                    ("pad", "<i4")])
+
+    @staticmethod
+    def fits(src, dst):
+        A, C = src.shape
+        return (src.dtype == torch.bfloat16 and dst.dtype == torch.bfloat16 and src.is_contiguous()
+                and dst.is_contiguous() and tuple(dst.shape) == (C, A) and A % 128 == 0 and C % 128 == 0
+                and src.data_ptr() % 16 == 0 and dst.data_ptr() % 16 == 0)
+
+    def __init__(self, pairs):
+        self.pairs = list(pairs)
+        if not self.pairs or not all(self.fits(s_, d_) for s_, d_ in self.pairs):
+            raise ValueError("TransposeBatch: every pair must be bf16 [A][C] -> [C][A], A, C % 128 == 0, aligned")
+        self._ptrs = None
+        self._tab = None
+        self.tiles = 0
+        self._build()
+
+    def _build(self):
+        rows, t = [], 0
+        for s_, d_ in self.pairs:
+            A, C = s_.shape
+            rows.append((s_.data_ptr(), d_.data_ptr(), A, C, t, 0))
+            t += (A // 128) * (C // 128)
+        self._tab = torch.from_numpy(np.array(rows, dtype=self._DT).view(np.uint8).copy()).to(self.pairs[0][0].device)
+        self.tiles = t
+        self._ptrs = [(s_.data_ptr(), d_.data_ptr()) for s_, d_ in self.pairs]
+
+    def run(self, pairs=None):
+        """pairs: this call's (src, dst) tensors (default: the constructor's); the table is rebuilt
+        when any pointer differs from the one it holds."""
+        if pairs is not None:
+            self.pairs = list(pairs)
+        ptrs = [(s_.data_ptr(), d_.data_ptr()) for s_, d_ in self.pairs]
+        if ptrs != self._ptrs:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("TransposeBatch: tensors moved during a graph capture")
+            self._build()
+        _lib.call("ttdk_transpose128_batch_bf16", self._tab.data_ptr(), len(self.pairs), self.tiles, _s())
+
+
 class WeightPrep:
     """Every data-gradient filter operand of a network in one launch per step (ttdk_wprep):
     [C,R,S,K] transposes of the [K,R,S,C] filters, and for strided 3x3 dgrads the sub-pixel

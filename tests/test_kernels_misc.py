@@ -345,6 +345,28 @@ def test_bf16_rounding_matches_torch_bitwise():
     assert int(((dev_ref != ref) & ~isnan).sum()) == 0
 
 
+def test_transpose_batch_matches_torch():
+    """Many [A][C] -> [C][A] transposes in one launch (ops.kernels.TransposeBatch, BERT's weight
+    copies) bit for bit against torch, and a rebuilt pointer table after a destination moves."""
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    torch.manual_seed(0)
+    shapes = [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096), (128, 256)]
+    src = [torch.randn(a, c, device="cuda").to(torch.bfloat16) for a, c in shapes]
+    dst = [torch.empty(c, a, device="cuda", dtype=torch.bfloat16) for a, c in shapes]
+    tb = K.TransposeBatch(list(zip(src, dst)))
+    tb.run()
+    for s_, d_ in zip(src, dst):
+        assert torch.equal(d_, s_.t())
+    dst[2] = torch.empty_like(dst[2])
+    src[0].mul_(2)
+    tb.run(list(zip(src, dst)))
+    for s_, d_ in zip(src, dst):
+        assert torch.equal(d_, s_.t())
+    with pytest.raises(ValueError):
+        K.TransposeBatch([(torch.zeros(100, 128, device="cuda", dtype=torch.bfloat16),
+                           torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16))])
+
+
 @pytest.mark.parametrize("A,B,C", [(1024, 1, 4096), (4096, 1, 1024), (3072, 1, 1024), (136, 1, 264), (1000, 1, 24),
                                    (13, 1, 40), (64, 9, 128)])
 def test_weight_transpose_matches_torch(A, B, C):
