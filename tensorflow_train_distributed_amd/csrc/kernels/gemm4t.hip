@@ -418,11 +418,16 @@ static int g4t_enabled() {
   return v;
 }
 
-// floats of workspace ttdk_gemm4t_wgrad needs: split partial tiles + bias-gradient partials
+// floats of workspace ttdk_gemm4t_wgrad needs: split partial tiles + bias-gradient partials;
+// -1 when the kernel would refuse the shape (the same admission checks as ttdk_gemm4t_wgrad,
+// except the leading dimensions / pointers, with lda = M and ldb = N)
 TTDK_EXPORT long long ttdk_gemm4t_ws(int M, int N, int K, int splits) {
   using namespace ttdk;
+  const long long lim = 1LL << 31;
+  if (!g4t_enabled() || K % 64 || K < 128 || M < 8 || N < 8 || M % 8 || N % 8 ||
+      static_cast<long long>(K) * M * 2 >= lim || static_cast<long long>(K) * N * 2 >= lim)
+    return -1;
   const int ktiles = K / 64;
-  if (ktiles < 2) return -1;
   splits = std::max(1, std::min(splits, ktiles / 2));
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);

@@ -150,8 +150,10 @@ TTDK_EXPORT int ttdk_gemm_bf16_splitk(const bf16_t* A, long long lda, int a_kmaj
 // splits * ceil(N / 256) * M floats (row-sum partials). Returns hipErrorInvalidValue when the
 // shape does not take the 256-row ping-pong kernel (the caller keeps its column-sum pass).
 TTDK_EXPORT long long ttdk_gemm_wgrad_bias_ws(int M, int N, int K, int splits) {
+  // -1 (no fused path: the caller keeps its column-sum pass) unless gemm4t or the 256-row
+  // kernel admits the shape
   const long long w4 = ttdk_gemm4t_ws(M, N, K, splits);
-  if (big_bn(M, N, K) != 256) return w4;
+  if (big_bn(M, N, K) != 256 || M % 8 || N % 8 || K % 64) return w4;
   const int ktiles = K / 64;
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles;

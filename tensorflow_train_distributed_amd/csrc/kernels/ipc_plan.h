@@ -62,11 +62,15 @@ constexpr void part(long long lo, long long hi, int vec, int nb, int b, long lon
   *phi = e;
 }
 
-// Workgroups of one launch: ~16 KB of the bucket per workgroup, 8 .. kMaxBlocks.
-constexpr int blocks_for(long long bytes) {
+// Workgroups of one launch: ~16 KB of the bucket per workgroup, 8 .. kMaxBlocks, and never more
+// than `budget` (> 0): the CTA budget the RCCL engine was given for the collectives that run
+// next to the backward (rccl.choose_cta_budget), so the direct path spins on no more CUs than
+// RCCL would hold.
+constexpr int blocks_for(long long bytes, int budget = 0) {
   long long b = ceil_div_ll(bytes, 16 << 10);
   if (b < 8) b = 8;
   if (b > kMaxBlocks) b = kMaxBlocks;
+  if (budget > 0 && b > budget) b = budget;
   return static_cast<int>(b);
 }
 

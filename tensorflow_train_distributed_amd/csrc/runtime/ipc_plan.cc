@@ -16,4 +16,4 @@ TTD_EXPORT void ttd_ipc_part(long long lo, long long hi, int vec, int nb, int b,
   ttd_ipc::part(lo, hi, vec, nb, b, plo, phi);
 }
 
-TTD_EXPORT int ttd_ipc_blocks(long long bytes) { return ttd_ipc::blocks_for(bytes); }
+TTD_EXPORT int ttd_ipc_blocks(long long bytes, int budget) { return ttd_ipc::blocks_for(bytes, budget); }

@@ -290,7 +290,8 @@ def gemm4t(dy, x, out=None, bias_out=None, *, splits=1, beta=0, alpha=1.0):
         raise ValueError("gemm4t: bias_out must be a contiguous fp32 [%d]" % M)
     nws = int(_lib.query("ttdk_gemm4t_ws", M, N, K, int(splits)))
     if nws < 0:
-        raise ValueError("gemm4t: K=%d needs >= 2 K-tiles of 64" % K)
+        raise ValueError("gemm4t does not take M=%d N=%d K=%d (K a multiple of 64 >= 128, M / N multiples "
+                         "of 8, operands < 2 GiB, TTD_G4T on)" % (M, N, K))
     ws = torch.empty(max(nws, 1), dtype=torch.float32, device=dy.device)
     _log("gemm4t", M, N, K, splits)
     _lib.call("ttdk_gemm4t_wgrad", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K, int(splits),

@@ -112,7 +112,7 @@ class BucketedAllReducer:
         if self.comm is not None and self.world > 1 and not compress_bf16 and flat.grad.is_cuda:
             from . import ipc as ipcm
             if not ipcm.enabled():
-                self.ipc_reason = "disabled (TTD_IPC_AR=0)"
+                self.ipc_reason = "off (opt-in: TTD_IPC_AR=1)"
             else:
                 same = ipcm.group_same_node(group)
                 paths = ipcm.plan_paths([(e - s) * 4 for s, e in self.buckets], self.world, same)
@@ -123,7 +123,8 @@ class BucketedAllReducer:
                     self.ipc_reason = "group spans several nodes"
                 elif any(p != ipcm.RCCL for p in paths):
                     try:
-                        self.ipc = ipcm.IpcAllReducer(group)
+                        # no more workgroups per launch than RCCL's CTA budget (co-scheduling)
+                        self.ipc = ipcm.IpcAllReducer(group, max_blocks=int(getattr(self.comm, "max_ctas", 0) or 0))
                     except Exception as e:  # noqa: BLE001 - every rank raised together: all use RCCL
                         self.ipc_reason = "%s: %s" % (type(e).__name__, e)
                     if self.ipc is not None:
@@ -191,8 +192,16 @@ class BucketedAllReducer:
         if self.comm is None:
             return
         from . import rccl
+        old = self.comm
         self.comm = rccl.retune(self.group, self.comm, float(overlap_ms),
                                 [(e - s) * (2 if self.compress else 4) for s, e in self.buckets])
+        if self.comm is not old:
+            if self.compress and self.buckets:
+                # the fresh communicator's bf16 staging buffer at its final size before any
+                # step can be graph-captured (as in __init__)
+                self.comm.reserve(max(e - s for s, e in self.buckets))
+            if self.ipc is not None:
+                self.ipc.max_blocks = int(getattr(self.comm, "max_ctas", 0) or 0)
 
     def _make_buckets(self):
         """Greedy buckets on variable boundaries: the first `first_bucket_mb` (communication
@@ -242,7 +251,14 @@ class BucketedAllReducer:
         st["overlap_pct"] = round(100.0 * max(0.0, 1.0 - exposed / st["busy_ms"]), 1) if st["busy_ms"] > 0 else None
         return st
 
+    def check(self):
+        """Raise UnavailableError when a direct-path bucket of a finished call failed (a peer
+        missed a barrier: that bucket holds NaN, not a sum). Reads a host-mapped word: no sync."""
+        if self.ipc is not None:
+            self.ipc.check()
+
     def begin(self):
+        self.check()  # the previous step's direct-path buckets, as far as they have run
         self._next = 0
         self._works = []
         self._keep = []
@@ -346,6 +362,7 @@ class BucketedAllReducer:
                 graphs.join(torch.cuda.current_stream(), self.comm.stream)
             else:
                 self.comm.join()  # the current stream waits for the buckets (no host sync)
+                self.check()
             if self._timed is not None:
                 self._timed[1].record()
             return

@@ -15,8 +15,16 @@ is left to hide it — and records the path of every bucket (`bucket_paths`, in 
 Reference aggregation: /root/reference/distribute_training.py:142-148 (PS accumulators; the
 Mirrored strategies' all-reduce is the north star's, BASELINE.json).
 
-Environment: TTD_IPC_AR=0 disables the path (RCCL for every bucket); TTD_IPC_AR_CAP_MB sets the
-staging buffer size (default 8 MB: the two-shot limit).
+Failure contract: a barrier whose peer does not arrive within the spin bound (TTD_IPC_SPIN polls,
+~1-2 s by default) sets a host-mapped error word and its workgroup writes NaN over its share of
+the bucket instead of a sum; every later call of that engine poisons without waiting. The
+reducer checks the word at its join points (no device sync) and raises UnavailableError, which
+MonitoredTrainingSession turns into a recovery (reference:
+/root/reference/distribute_training.py:209-215). A late peer therefore never yields a wrong sum.
+
+Environment: TTD_IPC_AR=1 enables the path (opt-in: it has run on one GPU with two processes,
+never on several GPUs); TTD_IPC_AR_CAP_MB sets the staging buffer size (default 8 MB: the
+two-shot limit); TTD_IPC_SPIN the barrier poll bound.
 """
 from __future__ import annotations
 
@@ -44,17 +52,19 @@ def _hip():
     lib = _native.hip()
     if not _bound:
         lib.ttdi_create.restype = c_void_p
-        lib.ttdi_create.argtypes = [c_int, c_int, c_int, c_longlong]
+        lib.ttdi_create.argtypes = [c_int, c_int, c_int, c_longlong, c_longlong]
         lib.ttdi_handle.restype = c_int
         lib.ttdi_handle.argtypes = [c_void_p, c_char_p]
         lib.ttdi_open.restype = c_int
         lib.ttdi_open.argtypes = [c_void_p, c_char_p, ctypes.POINTER(c_int)]
         lib.ttdi_allreduce.restype = c_int
-        lib.ttdi_allreduce.argtypes = [c_void_p, c_void_p, c_longlong, c_int, c_int, c_void_p]
+        lib.ttdi_allreduce.argtypes = [c_void_p, c_void_p, c_longlong, c_int, c_int, c_int, c_void_p]
         lib.ttdi_link_local.restype = c_int
         lib.ttdi_link_local.argtypes = [c_void_p, c_void_p]
         lib.ttdi_error.restype = c_int
         lib.ttdi_error.argtypes = [c_void_p]
+        lib.ttdi_clear_error.restype = None
+        lib.ttdi_clear_error.argtypes = [c_void_p]
         lib.ttdi_destroy.restype = None
         lib.ttdi_destroy.argtypes = [c_void_p]
         _bound = True
@@ -72,7 +82,7 @@ def _rt():
     lib.ttd_ipc_part.argtypes = [c_longlong, c_longlong, c_int, c_int, c_int, ctypes.POINTER(c_longlong),
                                  ctypes.POINTER(c_longlong)]
     lib.ttd_ipc_blocks.restype = c_int
-    lib.ttd_ipc_blocks.argtypes = [c_longlong]
+    lib.ttd_ipc_blocks.argtypes = [c_longlong, c_int]
     return lib
 
 
@@ -81,7 +91,12 @@ def default_cap() -> int:
 
 
 def enabled() -> bool:
-    return os.environ.get("TTD_IPC_AR", "1") != "0"
+    return os.environ.get("TTD_IPC_AR", "0") == "1"
+
+
+def default_spin() -> int:
+    """Barrier polls before a peer counts as lost (0: the kernel default, ~1-2 s)."""
+    return int(os.environ.get("TTD_IPC_SPIN", "0"))
 
 
 def choose(nbytes: int, world: int, same_node: bool, cap: Optional[int] = None) -> int:
@@ -102,8 +117,8 @@ def part(lo: int, hi: int, vec: int, nb: int, b: int):
     return a.value, e.value
 
 
-def blocks_for(nbytes: int) -> int:
-    return int(_rt().ttd_ipc_blocks(int(nbytes)))
+def blocks_for(nbytes: int, budget: int = 0) -> int:
+    return int(_rt().ttd_ipc_blocks(int(nbytes), int(budget)))
 
 
 def plan_paths(bucket_bytes: List[int], world: int, same_node: bool, cap: Optional[int] = None,
@@ -133,15 +148,17 @@ class LocalGroup:
     """Every rank of a `world`-rank group as engines of THIS process on one device, peers linked
     by plain pointers (no IPC): tests run the ranks' kernels on separate streams."""
 
-    def __init__(self, world: int, device=None, cap_bytes: Optional[int] = None):
+    def __init__(self, world: int, device=None, cap_bytes: Optional[int] = None, spin: Optional[int] = None,
+                 max_blocks: int = 0):
         lib = _hip()
         self.world = world
+        self.max_blocks = int(max_blocks)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.cap = int(default_cap() if cap_bytes is None else cap_bytes)
         self.h = []
         with torch.cuda.device(self.device):
             for r in range(world):
-                h = lib.ttdi_create(r, world, self.device.index, self.cap)
+                h = lib.ttdi_create(r, world, self.device.index, self.cap, int(default_spin() if spin is None else spin))
                 if not h:
                     self.destroy()
                     raise errors.UnavailableError("ttdi_create failed")
@@ -154,13 +171,17 @@ class LocalGroup:
 
     def all_reduce_(self, r: int, t: torch.Tensor, path: int, stream) -> torch.Tensor:
         rc = _hip().ttdi_allreduce(self.h[r], t.data_ptr(), t.numel(), 0 if t.dtype == torch.float32 else 1,
-                                   int(path), stream.cuda_stream)
+                                   int(path), self.max_blocks, stream.cuda_stream)
         if rc != 0:
             raise errors.InternalError("ipc all-reduce launch failed (hipError %d)" % rc)
         return t
 
     def timed_out(self) -> bool:
         return any(_hip().ttdi_error(h) != 0 for h in self.h)
+
+    def clear_error(self):
+        for h in self.h:
+            _hip().ttdi_clear_error(h)
 
     def destroy(self):
         for h in self.h:
@@ -172,15 +193,20 @@ class IpcAllReducer:
     """The staging buffers and peer mappings of one group; `all_reduce_(t, path, stream)` runs
     one bucket. Collective construction: every rank of `group` must create it together."""
 
-    def __init__(self, group=None, device=None, cap_bytes: Optional[int] = None):
+    def __init__(self, group=None, device=None, cap_bytes: Optional[int] = None, spin: Optional[int] = None,
+                 max_blocks: int = 0):
+        """max_blocks: workgroups per launch at most (the collectives' CTA budget; 0: no cap
+        beyond ipc_plan.h's 64). spin: barrier polls before a peer counts as lost."""
         lib = _hip()
         self.group = group
+        self.max_blocks = int(max_blocks)
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.cap = int(default_cap() if cap_bytes is None else cap_bytes)
         with torch.cuda.device(self.device):
-            h = lib.ttdi_create(self.rank, self.world, self.device.index, self.cap)
+            h = lib.ttdi_create(self.rank, self.world, self.device.index, self.cap,
+                                int(default_spin() if spin is None else spin))
         self._h = h
         # every rank learns whether any rank failed, so all of them raise together
         ok = self._all_ok(bool(h))
@@ -220,7 +246,7 @@ class IpcAllReducer:
             raise ValueError("ipc all-reduce wants a contiguous fp32 / bf16 tensor")
         s = stream if stream is not None else torch.cuda.current_stream()
         rc = _hip().ttdi_allreduce(self._h, t.data_ptr(), t.numel(), 0 if t.dtype == torch.float32 else 1, int(path),
-                                   s.cuda_stream)
+                                   self.max_blocks, s.cuda_stream)
         if rc != 0:
             raise errors.InternalError("ipc all-reduce launch failed (hipError %d)" % rc)
         return t
@@ -233,8 +259,20 @@ class IpcAllReducer:
                 and t.dtype in (torch.float32, torch.bfloat16))
 
     def timed_out(self) -> bool:
-        """Whether a barrier of some call timed out (a peer never arrived). Synchronizes."""
-        return _hip().ttdi_error(self._h) != 0
+        """Whether a barrier of some call that has run so far timed out (a peer never arrived):
+        a host-mapped word, read without synchronising (calls still queued are not covered)."""
+        return bool(self._h) and _hip().ttdi_error(self._h) != 0
+
+    def check(self):
+        """Raise UnavailableError when a call has failed (its bucket holds NaN, not a sum)."""
+        if self.timed_out():
+            raise errors.UnavailableError(
+                "direct xGMI all-reduce: a peer did not reach a barrier within the spin bound (lost or "
+                "stalled rank); the affected gradient bucket was poisoned with NaN, not summed")
+
+    def clear_error(self):
+        if self._h:
+            _hip().ttdi_clear_error(self._h)
 
     def destroy(self):
         h, self._h = getattr(self, "_h", None), None

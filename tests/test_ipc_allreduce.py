@@ -9,7 +9,11 @@ sum, on one GPU:
   waits behind a spinning one until the barrier's bounded spin gives up — measured with 3.);
 * 2 processes on the same GPU through real IPC handles (hipIpcGetMemHandle / OpenMemHandle over
   a gloo rendezvous on 127.0.0.1), eager and replayed from a captured hipGraph (the epoch lives
-  in device memory, so replays see fresh barrier epochs).
+  in device memory, so replays see fresh barrier epochs);
+* the failure contract: a rank that skips a call (lost / stalled peer) makes the other rank's
+  barrier time out; the bucket then holds NaN, never a partial or stale sum, the host-mapped
+  error word surfaces as UnavailableError at the next check (no device sync), later calls of
+  the dead engine poison without waiting, and the skipping rank's next call fails too.
 Multi-GPU runs use the same kernels with peers on other devices (xGMI)."""
 import os
 
@@ -151,3 +155,133 @@ def test_two_processes_one_gpu_ipc():
         for k, v in res.items():
             if k != "timed_out":
                 assert v < 1e-6, (rank, k, v)
+
+
+SPIN = 1 << 14  # barrier polls before a peer counts as lost: ~ms instead of the default ~1-2 s
+
+
+@pytest.mark.parametrize("path", ["one", "two"])
+def test_local_group_missing_peer_poisons_not_sums(path):
+    from tensorflow_train_distributed_amd.parallel import ipc
+    p = ipc.ONE_SHOT if path == "one" else ipc.TWO_SHOT
+    grp = ipc.LocalGroup(2, device="cuda:0", cap_bytes=8 * MB, spin=SPIN)
+    streams = _streams(2)
+    try:
+        n = (256 * 1024 if path == "one" else 3 * MB) // 4
+        x = torch.ones(n, device="cuda")
+        torch.cuda.synchronize()
+        grp.all_reduce_(0, x, p, streams[0])  # rank 1 never calls
+        torch.cuda.synchronize()
+        assert grp.timed_out()
+        assert bool(torch.isnan(x).all()), "a rank whose peer is missing must not return a sum"
+        # the engine is dead: the next call poisons at once (no spin on the rank that failed)
+        y = torch.ones(n, device="cuda")
+        grp.all_reduce_(0, y, p, streams[0])
+        torch.cuda.synchronize()
+        assert bool(torch.isnan(y).all())
+        grp.clear_error()
+        assert not grp.timed_out()
+    finally:
+        grp.destroy()
+
+
+def test_limited_blocks_sum_exact():
+    """max_blocks (the collectives' CTA budget) caps the launch; the sum stays exact."""
+    from tensorflow_train_distributed_amd.parallel import ipc
+    grp = ipc.LocalGroup(2, device="cuda:0", cap_bytes=8 * MB, max_blocks=4)
+    streams = _streams(2)
+    try:
+        for p, nbytes in [(ipc.ONE_SHOT, MB), (ipc.TWO_SHOT, 6 * MB)]:
+            xs = _inputs(2, nbytes // 4, torch.float32, nbytes)
+            dev = [x.cuda() for x in xs]
+            torch.cuda.synchronize()
+            for r in range(2):
+                grp.all_reduce_(r, dev[r], p, streams[r])
+            torch.cuda.synchronize()
+            assert not grp.timed_out()
+            want = xs[0] + xs[1]
+            for r in range(2):
+                assert torch.equal(dev[r].cpu(), want)
+    finally:
+        grp.destroy()
+
+
+def _skip_worker(rank, world, port, q):
+    try:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from tensorflow_train_distributed_amd.parallel import ipc
+        from tensorflow_train_distributed_amd.utils import errors
+        r = ipc.IpcAllReducer(device="cuda:0", cap_bytes=8 * MB, spin=SPIN)
+        res = {}
+        n = 512 * 1024 // 4
+        # step 1: both ranks, exact
+        x = torch.full((n,), float(rank + 1), device="cuda")
+        r.all_reduce_(x, ipc.ONE_SHOT)
+        torch.cuda.synchronize()
+        res["step1_exact"] = bool((x == 3.0).all())
+        r.check()
+        dist.barrier()
+        # step 2: rank 1 skips its call (a stalled / lost peer)
+        x = torch.full((n,), float(rank + 1), device="cuda")
+        if rank == 0:
+            r.all_reduce_(x, ipc.ONE_SHOT)
+        torch.cuda.synchronize()
+        res["step2_nan"] = bool(torch.isnan(x).all()) if rank == 0 else None
+        try:
+            r.check()
+            res["step2_raised"] = False
+        except errors.UnavailableError:
+            res["step2_raised"] = True
+        dist.barrier()
+        # step 3: both call again; rank 0's engine is dead (publishes nothing), so rank 1's
+        # barrier times out too: the failure reaches the rank that skipped within one step
+        x = torch.full((n,), float(rank + 1), device="cuda")
+        r.all_reduce_(x, ipc.ONE_SHOT)
+        torch.cuda.synchronize()
+        res["step3_nan"] = bool(torch.isnan(x).all())
+        try:
+            r.check()
+            res["step3_raised"] = False
+        except errors.UnavailableError:
+            res["step3_raised"] = True
+        dist.barrier()
+        r.destroy()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:  # noqa: BLE001 - reported to the test
+        q.put((rank, "%s: %s" % (type(e).__name__, e)))
+
+
+def test_two_processes_skipped_call_surfaces_error():
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_skip_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(2):
+            rank, res = q.get(timeout=100)
+            out[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(2):
+        assert isinstance(out[rank], dict), out[rank]
+        assert out[rank]["step1_exact"]
+    assert out[0]["step2_nan"] and out[0]["step2_raised"], out[0]
+    assert not out[1]["step2_raised"], out[1]
+    # no wrong sum is ever consumed: each rank's step-3 bucket is NaN and its check raises
+    for rank in range(2):
+        assert out[rank]["step3_nan"] and out[rank]["step3_raised"], (rank, out[rank])

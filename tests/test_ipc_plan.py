@@ -121,3 +121,41 @@ def test_reducer_bucket_paths_on_torch_backend():
             is_cuda = False
     r = BucketedAllReducer(_Flat(), first_bucket_mb=0.001, bucket_mb=0.01)
     assert r.bucket_paths == ["none"] * len(r.buckets)
+
+
+def test_blocks_for_respects_cta_budget():
+    # ~16 KB per workgroup, 8 .. 64, and never above the collectives' CTA budget
+    assert ipc.blocks_for(4096) == 8
+    assert ipc.blocks_for(MB) == 64
+    assert ipc.blocks_for(8 * MB) == 64
+    for budget in (1, 4, 8, 16):
+        for nbytes in (4096, 256 * 1024, MB, 8 * MB):
+            assert ipc.blocks_for(nbytes, budget) == min(budget, ipc.blocks_for(nbytes))
+
+
+def test_direct_path_is_opt_in(monkeypatch):
+    monkeypatch.delenv("TTD_IPC_AR", raising=False)
+    assert not ipc.enabled()
+    monkeypatch.setenv("TTD_IPC_AR", "1")
+    assert ipc.enabled()
+
+
+def test_reducer_raises_when_direct_path_failed():
+    """begin() / finish() surface the direct path's error word as UnavailableError (the
+    session's recovery trigger) without a device sync."""
+    from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer
+    from tensorflow_train_distributed_amd.utils import errors
+
+    class FakeIpc:
+        failed = False
+
+        def check(self):
+            if self.failed:
+                raise errors.UnavailableError("peer lost")
+
+    r = BucketedAllReducer.__new__(BucketedAllReducer)
+    r.ipc = FakeIpc()
+    r.begin()  # healthy: no raise
+    r.ipc.failed = True
+    with pytest.raises(errors.UnavailableError):
+        r.begin()
