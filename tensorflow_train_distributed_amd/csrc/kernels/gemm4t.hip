@@ -23,6 +23,12 @@
 //  * split-K without a fold pass: every split stores its fp32 partial tile lane-linear (1 KB per
 //    store instruction), the LAST split of a tile to arrive (per-tile counter) sums the tile's
 //    partials in split order (deterministic) and writes dW (+= with beta);
+//  * GB: B read as the im2col of a convolution input x [N][H][W][C] (the weight gradient of a
+//    strided / 3x3 conv: k-row = output pixel, column = filter tap (r, s, c)): each lane's 16-B
+//    DMA chunk has its own source offset per k-row, formed for K-tile kt + 2 between the MFMAs
+//    of K-tile kt (pixel -> (n, p, q) by multiply-high divisions, tap validity against the
+//    padding); a tap in the padding gets an offset past the buffer's end, which the buffer load
+//    returns as zeros — no branch, no zero fill;
 //  * RS: the bias gradient rowsum(A^T) = column sums of dY from the A fragments already in
 //    registers, as an MFMA against a ones operand (D = 1 . A): 4 extra MFMAs per K-step and wave
 //    on 1 / tiles_n of the K-tiles (spread over the tile columns); the last workgroup of a tile
@@ -103,6 +109,34 @@ struct LoadMN {
   }
 };
 
+// im2col geometry of a gathered B operand: conv input x [N][H][W][C], k-row = output pixel
+// (n, p, q) of a P x Q map, column = (r, s, c) of an R x S filter. Divisions by P*Q and Q are
+// multiply-high + shift (magic numbers from the host, exact for k < 2^31).
+struct Gather {
+  int H, W, C, Q, PQ, S, sh, sw, ph, pw;
+  unsigned pq_m, q_m;
+  int pq_s, q_s;
+};
+
+constexpr uint32_t kOob = 0x80000000u;  // past the end of every gathered buffer (< 2 GiB): reads 0
+
+// per-lane column decode of a gathered operand (once per kernel): tap (r, s) and the element
+// offset of (r, s, c) relative to the pixel's (h0, w0) corner
+struct GCol {
+  int r[2], s[2], toff[2];
+};
+
+__device__ __forceinline__ uint32_t gather_voff(const Gather& G, const GCol& gc, int j, int k) {
+  const int n = static_cast<int>(__umulhi(static_cast<unsigned>(k), G.pq_m) >> G.pq_s);
+  const int rem = k - n * G.PQ;
+  const int p = static_cast<int>(__umulhi(static_cast<unsigned>(rem), G.q_m) >> G.q_s);
+  const int q = rem - p * G.Q;
+  const int hb = p * G.sh - G.ph, wb = q * G.sw - G.pw;
+  const bool ok = static_cast<unsigned>(hb + gc.r[j]) < static_cast<unsigned>(G.H) &&
+                  static_cast<unsigned>(wb + gc.s[j]) < static_cast<unsigned>(G.W);
+  return ok ? static_cast<uint32_t>((((n * G.H + hb) * G.W + wb) * G.C + gc.toff[j]) * 2) : kOob;
+}
+
 __device__ __forceinline__ ttd_s16x4_t trd(const lds_char_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)p);
 }
@@ -149,13 +183,13 @@ __device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int gro
 constexpr bool fr_is_a(int r) { return r == 0 || r >= 9; }
 constexpr int fr_blk(int r) { return r == 0 ? 0 : (r <= 8 ? r - 1 : r - 8); }
 
-template <bool RS>
+template <bool RS, bool GB>
 __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, int M, int N, int K,
                                                      int tiles_m, int tiles_n, int splits, int kt_per,
                                                      float* __restrict__ ws, float* __restrict__ out, int beta,
                                                      float alpha, int* __restrict__ ctr, float* __restrict__ rsw,
-                                                     float* __restrict__ rowsum) {
+                                                     float* __restrict__ rowsum, Gather G, long long b_bytes) {
   // 1 KB aligned: the read bases' bits 5..9 are the lane's own, so a column block is one XOR
   __shared__ __attribute__((aligned(1024))) char smem[SMEM + 16];
   // the epilogue's arguments into SGPRs now: loaded lazily behind the main loop's first K-tile,
@@ -188,7 +222,27 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
   LoadMN la, lb;
   la.init(A, lda, K, M, m0, tid);
-  lb.init(B, ldb, K, N, n0, tid);
+  GCol gc;
+  uint32_t gv[8];  // GB: this lane's source offsets of the 8 B pieces of the next K-tile to load
+  if constexpr (GB) {
+    lb.srd = make_srd(B, static_cast<uint32_t>(b_bytes));
+    const int pc = tid & 31;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int f = ((tid >> 5) & 3) | (j << 2);
+      const int col = min(n0 + (((pc >> 1) ^ f) << 4) + (pc & 1) * 8, N - 8);
+      const int tap = col / G.C, c = col - tap * G.C;
+      gc.r[j] = tap / G.S;
+      gc.s[j] = tap - gc.r[j] * G.S;
+      gc.toff[j] = (gc.r[j] * G.W + gc.s[j]) * G.C + c;
+    }
+  } else {
+    lb.init(B, ldb, K, N, n0, tid);
+  }
+  // GB: offsets of K-tile kt's 8 B pieces (piece i: k-row i * 8 + tid / 32)
+  auto gather_piece = [&](int kt, int i) {
+    if constexpr (GB) gv[i] = gather_voff(G, gc, i & 1, (kt0 + kt) * 64 + i * 8 + (tid >> 5));
+  };
   const int kstride_a = static_cast<int>(lda * 128), kstride_b = static_cast<int>(ldb * 128);  // bytes per K-tile
 
   f32x4_t acc[8][8];
@@ -220,9 +274,13 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   };
   auto dma1 = [&](auto Q, int st, int kt) {  // piece q of K-tile kt into stage st (M0 = its base)
     constexpr int qq = decltype(Q)::value, i = qq & 7;
-    const LoadMN& L = qq < 8 ? la : lb;
-    dma_chain(L.voff[i & 1], L.srd, (kt0 + kt) * (qq < 8 ? kstride_a : kstride_b) + i * L.row8,
-              qq < 15 ? m0_of(qq + 1, st) : m0_of(0, st ^ 1));
+    const uint32_t next = qq < 15 ? m0_of(qq + 1, st) : m0_of(0, st ^ 1);
+    if constexpr (GB && qq >= 8) {
+      dma_chain(gv[i], lb.srd, 0, next);
+    } else {
+      const LoadMN& L = qq < 8 ? la : lb;
+      dma_chain(L.voff[i & 1], L.srd, (kt0 + kt) * (qq < 8 ? kstride_a : kstride_b) + i * L.row8, next);
+    }
   };
   auto fa = [&](int set, int a) { return cat(fl[set][a], fh[set][a]); };
   auto fb = [&](int set, int b) { return cat(fl[set][8 + b], fh[set][8 + b]); };
@@ -239,6 +297,8 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
       constexpr int i = decltype(I)::value;
       if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, std::integral_constant<int, 1>{}, st, std::integral_constant<int, 1>{});
       mfma_acc<FIRST>(acc[i / 8][i % 8], fa(0, i / 8), fb(0, i % 8));
+      // GB: the gathered B offsets of K-tile kt + 2 (DMA'd in phase 1b), between the MFMAs
+      if constexpr (GB && has2 && i % 8 == 5) gather_piece(kt + 2, i / 8);
     });
     if constexpr (RS) {
       if (rs_on) {  // (wave-uniform branches: no VALU-selected operand)
@@ -294,7 +354,12 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
 
   // prologue: K-tiles 0 and 1 into stages 0 and 1, K-step 0 fragments of K-tile 0
   m0_init(m0_of(0, 0));
+  if constexpr (GB)
+    for (int i = 0; i < 8; ++i) gather_piece(0, i);
   static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
+  if constexpr (GB)
+    if (nk > 1)
+      for (int i = 0; i < 8; ++i) gather_piece(1, i);
   static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
@@ -393,12 +458,28 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   // just wrote (deterministic whoever is last; no accumulator stays live through the fold)
   const float* src0 = ws + static_cast<long long>(t) * SLAB + lin;
   const long long sstride = static_cast<long long>(tiles) * SLAB;
-#pragma unroll
+  // (one workgroup streams splits x 256 KB: the loads of 4 splits are issued before their adds —
+  // 32 x 16 B in flight per lane instead of 8 — the adds stay in split order)
+#pragma unroll 1
   for (int a = 0; a < 8; ++a) {
     f32x4_t v[8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) v[b] = *reinterpret_cast<const f32x4_t*>(src0 + (a * 8 + b) * 256);
-    for (int s = 1; s < splits; ++s) {
+    int s = 1;
+    for (; s + 4 <= splits; s += 4) {
+      f32x4_t x[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* src = src0 + (s + u) * sstride + a * 8 * 256;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) x[u][b] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(src + b * 256));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) v[b] += x[u][b];
+    }
+    for (; s < splits; ++s) {
       const float* src = src0 + s * sstride + a * 8 * 256;
 #pragma unroll
       for (int b = 0; b < 8; ++b) v[b] += *reinterpret_cast<const f32x4_t*>(src + b * 256);
@@ -460,11 +541,77 @@ TTDK_EXPORT int ttdk_gemm4t_wgrad(const bf16_t* A, long long lda, const bf16_t* 
   }
   float* rsw = rowsum ? ws + static_cast<long long>(splits) * tiles * g4t::SLAB : nullptr;
   const dim3 grid(tiles * splits);
+  const g4t::Gather G{};
   if (rowsum)
-    hipLaunchKernelGGL((g4t::gemm4t_kernel<true>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
-                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum);
+    hipLaunchKernelGGL((g4t::gemm4t_kernel<true, false>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
+                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum, G, 0LL);
   else
-    hipLaunchKernelGGL((g4t::gemm4t_kernel<false>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
-                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum);
+    hipLaunchKernelGGL((g4t::gemm4t_kernel<false, false>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
+                       tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum, G, 0LL);
+  return hipGetLastError();
+}
+
+namespace {
+// multiply-high magic for q = n / d, exact for 0 <= n < 2^31 (d >= 2): s = ceil(log2 d) - 1,
+// m = floor(2^(32 + s) / d) + 1 (< 2^32); error (m d - 2^(32+s)) n / (d 2^(32+s)) < 1 / d
+void magic_div(unsigned d, unsigned* m, int* s) {
+  int l = 0;
+  while ((1u << l) < d) ++l;
+  *s = l > 0 ? l - 1 : 0;
+  *m = static_cast<unsigned>(((static_cast<unsigned __int128>(1) << (32 + *s)) / d) + 1);
+}
+}  // namespace
+
+// floats of workspace ttdk_conv_wgrad4t needs (-1: the kernel does not take the conv)
+TTDK_EXPORT long long ttdk_conv_wgrad4t_ws(const TtdkConv* g, int splits) {
+  const int M = g->K, N = g->R * g->S * g->C;
+  const long long K = static_cast<long long>(g->N) * g->P * g->Q;
+  const long long xb = static_cast<long long>(g->N) * g->H * g->W * g->C * 2, yb = K * g->K * 2;
+  if (g->C % 8 || g->K % 8 || K % 64 || K < 128 || g->dh != 1 || g->dw != 1 || xb >= (1LL << 31) ||
+      yb >= (1LL << 31) || g->P * g->Q < 2 || g->Q < 2)
+    return -1;
+  return ttdk_gemm4t_ws(M, N, static_cast<int>(K), splits);
+}
+
+// Convolution weight gradient dw[K][R][S][C] (+)= sum over pixels of dy (x) im2col(x) on the 4-wave
+// transposed-read kernel: A = dy [pixels][K] (MN-major), B = x read through the im2col gather
+// (dense [pixels][C] for unit-stride 1x1 convs); split-K summed inside the launch (no fold pass).
+// ws: ttdk_conv_wgrad4t_ws floats. hipErrorInvalidValue: the kernel does not take the conv.
+TTDK_EXPORT int ttdk_conv_wgrad4t(const bf16_t* x, const bf16_t* dy, const TtdkConv* g, float* dw, float* ws,
+                                  int splits, int beta, hipStream_t st) {
+  using namespace ttdk;
+  if (ttdk_conv_wgrad4t_ws(g, splits) < 0 || !g4t_enabled()) return hipErrorInvalidValue;
+  if (is_pointwise(g))
+    return ttdk_gemm4t_wgrad(dy, g->K, x, g->C, g->K, g->C, g->N * g->P * g->Q, splits, ws, dw, beta, 1.f, nullptr, st);
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!al16(x) || !al16(dy) || !al16(dw) || !ws) return hipErrorInvalidValue;
+  const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
+  const int ktiles = K / 64;
+  splits = std::max(1, std::min(splits, ktiles / 2));
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
+  int* ctr = nullptr;
+  if (splits > 1) {
+    ctr = big::tile_counters(st, tiles);
+    if (!ctr) return hipErrorInvalidValue;
+  }
+  g4t::Gather G{};
+  G.H = g->H;
+  G.W = g->W;
+  G.C = g->C;
+  G.Q = g->Q;
+  G.PQ = g->P * g->Q;
+  G.S = g->S;
+  G.sh = g->sh;
+  G.sw = g->sw;
+  G.ph = g->ph;
+  G.pw = g->pw;
+  magic_div(static_cast<unsigned>(G.PQ), &G.pq_m, &G.pq_s);
+  magic_div(static_cast<unsigned>(G.Q), &G.q_m, &G.q_s);
+  const long long xb = static_cast<long long>(g->N) * g->H * g->W * g->C * 2;
+  hipLaunchKernelGGL((g4t::gemm4t_kernel<false, true>), dim3(tiles * splits), dim3(g4t::T), 0, st, dy,
+                     static_cast<long long>(g->K), x, 0LL, M, N, K, tiles_m, tiles_n, splits, per, ws, dw, beta, 1.f,
+                     ctr, nullptr, nullptr, G, xb);
   return hipGetLastError();
 }

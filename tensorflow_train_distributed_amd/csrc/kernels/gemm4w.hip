@@ -260,6 +260,8 @@ __device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int gro
   tn = r / gm;
 }
 
+// SCHED 2: the production one-tile-per-workgroup loop (hand-ordered inline asm); SCHED 0: the
+// same schedule left to the compiler, kept as the A/B oracle of the hand ordering
 template <int EK, int SCHED>
 __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
@@ -367,13 +369,14 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   };
   for (int kt = 0; kt < ktiles; ++kt) ktile(kt, F{});
   } else {
-  // SCHED 1: the whole main loop as inline asm in a fixed issue order (hipcc grouped all 16
+  // SCHED 2: the whole main loop as inline asm in a fixed issue order (hipcc grouped all 16
   // fragment reads and all 16 DMA pieces of a phase in front of its MFMAs; with one wave per
   // SIMD nothing else fills the MFMA pipe while they issue):
   //   phase 0: one fragment read before every 4th MFMA, graduated lgkmcnt for the K-step-0
   //            fragments still in flight (lgk0);
-  //   phase 1a: one DMA piece before every 2nd MFMA; phase 1b: one fragment read before every
-  //            2nd MFMA. LDS reads and DMA are counted by hand (hipcc does not count asm).
+  //   phase 1a: one DMA piece before every 4th MFMA; phase 1b: one DMA piece before every 4th
+  //            and one fragment read before every 2nd MFMA. LDS reads and DMA are counted by
+  //            hand (hipcc does not count asm).
   const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
   uint32_t va[2][2], vb[2][2];  // [stage][K-step] fragment base addresses (block offsets immediate)
 #pragma unroll
@@ -392,8 +395,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(xb[rd_blk(r)]) : "v"(b_base), "i"(rd_blk(r) * 2048));
   };
   // DMA piece q (0..7 A, 8..15 B) of K-tile kt into stage st, M0 = its LDS base (chained: every
-  // piece sets M0 for its successor; the issue order is stage st 0..15, stage st ^ 1 0..15, ...
-  // — SCHED 1 / 3 issue A and B of a K-tile in the same 0..15 order)
+  // piece sets M0 for its successor; the issue order is stage st 0..15, stage st ^ 1 0..15, ...)
   auto m0_of = [&](int q, int st) {
     return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
         static_cast<int>(ldsw + st * STAGE + (q < 8 ? 0 : OPB) + (q & 7) * 4096)));
@@ -429,34 +431,20 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
         asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(lgk0(i)) : "memory");
       mfma1(a, b, fa[0][a], fb[0][b], first);
     });
-    if constexpr (SCHED == 3) {
-      // one barrier per K-tile: this stage is free AND K-tile kt + 1 has landed; then the 16
-      // DMA pieces of kt + 2 and the 16 K-step-0 reads of kt + 1 alternate, one every 2 MFMAs
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      static_for<64>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        if constexpr (i % 4 == 0)
-          if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
-        if constexpr (i % 4 == 2)
-          rd1(std::integral_constant<int, i / 4>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
-        mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
-      });
-    } else {
+    {
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       // phase 1a: K-tile kt + 2 into this stage (the MFMA sequence is never duplicated per
       // branch: with the MFMAs inside if / else copies hipcc allocated the accumulators
       // differently per copy and shuffled them with unpadded v_accvgpr_mov between).
-      // SCHED 1: all 16 pieces in the first 32 MFMAs; SCHED 2: 8 here, 8 in phase 1b.
-      constexpr int DSTEP = SCHED == 1 ? 2 : 4;
+      // 8 pieces here, 8 in phase 1b (all 16 in the first 32 MFMAs measured slower).
       static_for<32>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        if constexpr (i % DSTEP == 0)
-          if constexpr (has2) dma1(std::integral_constant<int, i / DSTEP>{}, st, kt + 2);
+        if constexpr (i % 4 == 0)
+          if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
         mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
       });
       if constexpr (has2) {
-        if constexpr (SCHED == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -465,7 +453,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
       // K-tile they are never used)
       static_for<32>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        if constexpr (SCHED != 1 && i % 4 == 1)
+        if constexpr (i % 4 == 1)
           if constexpr (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
         if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
         mfma1(4 + i / 8, i % 8, fa[1][4 + i / 8], fb[1][i % 8], F{});
@@ -487,19 +475,6 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   if (m0 + BM <= M && n0 + BN <= N) epilogue<EK, false>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
   else epilogue<EK, true>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
 }
-
-// 32x32x16 MFMA with an AGPR accumulator, and the VGPR-staged loader pieces of gemm4v
-__device__ __forceinline__ void mfma32(f32x16_t& c, const bf16x8_t& x, const bf16x8_t& y) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(y), "v"(x));
-}
-
-__device__ __forceinline__ void ds_w128(uint32_t a, const ttd_i32x4_t& v) {
-  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void buf_ld16(ttd_i32x4_t& d, uint32_t voff, const ttd_i32x4_t& srd, int soff) {
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(srd), "s"(soff));
-}
-
 
 // ============================================================================================
 // gemm4p: the production form — persistent 4-wave 256 x 256 kernel on the SCHED 2 main loop
@@ -528,17 +503,7 @@ __device__ __forceinline__ void ds_rd(bf16x8_t& d, uint32_t base) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(OFF));
 }
 
-// STAMP (diagnostic build, TTD_G4_SCHED=31): s_memtime around the tile phases, per-wave sums
-// written to g_stamps[block][wave][4] = (tile start -> K-tile 0 landed, main loop, epilogue, tiles)
-__device__ unsigned long long g_stamps[2048 * 4 * 4];
-
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-
-template <int EK, bool STAMP = false>
+template <int EK>
 __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
                                                      int N, int K, int tiles_m, int tiles_n, int group,
@@ -655,9 +620,7 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
   int prev = 0;  // what the previous tile left in the VMEM queue after this tile's DMA: 0 none,
                  // 1 an unchecked epilogue's EPI_ST stores, 2 a data-dependent count
   const float alpha = epi_alpha(E);
-  unsigned long long st_land = 0, st_loop = 0, st_epi = 0, st_n = 0, tA = 0, tB = 0;
   for (;;) {
-    if constexpr (STAMP) tA = stamp();
     // Tile queue (tq: 8 per-XCD counters + a finished-workgroup count): after its static first
     // tile a workgroup claims the next unclaimed tile of its XCD's range. In the two-stream
     // BERT step the side stream's weight gradients hold up to 192 CUs for hundreds of us, so
@@ -676,10 +639,6 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     asm volatile("s_barrier" ::: "memory");
-    if constexpr (STAMP) {
-      tB = stamp();
-      st_land += tB - tA;
-    }
     static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
     if (ktiles >= 3) {
       ktile(0, std::true_type{}, std::true_type{});
@@ -693,10 +652,6 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
     if (tq && tid == 0) *reinterpret_cast<int*>(smem + SMEM) = claim;
     // every wave past its last LDS read before the stages are refilled
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (STAMP) {
-      tA = stamp();
-      st_loop += tA - tB;
-    }
     const int nidx = tq ? G8 + __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + SMEM)) : idx + G8;
     const bool more = nidx < xcnt;
     int nm0 = 0, nn0 = 0;
@@ -710,10 +665,6 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
     const bool whole = m0 + BM <= M && n0 + BN <= N;
     if (whole) epilogue<EK, false>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
     else epilogue<EK, true>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
-    if constexpr (STAMP) {
-      st_epi += stamp() - tA;
-      st_n += 1;
-    }
     if (!more) break;
     if (EPI_LOADS) {
       prologue(nm0, nn0);
@@ -733,247 +684,6 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
       for (int i = 0; i < 9; ++i) tq[i] = 0;
     }
   }
-  if constexpr (STAMP) {
-    if (lane == 0 && blockIdx.x < 2048) {
-      unsigned long long* o = g_stamps + (blockIdx.x * 4 + wave) * 4;
-      o[0] = st_land;
-      o[1] = st_loop;
-      o[2] = st_epi;
-      o[3] = st_n;
-    }
-  }
-}
-
-// ============================================================================================
-// gemm4v: the production form. Same 256 x 256 tile, 4 waves, AGPR accumulators, but
-//  * v_mfma_f32_32x32x16_bf16 (4 x 4 tiles of 32 x 32 per wave): 32-cycle MFMA gaps leave ~24
-//    issue cycles each for the loads / LDS traffic of a one-wave-per-SIMD loop;
-//  * operands staged global -> VGPRs (buffer_load_dwordx4, two register sets) -> LDS
-//    (ds_write_b128) instead of LDS-DMA: measured on the diagnostic loop, 16 DMA pieces next to
-//    32 fragment reads per K-tile cost 25 % of the MFMA rate, loads + writes ~7 %;
-//  * per K-tile (4 K-steps of 16 MFMAs): each K-step opens with a burst of the next K-step's 8
-//    fragment reads (bursts measured faster than reads spread one per MFMA gap); K-tile kt + 2's
-//    loads go out in K-steps 0-1, K-tile kt + 1's registers are written to the other LDS stage
-//    in K-step 2, one barrier, then K-step 3 reads K-tile kt + 1's first fragments.
-// K-tiles per launch must be even (the loop body is two K-tiles: static register-set indices).
-
-template <class OFF>
-__device__ __forceinline__ void ld_frag(bf16x8_t& d, uint32_t base, OFF) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(OFF::value));
-}
-
-template <int EK, bool CHECK>
-__device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[4][4], const EpiParams& E, int m0, int n0, int M,
-                                           int N, float alpha, int lane, int wm, int wn) {
-  // acc[a][b][r] = C[m0 + wm*128 + a*32 + (lane & 31)][n0 + wn*128 + b*32 + 4h + 8(r >> 2) + (r & 3)], h = lane >> 5.
-  // Column groups j = r >> 2 (4 columns each): lanes h = 0 / 1 swap groups (1 <-> 0) and (3 <-> 2)
-  // through v_permlane32_swap so each lane stores 8 consecutive columns (16 B) twice per block.
-  const int r32 = lane & 31, h = lane >> 5;
-  bf16_t* const out = static_cast<bf16_t*>(E.out);
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int m = m0 + wm * 128 + a * 32 + r32;
-    const bool mok = !CHECK || m < M;
-    const long long row = static_cast<long long>(m) * E.ldo;
-    const long long rrow = static_cast<long long>(m) * E.ldr;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int nb = n0 + wn * 128 + b * 32 + 4 * h;
-      uint32_t po[4][2], pa[4][2];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = nb + 8 * j;
-        const bool ok = mok && (!CHECK || n < N);
-        f32x4_t v = {acc[a][b][4 * j], acc[a][b][4 * j + 1], acc[a][b][4 * j + 2], acc[a][b][4 * j + 3]};
-        v *= alpha;
-        if constexpr ((EK & kEkBias) != 0)
-          if (!CHECK || n < N) v += *reinterpret_cast<const f32x4_t*>(E.bias + n);
-        if constexpr ((EK & kEkDGelu) != 0) {
-          uint2 rv = make_uint2(0, 0);
-          if (ok) rv = *reinterpret_cast<const uint2*>(E.residual + rrow + n);
-          v[0] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.x & 0xffff)));
-          v[1] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.x >> 16)));
-          v[2] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.y & 0xffff)));
-          v[3] *= gelu_tanh_grad(bf2f(static_cast<bf16_t>(rv.y >> 16)));
-        }
-        if constexpr ((EK & kEkBeta) != 0) {
-          uint2 ov = make_uint2(0, 0);
-          if (ok) ov = *reinterpret_cast<const uint2*>(out + row + n);
-          v[0] += bf2f(static_cast<bf16_t>(ov.x & 0xffff));
-          v[1] += bf2f(static_cast<bf16_t>(ov.x >> 16));
-          v[2] += bf2f(static_cast<bf16_t>(ov.y & 0xffff));
-          v[3] += bf2f(static_cast<bf16_t>(ov.y >> 16));
-        }
-        if constexpr ((EK & kEkAux) != 0) {
-          pa[j][0] = pack_bf16x2(v[0], v[1]);
-          pa[j][1] = pack_bf16x2(v[2], v[3]);
-        }
-        if constexpr ((EK & kEkGelu) != 0) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = gelu_tanh(v[q]);
-        }
-        po[j][0] = pack_bf16x2(v[0], v[1]);
-        po[j][1] = pack_bf16x2(v[2], v[3]);
-      }
-      // (X, Y) = groups (2i, 2i + 1): after the swap lane h = 0 holds columns 16i + 0..7 (its X and
-      // h = 1's X), lane h = 1 columns 16i + 8..15 (h = 0's Y and its Y)
-      auto store2 = [&](uint32_t (&p)[4][2], bf16_t* base) {
-#pragma unroll
-        for (int i2 = 0; i2 < 2; ++i2) {
-          uint32_t x0 = p[2 * i2][0], x1 = p[2 * i2][1], y0 = p[2 * i2 + 1][0], y1 = p[2 * i2 + 1][1];
-          const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
-          const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-          x0 = s0[0]; y0 = s0[1]; x1 = s1[0]; y1 = s1[1];
-          const int n = n0 + wn * 128 + b * 32 + 16 * i2 + 8 * h;
-          if (mok && (!CHECK || n < N))
-            *reinterpret_cast<uint4*>(base + row + n) = make_uint4(x0, x1, y0, y1);
-        }
-      };
-      store2(po, out);
-      if constexpr ((EK & kEkAux) != 0) store2(pa, E.aux);
-    }
-  }
-}
-
-__device__ __forceinline__ void vload16(ttd_i32x4_t& d, uint32_t voff, const ttd_i32x4_t& srd, int soff) {
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(srd), "s"(soff));
-}
-template <int OFF>
-__device__ __forceinline__ void vstore_lds(uint32_t a, const ttd_i32x4_t& v) {
-  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(OFF) : "memory");
-}
-
-template <int EK>
-__global__ __launch_bounds__(T, 1) void gemm4v_kernel(const bf16_t* __restrict__ A, long long lda,
-                                                     const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
-                                                     int N, int K, int tiles_m, int tiles_n, int group) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int nblk = tiles_m * tiles_n;
-  const int t = xcd_remap(blockIdx.x, nblk);
-  int tm_, tn_;
-  tile_of(t, tiles_m, tiles_n, group, tm_, tn_);
-  const int m0 = tm_ * BM, n0 = tn_ * BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int ktiles = K / 64;
-
-  LoadK la, lb;
-  la.init(A, lda, M, m0, tid);
-  lb.init(B, ldb, N, n0, tid);
-  const int r32 = lane & 31, h = lane >> 5;
-  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
-  // fragment bases [stage][K-step]: row r32, chunk 2s + h XOR (r32 >> 1) & 7; blocks (32 rows,
-  // 4096 B) are immediate offsets
-  uint32_t fA[2][4], fB[2][4];
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const uint32_t l = r32 * 128 + ((((2 * s4 + h) ^ ((r32 >> 1) & 7))) << 4);
-      fA[st][s4] = sb + st * STAGE + wm * 16384 + l;
-      fB[st][s4] = sb + st * STAGE + OPB + wn * 16384 + l;
-    }
-  const uint32_t wbase = sb + tid * 16;  // ds_write of piece q: + stage + (q < 8 ? 0 : OPB) + (q & 7) * 4096
-
-  f32x16_t acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      acc[a][b] = f32x16_t{};
-      asm volatile("" : "+a"(acc[a][b]));
-    }
-  bf16x8_t fa[2][4], fb[2][4];
-  ttd_i32x4_t S0[16], S1[16];
-
-  auto loads = [&](ttd_i32x4_t (&S)[16], int kt, auto Q0) {  // pieces Q0 .. Q0 + 7 of K-tile kt
-    constexpr int q0 = decltype(Q0)::value;
-    static_for<8>([&](auto J) {
-      constexpr int q = q0 + decltype(J)::value;
-      const LoadK& L = q < 8 ? la : lb;
-      vload16(S[q], L.voff[q & 7], L.srd, kt * 128);
-    });
-  };
-  auto writes = [&](const ttd_i32x4_t (&S)[16], uint32_t stage_off) {
-    static_for<16>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      vstore_lds<(q < 8 ? 0 : OPB) + (q & 7) * 4096>(wbase + stage_off, S[q]);
-    });
-  };
-  auto reads = [&](int st, auto S4, bf16x8_t (&xa)[4], bf16x8_t (&xb)[4]) {
-    constexpr int s4 = decltype(S4)::value;
-    static_for<4>([&](auto J) {
-      constexpr int j = decltype(J)::value;
-      ld_frag(xa[j], fA[st][s4], std::integral_constant<int, j * 4096>{});
-    });
-    static_for<4>([&](auto J) {
-      constexpr int j = decltype(J)::value;
-      ld_frag(xb[j], fB[st][s4], std::integral_constant<int, j * 4096>{});
-    });
-  };
-  auto mma16 = [&](const bf16x8_t (&xa)[4], const bf16x8_t (&xb)[4]) {
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) mfma32(acc[a][b], xa[a], xb[b]);
-  };
-
-  // prologue: K-tiles 0 and 1 into the register sets, K-tile 0 into LDS stage 0
-  loads(S0, 0, std::integral_constant<int, 0>{});
-  loads(S0, 0, std::integral_constant<int, 8>{});
-  if (ktiles > 1) {
-    loads(S1, 1, std::integral_constant<int, 0>{});
-    loads(S1, 1, std::integral_constant<int, 8>{});
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  writes(S0, 0);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  reads(0, std::integral_constant<int, 0>{}, fa[0], fb[0]);
-
-  // one K-tile; P = kt & 1 (compile time): tile kt in LDS stage P and register set P (now
-  // free), tile kt + 1 in register set P ^ 1
-  auto ktile = [&](int kt, auto PAR, ttd_i32x4_t (&Sp)[16], ttd_i32x4_t (&Sq)[16]) {
-    constexpr int P = decltype(PAR)::value;
-    const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
-    // K-step 0
-    reads(P, std::integral_constant<int, 1>{}, fa[1], fb[1]);
-    if (has2) loads(Sp, kt + 2, std::integral_constant<int, 0>{});
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    mma16(fa[0], fb[0]);
-    // K-step 1
-    reads(P, std::integral_constant<int, 2>{}, fa[0], fb[0]);
-    if (has2) loads(Sp, kt + 2, std::integral_constant<int, 8>{});
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    mma16(fa[1], fb[1]);
-    // K-step 2: K-tile kt + 1 -> the other stage
-    reads(P, std::integral_constant<int, 3>{}, fa[1], fb[1]);
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // K-step 2's fragments (older than the 8 reads)
-    if (has1) {
-      if (has2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      writes(Sq, (P ^ 1) * STAGE);
-    }
-    mma16(fa[0], fb[0]);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // K-step 3: first fragments of K-tile kt + 1 (read unconditionally: unused past the end)
-    reads(P ^ 1, std::integral_constant<int, 0>{}, fa[0], fb[0]);
-    mma16(fa[1], fb[1]);
-  };
-  for (int kt = 0; kt < ktiles; kt += 2) {
-    ktile(kt, std::integral_constant<int, 0>{}, S0, S1);
-    ktile(kt + 1, std::integral_constant<int, 1>{}, S1, S0);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) asm volatile("" : "+a"(acc[a][b]));
-  const float alpha = epi_alpha(E);
-  if (m0 + BM <= M && n0 + BN <= N) epilogue32<EK, false>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
-  else epilogue32<EK, true>(acc, E, m0, n0, M, N, alpha, lane, wm, wn);
 }
 
 }  // namespace g4
@@ -982,9 +692,10 @@ __global__ __launch_bounds__(T, 1) void gemm4v_kernel(const bf16_t* __restrict__
 
 // TTD_G4_SCHED: main-loop form. 2 (default) = one tile per workgroup, hand-ordered SCHED 2;
 // 30 = the persistent SCHED-2 kernel (gemm4p, next tile's DMA under this tile's epilogue);
-// 0 / 1 / 3 other one-tile forms (0 compiler-scheduled), 20 the VGPR-staged 32x32x16 form,
-// 31 = 30 with phase stamps. With the branch-free steady loop (same box, tools/g4_bench.py):
-// 8192^3 1515 (2) vs 1301 (30) TF/s, hipBLASLt 1650; BERT-Large step 154.8 / 156.2 vs 158.7 ms
+// 0 = the compiler-scheduled one-tile loop (oracle). With the branch-free steady loop (same box,
+// tools/g4_bench.py): 8192^3 1515 (2) vs 1301 (30) TF/s, hipBLASLt 1650; BERT-Large step
+// 154.8 / 156.2 vs 158.7 ms. (Measured and removed, round 5: all 16 DMA pieces in phase 1a,
+// one barrier per K-tile, a VGPR-staged 32x32x16 form, in-kernel phase stamps — git history.)
 static int& g4_sched() {
   static int v = ttdk::getenv_int("TTD_G4_SCHED", 2);
   return v;
@@ -1062,15 +773,6 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
       case 2: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 3: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 3>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 31: {                                                                                          \
-        const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
-        if (grid < 8) return hipErrorInvalidValue;                                                          \
-        hipLaunchKernelGGL((g4::gemm4p_kernel<EKV, true>), dim3(grid), dim3(g4::T), 0, st, A, lda, B, ldb, pe, \
-                           M, N, K, tm, tn, group, stag, tq);                                               \
-        break;                                                                                              \
-      }                                                                                                     \
       case 30: {                                                                                          \
         const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
         if (grid < 8 || tm * tn <= g4_cus()) { /* one tile per workgroup: nothing to overlap */           \
@@ -1082,10 +784,7 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
                            K, tm, tn, group, stag, tq);                                                     \
         break;                                                                                              \
       }                                                                                                     \
-      case 20: if (K % 128) return hipErrorInvalidValue;                                                   \
-               hipLaunchKernelGGL((g4::gemm4v_kernel<EKV>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb,   \
-                                  pe, M, N, K, tm, tn, group); break;                                        \
-      default: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 1>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda,   \
+      default: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda,   \
                                   B, ldb, pe, M, N, K, tm, tn, group); break;                                      \
     }                                                                                                       \
     return hipGetLastError();
@@ -1099,9 +798,4 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
   }
 #undef TTDK_G4
   return hipErrorInvalidValue;
-}
-
-// diagnostic: copy the per-wave phase stamps of the last TTD_G4_SCHED=31 launch (2048 x 4 x 4 u64)
-TTDK_EXPORT int ttdk_g4_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ttdk::g4::g_stamps), sizeof(ttdk::g4::g_stamps), 0, hipMemcpyDeviceToHost);
 }

@@ -819,12 +819,77 @@ def wgrad_splits(g, target_blocks=None, min_ktiles=8):
     return s
 
 
-def conv_wgrad(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, splits=None,
-               tile=(0, 0)):
-    """dw[K,R,S,C] (fp32) = sum over pixels of dy x im2col(x)."""
+# weight gradients on the 4-wave transposed-read kernel (gemm4t.hip: im2col gather of x for
+# strided / 3x3 convs, split-K summed in the launch). TTD_WGRAD4T: 0 off; 1 (default) the convs
+# where it measured faster standalone at b1024 (tools/wgrad4t_bench.py,
+# profiles/r6_wgrad4t_bench_b1024.txt): filters larger than 1x1 with >= 256 output channels, and
+# 1x1 convs with M, N >= 256 and M * N >= 512 * 1024 (the smaller 1x1 shapes have 4 output tiles
+# and need 32-64 K-splits: the in-kernel sum of that many slabs by one workgroup outweighs the
+# faster main loop); 2 every conv with M >= 256 and R*S*C >= 128; 3 the filters larger than 1x1 only.
+_WGRAD4T = int(_os.environ.get("TTD_WGRAD4T", "1"))
+# workgroup target per launch: 128 (in the two-stream step 256 for the 1x1 shapes, faster
+# standalone, cost 0.5 ms: profiles/r6_wgrad4t_step_ab.txt); 0: per shape (128 3x3, 256 1x1)
+_WGRAD4T_WGS = int(_os.environ.get("TTD_WGRAD4T_WGS", "128"))
+_WGRAD4T_MIN_KT = int(_os.environ.get("TTD_WGRAD4T_MIN_KT", "32"))
+
+
+def conv_wgrad4t_splits(g, target_blocks=None, min_ktiles=None):
+    """Split-K factor of the 4-wave weight gradient: ~target_blocks workgroups (the side stream
+    shares the CUs with the data-gradient chain; default 128 for gathered filters, 256 for 1x1),
+    >= min_ktiles K-tiles of 64 pixels per split."""
+    target = target_blocks or _WGRAD4T_WGS or (128 if g.R * g.S > 1 else 256)
+    mk = _WGRAD4T_MIN_KT if min_ktiles is None else min_ktiles
+    M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
+    tiles = -(-M // 256) * -(-N // 256)
+    return max(1, min((K // 64) // mk, -(-target // tiles)))
+
+
+def conv_wgrad4t_ok(g, mode=None) -> bool:
+    """Whether conv_wgrad runs this conv on the 4-wave kernel (TTD_WGRAD4T policy + the kernel's
+    own admission: C, K % 8, pixels % 64, operands < 2 GiB, no dilation)."""
+    mode = _WGRAD4T if mode is None else mode
+    M, N = g.K, g.R * g.S * g.C
+    if mode <= 0 or M < 256 or N < 128:
+        return False
+    if mode in (1, 3):
+        if g.R * g.S == 1 and (mode == 3 or N < 256 or M * N < 512 * 1024):
+            return False
+        if g.R * g.S > 1 and N < 256:
+            return False
+    return int(_lib.query("ttdk_conv_wgrad4t_ws", ctypes.byref(g), 1)) >= 0
+
+
+def conv_wgrad4t(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, splits=None):
+    """dw[K,R,S,C] (fp32) (+)= sum over pixels of dy x im2col(x) on the 4-wave transposed-read
+    kernel (gemm4t.hip; the im2col of x gathered by the operand DMA, split-K summed inside the
+    launch). Raises when the kernel does not take the conv (no silent fallback)."""
     _check(x, torch.bfloat16, "x")
     _check(dy, torch.bfloat16, "dy")
     g = conv_geom(x.shape, w_shape, stride, padding)
+    if out is None:
+        out = torch.empty(tuple(w_shape), dtype=torch.float32, device=x.device)
+    if splits is None:
+        splits = conv_wgrad4t_splits(g)
+    nws = int(_lib.query("ttdk_conv_wgrad4t_ws", ctypes.byref(g), int(splits)))
+    if nws < 0:
+        raise ValueError("conv_wgrad4t does not take x %s, w %s, stride %s, pad %s"
+                         % (tuple(x.shape), tuple(w_shape), stride, padding))
+    ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device)
+    _log("wgrad4t_%dx%d_s%d" % (g.R, g.S, g.sh), g.K, g.R * g.S * g.C, g.N * g.P * g.Q, splits)
+    _lib.call("ttdk_conv_wgrad4t", x.data_ptr(), dy.data_ptr(), ctypes.byref(g), out.data_ptr(), ws.data_ptr(),
+              int(splits), int(beta), _lib.stream())
+    return out
+
+
+def conv_wgrad(x, dy, w_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta=0, splits=None,
+               tile=(0, 0)):
+    """dw[K,R,S,C] (fp32) = sum over pixels of dy x im2col(x). Convs the 4-wave kernel takes
+    (conv_wgrad4t_ok) run there unless a split / tile is forced."""
+    _check(x, torch.bfloat16, "x")
+    _check(dy, torch.bfloat16, "dy")
+    g = conv_geom(x.shape, w_shape, stride, padding)
+    if splits is None and tile == (0, 0) and conv_wgrad4t_ok(g):
+        return conv_wgrad4t(x, dy, w_shape, stride, padding, out=out, beta=beta)
     if out is None:
         out = torch.empty(tuple(w_shape), dtype=torch.float32, device=x.device)
     if splits is None:

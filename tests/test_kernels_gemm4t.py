@@ -89,3 +89,62 @@ def test_conv_wgrad_1x1_takes_gemm4t(beta):
     G.conv_wgrad(x, dy, (512, 1, 1, 256), out=out, beta=beta, splits=4)
     want = ref + (old.view(512, 256) if beta else 0)
     assert _rel(out.view(512, 256), want) < 1e-5
+
+
+# --- convolution weight gradients on the 4-wave kernel with the im2col gather of x -------------
+# (the kernel gradients of the ResNet-50 convs; b1024 stage shapes: stage 4/5 3x3, strided 3x3 /
+# 1x1 projections, unit-stride 1x1), vs torch.nn.grad.conv2d_weight in fp32 on the same bf16 data
+
+def _conv_wgrad_ref(x, dy, w_shape, stride, pad):
+    xf = x.float().permute(0, 3, 1, 2)
+    dyf = dy.float().permute(0, 3, 1, 2)
+    K, R, S, C = w_shape
+    dw = torch.nn.grad.conv2d_weight(xf, (K, C, R, S), dyf, stride=stride, padding=pad)
+    return dw.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("N,H,C,K,R,stride,splits", [
+    (1024, 14, 256, 256, 3, 1, None),    # stage 4 c2 (3x3, pad 1)
+    (1024, 14, 512, 512, 3, 2, None),    # stage 5 block-1 c2 (3x3 stride 2)
+    (1024, 7, 512, 512, 3, 1, None),     # stage 5 c2
+    (1024, 14, 1024, 2048, 1, 2, None),  # stage 5 projection (1x1 stride 2)
+    (1024, 28, 512, 1024, 1, 2, None),   # stage 4 projection
+    (1024, 14, 256, 1024, 1, 1, None),   # stage 4 c3 (unit-stride 1x1: dense operands)
+    (64, 9, 64, 256, 3, 1, 3),           # odd spatial size, C = 64 (four taps per 256 columns)
+    (16, 12, 128, 264, 3, 2, 1),         # K not a multiple of 256, one split (576 pixels)
+    (4, 8, 8, 256, 3, 1, 2),             # C = 8 (256 pixels): 32 taps of 8 channels per 256 columns
+])
+def test_conv_wgrad4t_vs_fp32(N, H, C, K, R, stride, splits):
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(N + H + C + K + R + stride)
+    pad = R // 2
+    x = (torch.rand(N, H, H, C, device="cuda") * 2 - 1).bfloat16()
+    P = (H + 2 * pad - R) // stride + 1
+    dy = (torch.rand(N, P, P, K, device="cuda") * 2 - 1).bfloat16()
+    w_shape = (K, R, R, C)
+    ref = _conv_wgrad_ref(x, dy, w_shape, stride, pad)
+    out = G.conv_wgrad4t(x, dy, w_shape, (stride, stride), (pad, pad), splits=splits)
+    assert _rel(out, ref) < 1e-5
+    # deterministic (fixed split order), counters left zeroed for the next launch
+    out2 = G.conv_wgrad4t(x, dy, w_shape, (stride, stride), (pad, pad), splits=splits)
+    assert torch.equal(out, out2)
+    # accumulate
+    old = torch.randn_like(ref)
+    acc = old.clone()
+    G.conv_wgrad4t(x, dy, w_shape, (stride, stride), (pad, pad), out=acc, beta=1, splits=splits)
+    assert _rel(acc, ref + old) < 1e-5
+
+
+def test_conv_wgrad_dispatches_to_4wave_kernel():
+    """ops.gemm.conv_wgrad routes a stage-4 3x3 weight gradient to the 4-wave kernel (launch log)."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    x = (torch.rand(64, 14, 14, 256, device="cuda") * 2 - 1).bfloat16()
+    dy = (torch.rand(64, 14, 14, 256, device="cuda") * 2 - 1).bfloat16()
+    saved, G._LOG = G._LOG, []
+    try:
+        out = G.conv_wgrad(x, dy, (256, 3, 3, 256), (1, 1), (1, 1))
+        kinds = [e[0] for e in G.gemm_log()]
+    finally:
+        G._LOG = saved
+    assert any(k.startswith("wgrad4t_3x3") for k in kinds), kinds
+    assert _rel(out, _conv_wgrad_ref(x, dy, (256, 3, 3, 256), 1, 1)) < 1e-5
