@@ -37,6 +37,13 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+def _reducer_engine():
+    """TTD_REDUCER_ENGINE=ipc: the multi-rank rehearsal on fewer GPUs (ranks share a device over
+    gloo, every gradient bucket on the direct IPC kernels, so the N > 1 step — collectives
+    included — can be graph-captured and replayed as it would be over RCCL)."""
+    return os.environ.get("TTD_REDUCER_ENGINE", "auto")
+
+
 def build_resnet(args, dev, rank, world):
     from tensorflow_train_distributed_amd.models.resnet import resnet50
     from tensorflow_train_distributed_amd.parallel.collective import BucketedAllReducer, broadcast_flat_
@@ -55,7 +62,8 @@ def build_resnet(args, dev, rank, world):
                                              power=2.0, total_steps=10000), momentum=0.9, weight_decay=5e-5)
     # the backward window the collectives hide under is measured on a warm-up step (main) and
     # fed to the native engine's CTA-budget choice (BucketedAllReducer.retune)
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16,
+                                 engine=_reducer_engine())
     g = torch.Generator(device=dev)
     g.manual_seed(rank)
     S = args.image_size
@@ -103,7 +111,8 @@ def build_bert(args, dev, rank, world):
     opt = FlatLAMB(model.params, Schedule(kind=2, base_lr=4e-3, warmup_steps=100, end_lr=0.0, power=1.0,
                                           total_steps=10000), weight_decay=0.01, max_grad_norm=1.0)
     # (overlap window: measured on a warm-up step, see main)
-    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16)
+    reducer = BucketedAllReducer(model.params, bucket_mb=args.bucket_mb, compress_bf16=args.compress_bf16,
+                                 engine=_reducer_engine())
     batch = synthetic_batch(cfg, B, S, max_predictions=80 if S >= 512 else 20, device=dev, seed=rank)
 
     def step():
@@ -296,9 +305,10 @@ def main():
     auto_graph = 1 if world == 1 else int(os.environ.get("TTD_BENCH_GRAPH", "0"))
     use_graph = args.graph if args.graph >= 0 else auto_graph
     red0 = getattr(step, "reducer", None)
-    if on_cpu or (world > 1 and getattr(red0, "comm", None) is None):
+    if on_cpu or (world > 1 and getattr(red0, "comm", None) is None and getattr(red0, "ipc_stream", None) is None):
         # torch process-group collectives are issued eagerly; the native RCCL engine's bucket
-        # launches are stream-ordered and capture into the step's hipGraph
+        # launches (and the ipc rehearsal engine's kernels) are stream-ordered and capture into
+        # the step's hipGraph
         use_graph = 0
     graph = None
     out = None

@@ -465,13 +465,23 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const bf16_t* __restr
 
 // ------------------------------------------------------------------ vocabulary xent
 // inv_count[0] = scale / max(1, #labels >= 0)
+// inv_count[0] = scale / count; with both (the MLM step's metric and gradient scales from one
+// launch instead of a torch multiply) inv_count[0] = 1 / count, inv_count[1] = scale / count
 __global__ __launch_bounds__(256) void count_valid_kernel(const int* __restrict__ labels, int n, float scale,
-                                                          float* __restrict__ inv_count) {
+                                                          float* __restrict__ inv_count, int both) {
   __shared__ float red[16];
   float c = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) c += labels[i] >= 0 ? 1.f : 0.f;
   c = block_sum(c, red);
-  if (threadIdx.x == 0) inv_count[0] = scale / fmaxf(c, 1.f);
+  if (threadIdx.x == 0) {
+    const float cc = fmaxf(c, 1.f);
+    if (both) {
+      inv_count[0] = 1.f / cc;
+      inv_count[1] = scale / cc;
+    } else {
+      inv_count[0] = scale / cc;
+    }
+  }
 }
 
 // One block per row of bf16 logits [rows][ld] (first V columns valid). labels < 0 are
@@ -729,7 +739,13 @@ TTDK_EXPORT int ttdk_rng_advance(long long* t, hipStream_t st) {
 }
 
 TTDK_EXPORT int ttdk_count_valid(const int* labels, int n, float scale, float* inv_count, hipStream_t st) {
-  hipLaunchKernelGGL(count_valid_kernel, dim3(1), dim3(256), 0, st, labels, n, scale, inv_count);
+  hipLaunchKernelGGL(count_valid_kernel, dim3(1), dim3(256), 0, st, labels, n, scale, inv_count, 0);
+  return hipGetLastError();
+}
+
+// out[0] = 1 / count, out[1] = scale / count (count = labels >= 0)
+TTDK_EXPORT int ttdk_count_valid2(const int* labels, int n, float scale, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(count_valid_kernel, dim3(1), dim3(256), 0, st, labels, n, scale, out, 1);
   return hipGetLastError();
 }
 

@@ -462,9 +462,8 @@ class BertPretraining:
         logits = self._plain(t2, P.c["bert/embeddings/word_embeddings"], P.var["cls/predictions/output_bias"],
                              P.c["cls/predictions/output_bias"])
         sums = K.zeros(4, dtype=torch.float32, device=dev)  # own memset: no torch fill kernel in the step
-        inv_cnt = torch.empty(1, dtype=torch.float32, device=dev)
-        T.count_valid(labels, 1.0, inv_cnt)
-        gsc = inv_cnt * loss_scale
+        cnt = T.count_valid2(labels, loss_scale, torch.empty(2, dtype=torch.float32, device=dev))
+        inv_cnt, gsc = cnt[0:1], cnt[1:2]  # metric scale 1 / count, gradient scale loss_scale / count
         T.xent_vocab(logits, V, labels, gsc, dlogits=logits, sums=sums[0:2], mscale=inv_cnt)
         dlog = logits  # gradient now, in place
         # next-sentence head

@@ -25,6 +25,7 @@ _lib.register({
     "ttdk_scatter_rows": [P, P, I, L, P, L, I, I, I, P],
     "ttdk_rng_advance": [P, P],
     "ttdk_count_valid": [P, I, F, P, P],
+    "ttdk_count_valid2": [P, I, F, P, P],
     "ttdk_xent_vocab": [P, L, I, P, I, P, P, P, P, P],
     "ttdk_tanh_bf16": [P, L, P],
     "ttdk_dact_bf16": [P, P, P, L, I, P],
@@ -160,6 +161,12 @@ def scatter_rows(src, idx, dst, accumulate=False, *, group=(1, 0)):
 
 def count_valid(labels, scale, out):
     _lib.call("ttdk_count_valid", labels.data_ptr(), labels.numel(), float(scale), out.data_ptr(), _s())
+    return out
+
+
+def count_valid2(labels, scale, out):
+    """out[0] = 1 / count, out[1] = scale / count (count = labels >= 0), one launch."""
+    _lib.call("ttdk_count_valid2", labels.data_ptr(), labels.numel(), float(scale), out.data_ptr(), _s())
     return out
 
 

@@ -52,11 +52,17 @@ class BucketedAllReducer:
                  compress_bf16: bool = False, algorithm: str = "allreduce", num_packs: Optional[int] = None,
                  engine: str = "auto", overlap_ms: Optional[float] = None):
         """engine: "auto" (native RCCL engine on GPU process groups of > 1 rank), "native"
-        (required; also on a one-rank group — tests), "torch" (torch.distributed calls).
+        (required; also on a one-rank group — tests), "torch" (torch.distributed calls), "ipc"
+        (rehearsal: EVERY bucket on the direct xGMI one-/two-shot kernels over IPC-mapped staging
+        buffers, any process group as the control plane — e.g. gloo with several ranks sharing
+        one GPU, which RCCL refuses — so the multi-rank step, collectives included, is made of
+        stream-ordered GPU kernels and can be hipGraph-captured and replayed like the RCCL one).
         overlap_ms: the caller's estimate of the backward the collectives hide under (the native
         engine's start-up CTA-budget probe uses it, rccl.choose_cta_budget)."""
         if algorithm not in ALGORITHMS:
             raise ValueError("unknown all-reduce algorithm %r (one of %s)" % (algorithm, ALGORITHMS))
+        if engine not in ("auto", "native", "torch", "ipc"):
+            raise ValueError("unknown reducer engine %r" % engine)
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -65,13 +71,17 @@ class BucketedAllReducer:
         if num_packs is not None and num_packs > 0:
             # TF num_packs: that many (roughly equal) buckets over the whole gradient buffer
             bucket_mb = first_bucket_mb = max(flat.numel * 4 / num_packs, 4.0) / (1 << 20)
-        ends = []  # end offset (exclusive) of each variable, in layout order
-        for s in flat.specs:
-            o = flat.offsets[s.name]
+        # end offset (exclusive) of each variable in layout order, INCLUDING the alignment padding
+        # up to the next variable (flat.ALIGN elements): every bucket then starts and ends 256-B
+        # aligned (whole 16-B vectors for the direct kernels); the padding's gradient is zero
+        starts = [flat.offsets[s.name] for s in flat.specs]
+        ends = []
+        for i, s in enumerate(flat.specs):
             n = 1
             for d in s.shape:
                 n *= int(d)
-            ends.append(o + n)
+            nxt = min([o for o in starts if o > starts[i]], default=flat.numel)
+            ends.append(max(starts[i] + n, nxt))
         if ends:  # the alignment padding after the last variable rides in the last bucket
             ends[-1] = flat.numel
         self._var_end = {s.name: e for s, e in zip(flat.specs, ends)}
@@ -94,6 +104,7 @@ class BucketedAllReducer:
                 self._make_buckets()
         self.engine = "native-rccl" if self.comm is not None else ("torch-" + dist.get_backend(group)
                                                                    if self.world > 1 else "none")
+        self.ipc_stream = None  # engine "ipc": the direct kernels' own communicator stream
         # CUs the persistent kernels leave to the collectives while buckets are in flight
         # (rccl.py: co-scheduling policy). Opt-in: at the default CTA budget the measured
         # interference is < 1 % without it (tools/comm_interference.py)
@@ -134,12 +145,35 @@ class BucketedAllReducer:
                             self.ipc, self.ipc_reason = None, why
                         else:
                             self._paths = paths
+        if engine == "ipc":
+            self._init_ipc_rehearsal(group)
         self._next = 0
         self._works = []
         self._keep = []
         self._timed = None
         self._window = None
         self.launch_log: List[int] = []
+
+    def _init_ipc_rehearsal(self, group):
+        """engine "ipc": every bucket through the direct one-shot (<= 1 MB) / two-shot kernels on a
+        stream of the reducer's own (staging buffers sized for the largest bucket)."""
+        from ..utils import errors
+        from . import ipc as ipcm
+        if self.world < 2 or not self.flat.grad.is_cuda or self.compress:
+            raise errors.FailedPreconditionError("the ipc rehearsal engine wants >= 2 GPU ranks, fp32 buckets")
+        if any(s % 4 or (e - s) % 4 for s, e in self.buckets):
+            raise errors.FailedPreconditionError("ipc rehearsal: a bucket is not whole 16-B vectors")
+        cap = max(e - s for s, e in self.buckets) * 4
+        self.ipc = ipcm.IpcAllReducer(group, cap_bytes=cap)
+        why = self._ipc_selfcheck()
+        if why:
+            self.ipc.destroy()
+            self.ipc = None
+            raise errors.UnavailableError("ipc rehearsal engine: " + why)
+        self._paths = [ipcm.ONE_SHOT if (e - s) * 4 <= ipcm.ONE_SHOT_MAX else ipcm.TWO_SHOT
+                       for s, e in self.buckets]
+        self.ipc_stream = torch.cuda.Stream(device=self.flat.grad.device)
+        self.engine = "ipc-rehearsal"
 
     def _ipc_selfcheck(self) -> Optional[str]:
         """Both direct paths on a known pattern (sum of rank + 1), every rank voting: the paths
@@ -169,7 +203,7 @@ class BucketedAllReducer:
         """Path of every bucket: "ipc_oneshot" / "ipc_twoshot" (direct xGMI), "rccl" (native
         engine), or the torch backend's name."""
         from .ipc import PATH_NAMES
-        if self.comm is None:
+        if self.comm is None and self.ipc_stream is None:
             return [self.engine] * len(self.buckets)
         return [PATH_NAMES[p] for p in self._paths]
 
@@ -277,6 +311,13 @@ class BucketedAllReducer:
         self.launch_log.append(i)
         if self.world == 1 and self.comm is None:
             return
+        if self.ipc_stream is not None:
+            # rehearsal engine: the direct kernel on the reducer's stream, ordered after the
+            # producing stream (an event node pair under segmented capture)
+            from ..utils import graphs
+            graphs.fork(torch.cuda.current_stream(), self.ipc_stream)
+            self.ipc.all_reduce_(t, self._paths[i], stream=self.ipc_stream)
+            return
         if i == 0:
             # from the first bucket on, RCCL CTAs may hold CUs: persistent grids launched from
             # here to finish() use the remaining ones
@@ -354,6 +395,12 @@ class BucketedAllReducer:
         if self._window is not None:
             self._window[1].record()  # the backward's last queued work
             self._window[2] = True
+        if self.ipc_stream is not None:
+            from ..utils import graphs
+            graphs.join(torch.cuda.current_stream(), self.ipc_stream)
+            if not graphs.capturing_segmented():
+                self.check()
+            return
         if self.comm is not None:
             if self._timed is not None:
                 self._timed[0].record()  # the backward's last queued work

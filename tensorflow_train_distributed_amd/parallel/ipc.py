@@ -41,6 +41,7 @@ from .. import _native
 from ..utils import errors
 
 RCCL, ONE_SHOT, TWO_SHOT = 0, 1, 2
+ONE_SHOT_MAX = 1 << 20  # ipc_plan.h kOneShotMax
 PATH_NAMES = {RCCL: "rccl", ONE_SHOT: "ipc_oneshot", TWO_SHOT: "ipc_twoshot"}
 HANDLE_BYTES = 128  # data + flags hipIpcMemHandle_t
 

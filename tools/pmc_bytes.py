@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-kernel HBM traffic of the last profiled training step from two rocprofv3 --pmc runs
 (FETCH_SIZE, WRITE_SIZE; KB per dispatch). The step = dispatches from the last stem kernel on.
-usage: pmc_bytes.py <fetch_dir> <write_dir>"""
+With a kernel-trace run of the same command (third argument), each kernel's time in that step
+and its achieved bandwidth (bytes / time) against a 6 TB/s line.
+usage: pmc_bytes.py <fetch_dir> <write_dir> [<trace_dir>]"""
 import csv
 import glob
 import re
@@ -38,7 +40,19 @@ for _, n, v in wr:
     tot[short(n)][1] += v
 F = sum(v[0] for v in tot.values()) / 1e6
 W = sum(v[1] for v in tot.values()) / 1e6
-print("step HBM traffic: fetch %.1f GB, write %.1f GB, total %.1f GB (%d dispatches)" % (F, W, F + W, len(fe)))
-print("%-100s %5s %9s %9s" % ("kernel", "n", "fetch GB", "write GB"))
-for k, v in sorted(tot.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))[:45]:
-    print("%-100s %5d %9.2f %9.2f" % (k, v[2], v[0] / 1e6, v[1] / 1e6))
+tus = defaultdict(float)
+if len(sys.argv) > 3:
+    f = glob.glob(sys.argv[3] + "/**/*kernel_trace.csv", recursive=True)
+    rows = sorted(csv.DictReader(open(f[0])), key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "stem_fwd" in r["Kernel_Name"]]
+    for r in rows[idx[-1]:] if idx else rows:
+        tus[short(r["Kernel_Name"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+T = sum(tus.values())
+print("step HBM traffic: fetch %.1f GB, write %.1f GB, total %.1f GB (%d dispatches)%s"
+      % (F, W, F + W, len(fe), ", kernel time %.1f ms -> %.2f TB/s average" % (T / 1e3, (F + W) / T * 1e3) if T else ""))
+print("%-100s %5s %9s %9s %9s %7s %s" % ("kernel", "n", "fetch GB", "write GB", "time us", "TB/s", "vs 6 TB/s"))
+for k, v in sorted(tot.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))[:60]:
+    t = tus.get(k, 0.0)
+    bw = (v[0] + v[1]) / t * 1e-3 if t > 0 else 0.0
+    bar = ("#" * int(round(bw / 6.0 * 20))).ljust(20)[:30] if t > 0 else ""
+    print("%-100s %5d %9.2f %9.2f %9.1f %7.2f |%s|" % (k, v[2], v[0] / 1e6, v[1] / 1e6, t, bw, bar))
