@@ -129,7 +129,10 @@ __device__ __forceinline__ uint32_t attn_pair_of(uint32_t k) { return ((k >> 5) 
 // sampling noise) are pinned by tests/test_kernels_transformer.py on the mirror.
 __device__ __forceinline__ uint32_t attn_mix(uint32_t h) {
   h ^= h >> 16;
-  h = __umul24(h, 0x9E3779u);
+  // 24 x 24-bit multiply-add (one full-rate v_mad_u32_u24): the high byte, which the 24-bit
+  // multiply cannot see, is added in, so all 32 input bits reach the output (the multiply alone
+  // had at most 2^24 distinct outputs: x and x ^ 0x01000100 collided)
+  h = __umul24(h, 0x9E3779u) + (h >> 24);
   h ^= h >> 16;
   return h;
 }

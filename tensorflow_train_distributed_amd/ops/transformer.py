@@ -204,10 +204,11 @@ def _fmix32(h):
 
 
 def _attn_mix(h):
-    """tile_common.h attn_mix: xorshift, 24 x 24-bit multiply (v_mul_u32_u24), xorshift."""
+    """tile_common.h attn_mix: xorshift, 24 x 24-bit multiply-add of the high byte
+    (v_mad_u32_u24), xorshift."""
     h = np.asarray(h, dtype=np.uint64) & M32
     h ^= h >> np.uint64(16)
-    h = ((h & np.uint64(0xFFFFFF)) * np.uint64(0x9E3779)) & M32
+    h = ((h & np.uint64(0xFFFFFF)) * np.uint64(0x9E3779) + (h >> np.uint64(24))) & M32
     h ^= h >> np.uint64(16)
     return h
 

@@ -163,7 +163,9 @@ class BucketedAllReducer:
             raise errors.FailedPreconditionError("the ipc rehearsal engine wants >= 2 GPU ranks, fp32 buckets")
         if any(s % 4 or (e - s) % 4 for s, e in self.buckets):
             raise errors.FailedPreconditionError("ipc rehearsal: a bucket is not whole 16-B vectors")
-        cap = max(e - s for s, e in self.buckets) * 4
+        # at least the default staging size: the self-check's two-shot pattern is 3 MB, larger
+        # than every bucket of a small model
+        cap = max(max(e - s for s, e in self.buckets) * 4, ipcm.default_cap())
         self.ipc = ipcm.IpcAllReducer(group, cap_bytes=cap)
         why = self._ipc_selfcheck()
         if why:

@@ -63,6 +63,23 @@ def test_attention_dropout_pair_hash_statistics():
     assert abs(T.attention_drop_scale(0.1) - 1 / 0.9) < 1e-4
 
 
+def test_attention_pair_hash_has_full_32_bit_range():
+    """Every input bit reaches the pair hash (a bare 24 x 24-bit multiply had at most
+    2^24 outputs, x and x ^ 0x01000100 collided and each keep pattern repeated ~16 times per
+    BERT-Large layer). Exact collisions over 2^21 consecutive (row, pair) inputs stay at the
+    birthday rate of a 32-bit hash (n^2 / 2^33 = 512 expected; a 24-bit range gives ~131k)."""
+    rng = np.random.default_rng(0)
+    x = rng.integers(0, 1 << 32, size=1 << 16, dtype=np.uint64)
+    assert np.all(T._attn_mix(x) != T._attn_mix(x ^ np.uint64(0x01000100)))
+    key = np.uint64(T.drop_key(1234, 7, 3))
+    rowid = np.arange(1 << 13, dtype=np.uint64).reshape(-1, 1)
+    pair = np.arange(256, dtype=np.uint64).reshape(1, -1)
+    mixed = ((rowid * np.uint64(0x9E3779B1)) + (pair * np.uint64(0x7FEB352D))) & np.uint64(0xFFFFFFFF)
+    h = T._attn_mix(key ^ mixed).ravel()
+    dup = h.size - np.unique(h).size
+    assert dup < 2000, dup
+
+
 @gpu
 @pytest.mark.parametrize("S,masked,p,fused", [(256, False, 0.0, True), (256, True, 0.0, True), (256, False, 0.1, True),
                                              (512, True, 0.1, True), (128, False, 0.1, True), (512, False, 0.0, True),

@@ -86,15 +86,33 @@ def _worker(rank, world, port, q):
             opt.step()
             return s
 
+        from tensorflow_train_distributed_amd.parallel.collective import sync_on_read_mean_
+
+        def diverged():
+            # BN moving statistics are per replica (TF SyncOnRead): averaged as a checkpoint save
+            # would; then every variable must be bit-identical across the ranks
+            sync_on_read_mean_(m.params)
+            P = m.params
+            names = [n for n in P.names()]
+            w = torch.stack([P.var[n].double().sum() for n in names]).cpu()
+            ws = [torch.zeros_like(w) for _ in range(world)]
+            dist.all_gather(ws, w)
+            return [n for i, n in enumerate(names) if any(v[i] != ws[0][i] for v in ws[1:])]
+
+        # eager training steps first (collectives on the direct kernels, no graph)
+        with torch.cuda.stream(main):
+            for _ in range(2):
+                train()
+        torch.cuda.synchronize()
+        red.check()
+        res["eager_diverged"] = diverged()
         seg2 = graphs.capture_segmented(train, main=main, warmup=1)
         for _ in range(3):
             seg2.replay()
         torch.cuda.synchronize()
         red.check()
-        w = m.params.master.double().sum().reshape(1).cpu()
-        ws = [torch.zeros_like(w) for _ in range(world)]
-        dist.all_gather(ws, w)
-        res["weights_in_sync"] = all(torch.equal(ws[0], v) for v in ws[1:])
+        res["replay_diverged"] = diverged()
+        res["weights_in_sync"] = not res["eager_diverged"] and not res["replay_diverged"]
         red.ipc.destroy()
         dist.destroy_process_group()
         q.put((rank, res))
