@@ -436,6 +436,17 @@ def main():
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         replicas_in_sync = bool(lo.item() == hi.item())
+        if not replicas_in_sync:
+            # which variables differ (diagnostic for the failure line; collective on every rank)
+            names = params.names()
+            w = torch.stack([params.var[n].double().sum() for n in names])
+            wl, wh = w.clone(), w.clone()
+            dist.all_reduce(wl, op=dist.ReduceOp.MIN)
+            dist.all_reduce(wh, op=dist.ReduceOp.MAX)
+            bad = [n for n, a_, b_ in zip(names, wl.tolist(), wh.tolist()) if a_ != b_]
+            if rank == 0:
+                print("bench: %d of %d variables differ across replicas, e.g. %s" % (len(bad), len(names), bad[:8]),
+                      file=sys.stderr)
     # collective evidence for the scaling run: RCCL bus bandwidth of the gradient all-reduce at
     # the bucket sizes the reducer uses and at the whole gradient buffer (after the timed region,
     # on scratch copies: it does not touch the weights)

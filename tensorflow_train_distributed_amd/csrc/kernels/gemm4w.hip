@@ -408,16 +408,92 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   auto mfma1 = [&](int a, int b, const bf16x8_t& x, const bf16x8_t& y, auto first) {
     mfma_acc<decltype(first)::value>(acc[a][b], x, y);
   };
-  // prologue: K-tiles 0 and 1, wait for 0, K-step-0 fragments of K-tile 0
-  m0_init(m0_of(0, 0));
-  static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
+  // prologue: K-tiles 0 and 1, wait for 0, K-step-0 fragments of K-tile 0 (SCHED 3: K-tile kt
+  // in stage (kt + ktiles) & 1, so that the last two K-tiles always sit in stages 0, 1)
+  const int st0 = SCHED == 3 ? (ktiles & 1) : 0;
+  m0_init(m0_of(0, st0));
+  static_for<16>([&](auto Q) { dma1(Q, st0, 0); });
   if (ktiles > 1) {
-    static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
+    static_for<16>([&](auto Q) { dma1(Q, st0 ^ 1, 1); });
     asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
+  if constexpr (SCHED != 3) static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
+  if constexpr (SCHED == 3) {
+  // SCHED 3: the stage of K-tile kt is released in two halves, so the DMA of K-tile kt + 2 starts
+  // 32 MFMAs earlier than in SCHED 2 (every piece gets >= 132 MFMAs, ~2100 cycles, to land
+  // instead of >= 99) at the price of a third barrier; the stage index is compile-time (the
+  // K-tiles go in pairs), so no per-K-tile selects of the fragment / DMA bases:
+  //   A  (MFMAs  0-31, K-step 0): the 8 A fragments of K-step 1, one per 3 MFMAs;
+  //      lgkmcnt(0), barrier: every wave is done with this stage's A half
+  //   B  (MFMAs 32-63, K-step 0): the 8 B fragments of K-step 1 | DMA of K-tile kt + 2, A half;
+  //      lgkmcnt(0), barrier: ... and with its B half
+  //   C  (MFMAs 64-95, K-step 1): DMA of K-tile kt + 2, B half;
+  //      vmcnt(16 pieces of kt + 2), barrier: K-tile kt + 1 has landed for every wave
+  //   D  (MFMAs 96-127, K-step 1): the 16 K-step-0 fragments of K-tile kt + 1, one per 2 MFMAs.
+  auto rda = [&](auto Bk, uint32_t base, bf16x8_t (&xa)[8]) {
+    constexpr int b = decltype(Bk)::value;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(xa[b]) : "v"(base), "i"(b * 2048));
+  };
+  auto ktile3 = [&](int kt, auto stc, auto has2c) {
+    constexpr int st = decltype(stc)::value;
+    constexpr bool has2 = decltype(has2c)::value;
+    static_for<32>([&](auto I) {  // A
+      constexpr int i = decltype(I)::value, a = i / 8, b = i % 8;
+      if constexpr (i % 3 == 0 && i / 3 < 8) rda(std::integral_constant<int, i / 3>{}, va[st][1], fa[1]);
+      constexpr int issued = (i / 3 + 1) < 8 ? (i / 3 + 1) : 8;
+      constexpr int pi = i == 0 ? 0 : i - 1;
+      constexpr int issued_p = (pi / 3 + 1) < 8 ? (pi / 3 + 1) : 8;
+      if constexpr (i == 0 || 15 - need0(i) + issued != 15 - need0(pi) + issued_p)
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(15 - need0(i) + issued) : "memory");
+      mfma1(a, b, fa[0][a], fb[0][b], F{});
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    static_for<32>([&](auto I) {  // B
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 3 == 0 && i / 3 < 8) rda(std::integral_constant<int, i / 3>{}, vb[st][1], fb[1]);
+      if constexpr (i % 4 == 2)
+        if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
+      mfma1(4 + i / 8, i % 8, fa[0][4 + i / 8], fb[0][i % 8], F{});
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    static_for<32>([&](auto I) {  // C
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 4 == 0)
+        if constexpr (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
+      mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
+    });
+    if constexpr (has2) {
+      asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    static_for<32>([&](auto I) {  // D
+      constexpr int i = decltype(I)::value;
+      if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
+      mfma1(4 + i / 8, i % 8, fa[1][4 + i / 8], fb[1][i % 8], F{});
+    });
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  // (ktiles >= 2, host-checked.) Straight-line code around the loops: MFMA sequences inside
+  // if / else copies made hipcc allocate the accumulators per copy and spill (measured: 540
+  // scratch accesses); an odd K-tile count starts in stage 1 instead
+  if (st0) static_for<16>([&](auto R) { rd1(R, va[1][0], vb[1][0], fa[0], fb[0]); });
+  else static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
+  int kt = 0;
+  for (int i = 0; i < st0; ++i) {
+    ktile3(0, S1{}, Tr{});
+    kt = 1;
+  }
+  for (; kt < ktiles - 2; kt += 2) {
+    ktile3(kt, S0{}, Tr{});
+    ktile3(kt + 1, S1{}, Tr{});
+  }
+  ktile3(ktiles - 2, S0{}, F{});
+  ktile3(ktiles - 1, S1{}, F{});
+  } else {
   // HAS2 (K-tile kt + 2 exists) compile-time: no branch around the DMA pieces in the steady loop
   auto ktile = [&](int kt, auto first, auto has2c) {
     constexpr bool has2 = decltype(has2c)::value;
@@ -462,6 +538,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   };
   for (int kt = 0; kt < ktiles - 2; ++kt) ktile(kt, F{}, Tr{});
   for (int kt = ktiles - 2 < 0 ? 0 : ktiles - 2; kt < ktiles; ++kt) ktile(kt, F{}, F{});
+  }
   }
   // the last MFMAs' results -> the epilogue's v_accvgpr_read: XDL write -> read wait states
   // (hipcc pads nothing after asm); the empty "+a" statements order every read after the pad
@@ -690,14 +767,17 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
 }  // namespace
 }  // namespace ttdk
 
-// TTD_G4_SCHED: main-loop form. 2 (default) = one tile per workgroup, hand-ordered SCHED 2;
+// TTD_G4_SCHED: main-loop form. 3 (default) = one tile per workgroup, hand-ordered, the stage
+// released in two halves (3 barriers per K-tile, every DMA piece >= 132 MFMAs to land): same box,
+// interleaved, tools/g4_bench.py: 8192^3 1516 vs 1435 TF/s (SCHED 2), hipBLASLt 1578; BERT qkv
+// 1129 vs 1086, ffn2 1330 vs 1283, ffn1 dgrad 1322 vs 1297 TF/s; 2 = the two-barrier SCHED 2;
 // 30 = the persistent SCHED-2 kernel (gemm4p, next tile's DMA under this tile's epilogue);
 // 0 = the compiler-scheduled one-tile loop (oracle). With the branch-free steady loop (same box,
 // tools/g4_bench.py): 8192^3 1515 (2) vs 1301 (30) TF/s, hipBLASLt 1650; BERT-Large step
 // 154.8 / 156.2 vs 158.7 ms. (Measured and removed, round 5: all 16 DMA pieces in phase 1a,
 // one barrier per K-tile, a VGPR-staged 32x32x16 form, in-kernel phase stamps — git history.)
 static int& g4_sched() {
-  static int v = ttdk::getenv_int("TTD_G4_SCHED", 2);
+  static int v = ttdk::getenv_int("TTD_G4_SCHED", 3);
   return v;
 }
 static int g4_cus() { return ttdk::big::device_cus(); }
@@ -773,6 +853,12 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
       case 2: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
+      case 3: if (K >= 128) {                                                                              \
+          hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 3>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb,  \
+                             pe, M, N, K, tm, tn, group); break;                                              \
+        }                                                                                                   \
+        hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb,    \
+                           pe, M, N, K, tm, tn, group); break;                                                \
       case 30: {                                                                                          \
         const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
         if (grid < 8 || tm * tn <= g4_cus()) { /* one tile per workgroup: nothing to overlap */           \

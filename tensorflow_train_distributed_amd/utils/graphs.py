@@ -158,6 +158,9 @@ class SegmentedCapture:
         self.n_ev = 0
         self.tail = {}      # stream -> event recorded at the end of its last closed segment
         self.seg_index = 0  # segments closed so far (a mark remembers the one it was recorded in)
+        # stream -> streams whose record nodes in the CURRENT batch of segments it waits on (forks):
+        # the batch is launched in an order where every such record precedes its wait
+        self.deps = {}
 
     # -- capture bookkeeping
     def _begin(self, s):
@@ -169,9 +172,29 @@ class SegmentedCapture:
             g.capture_begin(pool=self.pools[key], capture_error_mode="relaxed")
         self.cur[key] = (s, g)
 
-    def _end_all(self):
+    def _launch_order(self):
+        """Streams of the current batch, main first, then every stream after the streams its
+        fork waits read records from. Insertion order alone is wrong when a stream that began
+        early (e.g. the communicator stream, forked from main for the first bucket) later waits
+        on a stream that began after it (the weight-gradient stream, for the next bucket): its
+        segment would be launched before the record it waits for, and the wait would pair with
+        the previous replay's record (the rehearsal's replicas diverged that way)."""
         main_key = self.main.cuda_stream
-        order = [main_key] + [k for k in self.cur if k != main_key]
+        keys = [main_key] + [k for k in self.cur if k != main_key]
+        placed, order = set(), []
+        while len(order) < len(keys):
+            for k in keys:
+                if k not in placed and all(d in placed or d not in self.cur for d in self.deps.get(k, ())):
+                    order.append(k)
+                    placed.add(k)
+                    break
+            else:
+                raise RuntimeError("segmented capture: cyclic fork dependencies between streams in one segment")
+        return order
+
+    def _end_all(self):
+        order = self._launch_order()
+        main_key = self.main.cuda_stream
         for k in order:
             if k not in self.cur:
                 continue
@@ -186,6 +209,7 @@ class SegmentedCapture:
             with torch.cuda.stream(s):
                 g.capture_end()
             self.segments.append((s, g))
+        self.deps = {}
         self.seg_index += 1
 
     def _event(self):
@@ -202,6 +226,8 @@ class SegmentedCapture:
         ev = self._event()
         _add_event_node(src, ev, wait=False)
         _add_event_node(dst, ev, wait=True)
+        if src.cuda_stream != dst.cuda_stream:
+            self.deps.setdefault(dst.cuda_stream, set()).add(src.cuda_stream)
 
     def join(self, dst, src):
         if dst.cuda_stream != self.main.cuda_stream:

@@ -17,12 +17,14 @@ import torch  # noqa: E402
 from tensorflow_train_distributed_amd.ops import kernels as K  # noqa: E402
 
 
-def timeit(fn, n=20):
+def timeit(fn, n=20, pre=None):
     fn()
     torch.cuda.synchronize()
     ts = []
     for _ in range(n):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if pre is not None:
+            pre()  # a producer that has just written the pass's input (as in the training step)
         a.record()
         fn()
         b.record()
@@ -35,10 +37,15 @@ def timeit(fn, n=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--after-write", action="store_true",
+                    help="re-write the input right before every timed pass (a producer kernel in front)")
+    ap.add_argument("--shapes", default="", help="comma list of HWxC, e.g. 28x128,56x64")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     N = a.batch
     shapes = [(56, 256), (56, 64), (28, 512), (28, 128), (14, 1024), (14, 256), (7, 2048), (7, 512)]
+    if a.shapes:
+        shapes = [tuple(int(v) for v in s_.split("x")) for s_ in a.shapes.split(",")]
     print("%-14s %-28s %9s %8s %8s" % ("shape", "pass", "us", "GB", "TB/s"))
     for hw, C in shapes:
         M = N * hw * hw
@@ -52,6 +59,8 @@ def main():
         dz = torch.empty_like(y)
         mask = torch.empty(M * C // 8, dtype=torch.uint8, device=dev)
         e = M * C
+        src = torch.randn(M, C, device=dev).bfloat16() if a.after_write else None
+        pre = (lambda: y.copy_(src)) if a.after_write else None
         cases = [
             ("copy", lambda: out.copy_(y), 4 * e),
             ("apply relu+mask", lambda: K.bn_apply(y, sc, sh, relu=True, out=out, mask=mask), 4 * e + e // 8),
@@ -65,9 +74,9 @@ def main():
              6 * e + e // 8),
         ]
         for name, fn, nbytes in cases:
-            us = timeit(fn)
+            us = timeit(fn, pre=pre)
             print("%-14s %-28s %9.1f %8.3f %8.2f" % ("%dx%d" % (M, C), name, us, nbytes / 1e9, nbytes / us / 1e6))
-        del y, r, g, out, dz, mask
+        del y, r, g, out, dz, mask, src
         torch.cuda.empty_cache()
 
 

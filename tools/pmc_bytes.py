@@ -3,7 +3,14 @@
 (FETCH_SIZE, WRITE_SIZE; KB per dispatch). The step = dispatches from the last stem kernel on.
 With a kernel-trace run of the same command (third argument), each kernel's time in that step
 and its achieved bandwidth (bytes / time) against a 6 TB/s line.
-usage: pmc_bytes.py <fetch_dir> <write_dir> [<trace_dir>]"""
+usage: pmc_bytes.py <fetch_dir> <write_dir> [<trace_dir>]
+
+Calibration (gfx950, rocprofv3 derived counters): FETCH_SIZE reports HALF the bytes a streaming
+read moves — a 205.5 MB device copy (hipMemcpy kernel, __amd_rocclr_copyBuffer) and the BN
+apply pass over a 205.5 MB tensor both read back ~100 MB, the fp32 -> bf16 cast of a 411 MB
+tensor 201 MB, while WRITE_SIZE matches the bytes written (201 MB for the copy, 213 MB for the
+apply with its ReLU bit mask) — profiles/r6_pmc_bytes_calibration.txt. The reads here are
+therefore FETCH_SIZE x FETCH_SCALE (2)."""
 import csv
 import glob
 import re
@@ -30,7 +37,8 @@ def short(n):
     return n.split("(")[0][:100]
 
 
-fe = load(sys.argv[1], "FETCH_SIZE")
+FETCH_SCALE = 2.0
+fe = [(d, n, v * FETCH_SCALE) for d, n, v in load(sys.argv[1], "FETCH_SIZE")]
 wr = load(sys.argv[2], "WRITE_SIZE")
 tot = defaultdict(lambda: [0.0, 0.0, 0])
 for _, n, v in fe:
@@ -48,7 +56,7 @@ if len(sys.argv) > 3:
     for r in rows[idx[-1]:] if idx else rows:
         tus[short(r["Kernel_Name"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 T = sum(tus.values())
-print("step HBM traffic: fetch %.1f GB, write %.1f GB, total %.1f GB (%d dispatches)%s"
+print("step HBM traffic (reads = FETCH_SIZE x %g, calibrated): fetch" % FETCH_SCALE + " %.1f GB, write %.1f GB, total %.1f GB (%d dispatches)%s"
       % (F, W, F + W, len(fe), ", kernel time %.1f ms -> %.2f TB/s average" % (T / 1e3, (F + W) / T * 1e3) if T else ""))
 print("%-100s %5s %9s %9s %9s %7s %s" % ("kernel", "n", "fetch GB", "write GB", "time us", "TB/s", "vs 6 TB/s"))
 for k, v in sorted(tot.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))[:60]:
