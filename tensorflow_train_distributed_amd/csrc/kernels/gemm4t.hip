@@ -46,10 +46,7 @@ namespace {
 namespace g4t {
 
 constexpr int T = 256;
-constexpr int OPB = 64 * 512;    // one operand's K-tile image: 64 k-rows x 256 bf16 columns
-constexpr int SB = 2 * OPB;      // A stages at 0 / OPB, B stages at SB / SB + OPB
-constexpr int SMEM = 4 * OPB;    // 128 KB
-constexpr int SLAB = 256 * 256;  // floats of one split's partial tile
+constexpr int OPB = 64 * 512;    // the B operand's K-tile image: 64 k-rows x 256 bf16 columns
 constexpr int kLgkm0 = 0xC07F;   // s_waitcnt encoding: lgkmcnt(0), vmcnt / expcnt not waited
 
 typedef __attribute__((address_space(3))) char lds_char_t;
@@ -178,20 +175,47 @@ __device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int gro
   tn = r / gm;
 }
 
-// fragment read order of a K-step (first use in the a-major MFMA sweep): 0: A0, 1..8: B0..B7,
-// 9..15: A1..A7; two transposed reads (k-rows +0..3, +4..7 of each lane group) per fragment
-constexpr bool fr_is_a(int r) { return r == 0 || r >= 9; }
-constexpr int fr_blk(int r) { return r == 0 ? 0 : (r <= 8 ? r - 1 : r - 8); }
+// Tile geometry: BM x 256 output tiles, BM = 256 (2 x 2 waves of 128 x 128) or 128 (2 x 2 waves of
+// 64 x 128: the weight gradients with 128 output rows — ResNet stage-3 c1 / 3x3 convs — no longer
+// pay a half-empty 256-row tile). A image: 64 k-rows x BM columns (rows of 2 BM bytes, the 32-B
+// slot XOR of the B image), B image: 64 k-rows x 256 columns.
+template <int BM>
+struct Geo {
+  static_assert(BM == 256 || BM == 128, "256- or 128-row tiles");
+  static constexpr int NA = BM / 32;        // A fragments (16-row blocks) per wave
+  static constexpr int NB = 8;              // B fragments per wave
+  static constexpr int NF = NA + NB;
+  static constexpr int AROW = BM * 2;       // bytes per A k-row
+  static constexpr int ACPR = AROW / 16;    // 16-B chunks per A k-row
+  static constexpr int ARPP = 256 / ACPR;   // A k-rows per DMA piece (one 16-B chunk per lane)
+  static constexpr int PA = 64 / ARPP;      // A DMA pieces per K-tile
+  static constexpr int OPA = 64 * AROW;     // A image bytes
+  static constexpr int SB = 2 * OPA;        // B stages at SB / SB + OPB
+  static constexpr int SMEMB = SB + 2 * OPB;
+  static constexpr int SLABB = BM * 256;    // floats of one split's partial tile
+  static constexpr int NMF = NA * NB;       // MFMAs per K-step and wave
+  static constexpr int NQ = PA + 8;         // DMA pieces per K-tile
+};
 
-template <bool RS, bool GB>
+// fragment read order of a K-step (first use in the a-major MFMA sweep): 0: A0, 1..NB: B0..B(NB-1),
+// NB+1..: A1..; two transposed reads (k-rows +0..3, +4..7 of each lane group) per fragment
+template <int NA, int NB>
+constexpr bool fr_is_a(int r) { return r == 0 || r > NB; }
+template <int NA, int NB>
+constexpr int fr_blk(int r) { return r == 0 ? 0 : (r <= NB ? r - 1 : r - NB); }
+
+template <bool RS, bool GB, int BM = 256>
 __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, int M, int N, int K,
                                                      int tiles_m, int tiles_n, int splits, int kt_per,
                                                      float* __restrict__ ws, float* __restrict__ out, int beta,
                                                      float alpha, int* __restrict__ ctr, float* __restrict__ rsw,
                                                      float* __restrict__ rowsum, Gather G, long long b_bytes) {
+  using Gm = Geo<BM>;
+  constexpr int NA = Gm::NA, NB = Gm::NB, NF = Gm::NF, OPA = Gm::OPA, SBO = Gm::SB;
+  static_assert(!RS || BM == 256, "bias row sums on the 256-row tile");
   // 1 KB aligned: the read bases' bits 5..9 are the lane's own, so a column block is one XOR
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM + 16];
+  __shared__ __attribute__((aligned(1024))) char smem[Gm::SMEMB + 16];
   // the epilogue's arguments into SGPRs now: loaded lazily behind the main loop's first K-tile,
   // a pending scalar load at the loop header makes hipcc's LDS-read waits there lgkmcnt(0)
   // (scalar loads complete out of order)
@@ -203,7 +227,7 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   const int split = w / tiles, t = w - split * tiles;
   int tm, tn;
   tile_of(t, tiles_m, tiles_n, 8, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
+  const int m0 = tm * BM, n0 = tn * 256;
   const int kt0 = split * kt_per;
   const int nk = min(kt_per, K / 64 - kt0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -214,14 +238,28 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
 
   lds_char_t* const lds = (lds_char_t*)smem;
   // per-lane read base of column block 0 of the wave's A / B columns per stage; block j is
-  // base ^ (32 j) (the slot XOR: 32 (j ^ f) = 32 j ^ 32 f), K-step and half are immediates
-  // (s * 16384 + h * 2048)
+  // base ^ (32 j): the wave's first 32-B slot s0 is a multiple of its block count, so the
+  // physical slot (s0 + j) ^ f = (s0 ^ f) ^ j; K-step and half are immediates
   const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
-  const uint32_t lanep = static_cast<uint32_t>((8 * g + q) * 512 + 8 * p + 32 * f);
-  const uint32_t bA0 = sb + lanep + wm * 256, bB0 = sb + SB + lanep + wn * 256;
+  const uint32_t krow = static_cast<uint32_t>(8 * g + q);
+  const uint32_t bA0 = sb + krow * Gm::AROW + 8 * p + 32 * ((wm * NA) ^ f);
+  const uint32_t bB0 = sb + SBO + krow * 512 + 8 * p + 32 * ((wn * 8) ^ f);
   const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
-  LoadMN la, lb;
-  la.init(A, lda, K, M, m0, tid);
+  // A loader: piece i of thread tid = A k-row i * ARPP + tid / ACPR, physical chunk tid % ACPR
+  ttd_i32x4_t srd_a = make_srd(A, static_cast<uint32_t>(static_cast<long long>(K) * lda * 2));
+  uint32_t voff_a[2];
+  {
+    const int pc = tid % Gm::ACPR, r0 = tid / Gm::ACPR;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = i * Gm::ARPP + r0;
+      const int fr = (r & 3) | (((r >> 3) & 1) << 2);
+      const int col = min(m0 + (((pc >> 1) ^ fr) << 4) + (pc & 1) * 8, M - 8);
+      voff_a[i] = static_cast<uint32_t>((static_cast<long long>(r0) * lda + col) * 2);
+    }
+  }
+  const int arow_step = static_cast<int>(lda * 2 * Gm::ARPP);  // bytes per A piece's k-rows
+  LoadMN lb;
   GCol gc;
   uint32_t gv[8];  // GB: this lane's source offsets of the 8 B pieces of the next K-tile to load
   if constexpr (GB) {
@@ -245,8 +283,8 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   };
   const int kstride_a = static_cast<int>(lda * 128), kstride_b = static_cast<int>(ldb * 128);  // bytes per K-tile
 
-  f32x4_t acc[8][8];
-  ttd_s16x4_t fl[2][16], fh[2][16];  // [set][fragment: 0..7 A, 8..15 B] low / high k halves
+  f32x4_t acc[NA][NB];
+  ttd_s16x4_t fl[2][NF], fh[2][NF];  // [set][fragment: 0..NA-1 A, NA.. B] low / high k halves
   f32x4_t rsacc[4];
   bf16x8_t ones;
   if constexpr (RS) {
@@ -255,50 +293,59 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
     ones = __builtin_bit_cast(bf16x8_t, ttd_i32x4_t{0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80});
   }
 
-  // read r (0..31) of K-step S of the image in stage st into fragment set SET
+  // read r (0 .. 2 NF - 1) of K-step S of the image in stage st into fragment set SET
   auto rd1 = [&](auto R, auto S, int st, auto SET) {
     constexpr int r = decltype(R)::value, s = decltype(S)::value, set = decltype(SET)::value;
-    constexpr int fr = r / 2, h = r % 2, blk = fr_blk(fr);
-    constexpr int imm = s * 16384 + h * 2048;
-    const uint32_t base = (fr_is_a(fr) ? bA0 : bB0) + st * OPB;
+    constexpr int fr = r / 2, h = r % 2, blk = fr_blk<NA, NB>(fr);
+    constexpr bool isa = fr_is_a<NA, NB>(fr);
+    constexpr int imm = isa ? s * 32 * Gm::AROW + h * 4 * Gm::AROW : s * 16384 + h * 2048;
+    const uint32_t base = isa ? bA0 + st * OPA : bB0 + st * OPB;
     const ttd_s16x4_t v = trd((const lds_char_t*)(uintptr_t)((blk ? (base ^ (32u * blk)) : base) + imm));
-    constexpr int slot = fr_is_a(fr) ? blk : 8 + blk;
+    constexpr int slot = isa ? blk : NA + blk;
     if constexpr (h == 0) fl[set][slot] = v;
     else fh[set][slot] = v;
   };
-  // LDS base of piece q (0..7 A, 8..15 B) in stage st; pieces go out in the order (stage st:
-  // 0..15), (stage st ^ 1: 0..15), ..., each setting M0 for its successor
-  auto m0_of = [&](int q, int st) {
-    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-        static_cast<int>(ldsw + (q < 8 ? 0 : SB) + st * OPB + (q & 7) * 4096)));
+  // LDS base of piece q (0..PA-1 A, PA.. B) in stage st; pieces go out in the order (stage st:
+  // all), (stage st ^ 1: all), ..., each setting M0 for its successor
+  auto m0_of = [&](int qq, int st) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
+        ldsw + (qq < Gm::PA ? st * OPA + qq * 4096 : SBO + st * OPB + (qq - Gm::PA) * 4096))));
   };
   auto dma1 = [&](auto Q, int st, int kt) {  // piece q of K-tile kt into stage st (M0 = its base)
-    constexpr int qq = decltype(Q)::value, i = qq & 7;
-    const uint32_t next = qq < 15 ? m0_of(qq + 1, st) : m0_of(0, st ^ 1);
-    if constexpr (GB && qq >= 8) {
-      dma_chain(gv[i], lb.srd, 0, next);
+    constexpr int qq = decltype(Q)::value;
+    const uint32_t next = qq < Gm::NQ - 1 ? m0_of(qq + 1, st) : m0_of(0, st ^ 1);
+    if constexpr (qq < Gm::PA) {
+      dma_chain(voff_a[qq & 1], srd_a, (kt0 + kt) * kstride_a + qq * arow_step, next);
     } else {
-      const LoadMN& L = qq < 8 ? la : lb;
-      dma_chain(L.voff[i & 1], L.srd, (kt0 + kt) * (qq < 8 ? kstride_a : kstride_b) + i * L.row8, next);
+      constexpr int i = qq - Gm::PA;
+      if constexpr (GB) dma_chain(gv[i], lb.srd, 0, next);
+      else dma_chain(lb.voff[i & 1], lb.srd, (kt0 + kt) * kstride_b + i * lb.row8, next);
     }
   };
   auto fa = [&](int set, int a) { return cat(fl[set][a], fh[set][a]); };
-  auto fb = [&](int set, int b) { return cat(fl[set][8 + b], fh[set][8 + b]); };
+  auto fb = [&](int set, int b) { return cat(fl[set][NA + b], fh[set][NA + b]); };
 
-  // HAS2 (K-tile kt + 2 exists) is compile-time: no branch around the 16 DMA pieces in the
-  // steady-state loop
+  // HAS2 (K-tile kt + 2 exists) is compile-time: no branch around the DMA pieces in the
+  // steady-state loop. Phases (MFMA counts for BM = 256 / 128):
+  //   0  (64 / 32, K-step 0)       | the 2 NF reads of K-step 1, spread evenly
+  //   1a (32 / 16, K-step 1 first half) | the A pieces of K-tile kt + 2 into the freed stage
+  //   1b (32 / 16, second half)   | the B pieces of kt + 2 | the 2 NF reads of K-tile kt + 1, K-step 0
+  constexpr int NR = 2 * NF, H0 = Gm::NMF, H1 = Gm::NMF / 2;
   auto ktile = [&](int kt, auto first, auto has2c) {
     constexpr bool FIRST = decltype(first)::value;
     constexpr bool has2 = decltype(has2c)::value;
     const int st = kt & 1;
     const bool rs_on = RS && ((kt0 + kt) % tiles_n == tn);
-    // phase 0: K-step 0 (set 0) | reads of K-step 1 into set 1
-    static_for<64>([&](auto I) {
+    // phase 0: K-step 0 (set 0) | reads of K-step 1 into set 1 (read j before MFMA j * H0 / NR)
+    static_for<H0>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, std::integral_constant<int, 1>{}, st, std::integral_constant<int, 1>{});
-      mfma_acc<FIRST>(acc[i / 8][i % 8], fa(0, i / 8), fb(0, i % 8));
+      static_for<NR>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (j * H0 / NR == i) rd1(J, std::integral_constant<int, 1>{}, st, std::integral_constant<int, 1>{});
+      });
+      mfma_acc<FIRST>(acc[i / NB][i % NB], fa(0, i / NB), fb(0, i % NB));
       // GB: the gathered B offsets of K-tile kt + 2 (DMA'd in phase 1b), between the MFMAs
-      if constexpr (GB && has2 && i % 8 == 5) gather_piece(kt + 2, i / 8);
+      if constexpr (GB && has2 && i % (H0 / 8) == (H0 / 8) - 3) gather_piece(kt + 2, i / (H0 / 8));
     });
     if constexpr (RS) {
       if (rs_on) {  // (wave-uniform branches: no VALU-selected operand)
@@ -318,11 +365,11 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
     __builtin_amdgcn_s_waitcnt(kLgkm0);  // (a real s_waitcnt: hipcc's own wait tracking sees it)
     asm volatile("s_barrier" ::: "memory");
     // phase 1a: first half of K-step 1 | A pieces of K-tile kt + 2 into the freed stage
-    static_for<32>([&](auto I) {
+    static_for<H1>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      if constexpr (i % 4 == 0)
-        if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
-      mfma_acc<false>(acc[i / 8][i % 8], fa(1, i / 8), fb(1, i % 8));
+      if constexpr (i % (H1 / Gm::PA) == 0)
+        if constexpr (has2) dma1(std::integral_constant<int, i / (H1 / Gm::PA)>{}, st, kt + 2);
+      mfma_acc<false>(acc[i / NB][i % NB], fa(1, i / NB), fb(1, i % NB));
     });
     if constexpr (RS) {
       if (rs_on) {  // (wave-uniform branches: no VALU-selected operand)
@@ -339,16 +386,19 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
         }
       }
     }
-    if constexpr (has2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (has2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::PA) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
     // phase 1b: second half of K-step 1 | B pieces of kt + 2 | reads of K-tile kt + 1, K-step 0
-    static_for<32>([&](auto I) {
+    static_for<H1>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      if constexpr (i % 4 == 1)
-        if constexpr (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
-      rd1(std::integral_constant<int, i>{}, std::integral_constant<int, 0>{}, st ^ 1, std::integral_constant<int, 0>{});
-      mfma_acc<false>(acc[4 + i / 8][i % 8], fa(1, 4 + i / 8), fb(1, i % 8));
+      if constexpr (i % (H1 / 8) == (H1 / 8 > 1 ? 1 : 0))
+        if constexpr (has2) dma1(std::integral_constant<int, Gm::PA + i / (H1 / 8)>{}, st, kt + 2);
+      static_for<NR>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (j * H1 / NR == i) rd1(J, std::integral_constant<int, 0>{}, st ^ 1, std::integral_constant<int, 0>{});
+      });
+      mfma_acc<false>(acc[NA / 2 + i / NB][i % NB], fa(1, NA / 2 + i / NB), fb(1, i % NB));
     });
   };
 
@@ -356,14 +406,14 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   m0_init(m0_of(0, 0));
   if constexpr (GB)
     for (int i = 0; i < 8; ++i) gather_piece(0, i);
-  static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
+  static_for<Gm::NQ>([&](auto Q) { dma1(Q, 0, 0); });
   if constexpr (GB)
     if (nk > 1)
       for (int i = 0; i < 8; ++i) gather_piece(1, i);
-  static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
+  static_for<Gm::NQ>([&](auto Q) { dma1(Q, 1, 1); });
   __builtin_amdgcn_s_waitcnt(kLgkm0);
-  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-  static_for<32>([&](auto R) { rd1(R, std::integral_constant<int, 0>{}, 0, std::integral_constant<int, 0>{}); });
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(Gm::NQ) : "memory");
+  static_for<NR>([&](auto R) { rd1(R, std::integral_constant<int, 0>{}, 0, std::integral_constant<int, 0>{}); });
   if (nk >= 3) {
     ktile(0, std::true_type{}, std::true_type{});
     for (int kt = 1; kt < nk - 2; ++kt) ktile(kt, std::false_type{}, std::true_type{});
@@ -375,9 +425,9 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+    for (int b = 0; b < NB; ++b) asm volatile("" : "+a"(acc[a][b]));
 
   // bias-gradient partials: rsw[(split * tiles_n + tn) * M + m], summed below by the last of the
   // splits * tiles_n workgroups of tile row tm to arrive
@@ -390,42 +440,42 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
       }
     }
   }
-  // acc[a][b] = C[m0 + wm*128 + a*16 + i16][n0 + wn*128 + b*16 + 4g .. +3]
-  const bool whole = m0 + 256 <= M && n0 + 256 <= N;
+  // acc[a][b] = C[m0 + wm*(BM/2) + a*16 + i16][n0 + wn*128 + b*16 + 4g .. +3]
+  const bool whole = m0 + BM <= M && n0 + 256 <= N;
   auto store = [&](int a, int b, f32x4_t v) {
-    const int m = m0 + wm * 128 + a * 16 + i16, n = n0 + wn * 128 + b * 16 + 4 * g;
+    const int m = m0 + wm * (BM / 2) + a * 16 + i16, n = n0 + wn * 128 + b * 16 + 4 * g;
     if (whole || (m < M && n < N)) {
       f32x4_t* o = reinterpret_cast<f32x4_t*>(out + static_cast<long long>(m) * N + n);
       if (beta) v += *o;
       *o = v;
     }
   };
-  // rows a..7 re-pinned before row a is read: hipcc would otherwise move all 256 accumulator
+  // rows a..NA-1 re-pinned before row a is read: hipcc would otherwise move all accumulator
   // reads to the top (VGPR spills)
   auto pin_from = [&](int a0) {
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < NA; ++a)
       if (a >= a0)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+        for (int b = 0; b < NB; ++b) asm volatile("" : "+a"(acc[a][b]));
   };
-  const long long lin = static_cast<long long>(wave * 64) * 64 * 4 + lane * 4;  // + (a * 8 + b) * 256
+  const long long lin = static_cast<long long>(wave) * NA * NB * 256 + lane * 4;  // + (a * NB + b) * 256
   if (splits == 1) {
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
+    for (int a = 0; a < NA; ++a) {
       pin_from(a);
 #pragma unroll
-      for (int b = 0; b < 8; ++b) store(a, b, acc[a][b] * alpha);
+      for (int b = 0; b < NB; ++b) store(a, b, acc[a][b] * alpha);
     }
     if constexpr (!RS) return;
   } else {
     // split-K: partial tile lane-linear into this split's slab (stored straight from the AGPRs)
-    float* slab = ws + static_cast<long long>(split * tiles + t) * SLAB + lin;
+    float* slab = ws + static_cast<long long>(split * tiles + t) * Gm::SLABB + lin;
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int b = 0; b < 8; ++b)
-        asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(slab + (a * 8 + b) * 256), "a"(acc[a][b])
+      for (int b = 0; b < NB; ++b)
+        asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(slab + (a * NB + b) * 256), "a"(acc[a][b])
                      : "memory");
   }
   // release the partials, count arrivals: per tile (ctr[t], splits) and per tile row for the
@@ -433,7 +483,7 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __threadfence();
   __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem + SMEM);
+  int* flag = reinterpret_cast<int*>(smem + Gm::SMEMB);
   if (tid == 0) {
     flag[0] = splits > 1 && atomicAdd(ctr + t, 1) == splits - 1;
     flag[1] = RS && atomicAdd(ctr + tiles + tm, 1) == splits * tiles_n - 1;
@@ -456,36 +506,36 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   if (!last_tile) return;
   // last split of this tile: sum the partials in split order, its own re-read from the slab it
   // just wrote (deterministic whoever is last; no accumulator stays live through the fold)
-  const float* src0 = ws + static_cast<long long>(t) * SLAB + lin;
-  const long long sstride = static_cast<long long>(tiles) * SLAB;
-  // (one workgroup streams splits x 256 KB: the loads of 4 splits are issued before their adds —
-  // 32 x 16 B in flight per lane instead of 8 — the adds stay in split order)
+  const float* src0 = ws + static_cast<long long>(t) * Gm::SLABB + lin;
+  const long long sstride = static_cast<long long>(tiles) * Gm::SLABB;
+  // (one workgroup streams splits x 128 / 256 KB: the loads of 4 splits are issued before their
+  // adds — 32 x 16 B in flight per lane instead of 8 — the adds stay in split order)
 #pragma unroll 1
-  for (int a = 0; a < 8; ++a) {
-    f32x4_t v[8];
+  for (int a = 0; a < NA; ++a) {
+    f32x4_t v[NB];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) v[b] = *reinterpret_cast<const f32x4_t*>(src0 + (a * 8 + b) * 256);
+    for (int b = 0; b < NB; ++b) v[b] = *reinterpret_cast<const f32x4_t*>(src0 + (a * NB + b) * 256);
     int s = 1;
     for (; s + 4 <= splits; s += 4) {
-      f32x4_t x[4][8];
+      f32x4_t x[4][NB];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float* src = src0 + (s + u) * sstride + a * 8 * 256;
+        const float* src = src0 + (s + u) * sstride + a * NB * 256;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) x[u][b] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(src + b * 256));
+        for (int b = 0; b < NB; ++b) x[u][b] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(src + b * 256));
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) v[b] += x[u][b];
+        for (int b = 0; b < NB; ++b) v[b] += x[u][b];
     }
     for (; s < splits; ++s) {
-      const float* src = src0 + s * sstride + a * 8 * 256;
+      const float* src = src0 + s * sstride + a * NB * 256;
 #pragma unroll
-      for (int b = 0; b < 8; ++b) v[b] += *reinterpret_cast<const f32x4_t*>(src + b * 256);
+      for (int b = 0; b < NB; ++b) v[b] += *reinterpret_cast<const f32x4_t*>(src + b * 256);
     }
 #pragma unroll
-    for (int b = 0; b < 8; ++b) store(a, b, v[b] * alpha);
+    for (int b = 0; b < NB; ++b) store(a, b, v[b] * alpha);
   }
   if (tid == 0) ctr[t] = 0;  // ready for the next launch on this counter block
 }
@@ -497,6 +547,13 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
 static int g4t_enabled() {
   static const int v = ttdk::getenv_int("TTD_G4T", 1);
   return v;
+}
+
+// tile rows: 128 when the output has at most 128 rows (a 256-row tile would run half its MFMAs
+// on padding), else 256; the bias row sums (BERT) use the 256-row form. TTD_G4T_BM128=0: always 256.
+static int g4t_bm(int M, bool rowsum) {
+  static const int v = ttdk::getenv_int("TTD_G4T_BM128", 1);
+  return (v && !rowsum && M <= 128) ? 128 : 256;
 }
 
 // floats of workspace ttdk_gemm4t_wgrad needs: split partial tiles + bias-gradient partials;
@@ -512,8 +569,9 @@ TTDK_EXPORT long long ttdk_gemm4t_ws(int M, int N, int K, int splits) {
   splits = std::max(1, std::min(splits, ktiles / 2));
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);
+  // (sized for 256-row tiles: at least the 128-row form's need, and the bias row-sum form's)
   const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256);
-  return static_cast<long long>(splits) * tiles_m * tiles_n * g4t::SLAB + static_cast<long long>(splits) * tiles_n * M;
+  return static_cast<long long>(splits) * tiles_m * tiles_n * 256 * 256 + static_cast<long long>(splits) * tiles_n * M;
 }
 
 // dW[M,N] (+)= alpha * A^T . B, A [K][M] (lda), B [K][N] (ldb) bf16 MN-major, out fp32 contiguous
@@ -533,18 +591,22 @@ TTDK_EXPORT int ttdk_gemm4t_wgrad(const bf16_t* A, long long lda, const bf16_t* 
   splits = std::max(1, std::min(splits, ktiles / 2));
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);
-  const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
+  const int bm = g4t_bm(M, rowsum != nullptr);
+  const int tiles_m = ceil_div(M, bm), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
   int* ctr = nullptr;
   if (splits > 1 || rowsum) {
     ctr = big::tile_counters(st, tiles + tiles_m);
     if (!ctr || !ws) return hipErrorInvalidValue;
   }
-  float* rsw = rowsum ? ws + static_cast<long long>(splits) * tiles * g4t::SLAB : nullptr;
+  float* rsw = rowsum ? ws + static_cast<long long>(splits) * tiles * bm * 256 : nullptr;
   const dim3 grid(tiles * splits);
   const g4t::Gather G{};
   if (rowsum)
     hipLaunchKernelGGL((g4t::gemm4t_kernel<true, false>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
                        tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum, G, 0LL);
+  else if (bm == 128)
+    hipLaunchKernelGGL((g4t::gemm4t_kernel<false, false, 128>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K,
+                       tiles_m, tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum, G, 0LL);
   else
     hipLaunchKernelGGL((g4t::gemm4t_kernel<false, false>), grid, dim3(g4t::T), 0, st, A, lda, B, ldb, M, N, K, tiles_m,
                        tiles_n, splits, per, ws, out, beta, alpha, ctr, rsw, rowsum, G, 0LL);
@@ -590,7 +652,8 @@ TTDK_EXPORT int ttdk_conv_wgrad4t(const bf16_t* x, const bf16_t* dy, const TtdkC
   splits = std::max(1, std::min(splits, ktiles / 2));
   const int per = ceil_div(ktiles, splits);
   splits = ceil_div(ktiles, per);
-  const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
+  const int bm = g4t_bm(M, false);
+  const int tiles_m = ceil_div(M, bm), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
   int* ctr = nullptr;
   if (splits > 1) {
     ctr = big::tile_counters(st, tiles);
@@ -610,8 +673,13 @@ TTDK_EXPORT int ttdk_conv_wgrad4t(const bf16_t* x, const bf16_t* dy, const TtdkC
   magic_div(static_cast<unsigned>(G.PQ), &G.pq_m, &G.pq_s);
   magic_div(static_cast<unsigned>(G.Q), &G.q_m, &G.q_s);
   const long long xb = static_cast<long long>(g->N) * g->H * g->W * g->C * 2;
-  hipLaunchKernelGGL((g4t::gemm4t_kernel<false, true>), dim3(tiles * splits), dim3(g4t::T), 0, st, dy,
-                     static_cast<long long>(g->K), x, 0LL, M, N, K, tiles_m, tiles_n, splits, per, ws, dw, beta, 1.f,
-                     ctr, nullptr, nullptr, G, xb);
+  if (bm == 128)
+    hipLaunchKernelGGL((g4t::gemm4t_kernel<false, true, 128>), dim3(tiles * splits), dim3(g4t::T), 0, st, dy,
+                       static_cast<long long>(g->K), x, 0LL, M, N, K, tiles_m, tiles_n, splits, per, ws, dw, beta, 1.f,
+                       ctr, nullptr, nullptr, G, xb);
+  else
+    hipLaunchKernelGGL((g4t::gemm4t_kernel<false, true>), dim3(tiles * splits), dim3(g4t::T), 0, st, dy,
+                       static_cast<long long>(g->K), x, 0LL, M, N, K, tiles_m, tiles_n, splits, per, ws, dw, beta, 1.f,
+                       ctr, nullptr, nullptr, G, xb);
   return hipGetLastError();
 }

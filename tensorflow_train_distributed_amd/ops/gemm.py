@@ -831,6 +831,19 @@ _WGRAD4T = int(_os.environ.get("TTD_WGRAD4T", "1"))
 # standalone, cost 0.5 ms: profiles/r6_wgrad4t_step_ab.txt); 0: per shape (128 3x3, 256 1x1)
 _WGRAD4T_WGS = int(_os.environ.get("TTD_WGRAD4T_WGS", "128"))
 _WGRAD4T_MIN_KT = int(_os.environ.get("TTD_WGRAD4T_MIN_KT", "32"))
+# convs with fewer than 256 output channels (>= TTD_WGRAD4T_MINM) on the kernel's 128-row tile form
+# (gemm4t.hip g4t_bm): TTD_WGRAD4T_SMALL "c3" the filters larger than 1x1, "all" the 1x1 ones too,
+# "none" (default) the previous kernels. Measured (profiles/r6_wgrad4t_small_m.txt): the 128-row
+# form needs 37 % less CU time on the stage-3 3x3 weight gradients (77 vs 121 CU-ms at 128
+# workgroups) but holds each CU ~590 us; in the two-stream step the data-gradient chain waits
+# for those CUs (66.61 / 66.79 vs 66.54 / 66.67 ms), so it stays opt-in
+_WGRAD4T_SMALL = _os.environ.get("TTD_WGRAD4T_SMALL", "none")
+_WGRAD4T_MINM = int(_os.environ.get("TTD_WGRAD4T_MINM", "128"))
+
+
+def wgrad4t_rows(M: int) -> int:
+    """Output rows per tile of the 4-wave weight-gradient kernel (mirror of gemm4t.hip g4t_bm)."""
+    return 128 if (M <= 128 and _os.environ.get("TTD_G4T_BM128", "1") != "0") else 256
 
 
 def conv_wgrad4t_splits(g, target_blocks=None, min_ktiles=None):
@@ -840,7 +853,8 @@ def conv_wgrad4t_splits(g, target_blocks=None, min_ktiles=None):
     target = target_blocks or _WGRAD4T_WGS or (128 if g.R * g.S > 1 else 256)
     mk = _WGRAD4T_MIN_KT if min_ktiles is None else min_ktiles
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
-    tiles = -(-M // 256) * -(-N // 256)
+    bm = wgrad4t_rows(M)
+    tiles = -(-M // bm) * -(-N // 256)
     return max(1, min((K // 64) // mk, -(-target // tiles)))
 
 
@@ -849,9 +863,15 @@ def conv_wgrad4t_ok(g, mode=None) -> bool:
     own admission: C, K % 8, pixels % 64, operands < 2 GiB, no dilation)."""
     mode = _WGRAD4T if mode is None else mode
     M, N = g.K, g.R * g.S * g.C
-    if mode <= 0 or M < 256 or N < 128:
+    if mode <= 0 or N < 128:
         return False
-    if mode in (1, 3):
+    if M < 256:
+        if M < _WGRAD4T_MINM or mode == 3 and g.R * g.S == 1:
+            return False
+        if mode == 1 and (_WGRAD4T_SMALL == "none" or (_WGRAD4T_SMALL == "c3" and g.R * g.S == 1)
+                          or (g.R * g.S > 1 and N < 256)):
+            return False
+    elif mode in (1, 3):
         if g.R * g.S == 1 and (mode == 3 or N < 256 or M * N < 512 * 1024):
             return False
         if g.R * g.S > 1 and N < 256:

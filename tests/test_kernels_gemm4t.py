@@ -4,7 +4,8 @@ Pins the kernel that carries BERT's dense-layer weight gradients (the kernel gra
 tf.layers.dense, /root/reference/distribute_training.py:54,61, formed by compute_gradients at
 :152): dW = dy^T . x on MN-major operands with the split-K sum inside the launch, the fused bias
 gradient (column sums of dy), accumulate (beta) and alpha, at BERT-Large shapes and edge shapes
-(M, N not multiples of 256; row-strided operands)."""
+(M, N not multiples of 256; row-strided operands), and the 128-row tile form taken by outputs of at
+most 128 rows (ResNet stage-2/3 convs)."""
 import pytest
 import torch
 
@@ -17,7 +18,9 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("M,N,K,splits", [
     (256, 256, 128, 1), (256, 256, 1024, 4), (512, 768, 2048, 3), (264, 1000, 384, 2), (1000, 264, 640, 5),
-    (1024, 1024, 8192, 16), (3072, 1024, 8192, 4), (4096, 1024, 4096, 3), (8, 16, 128, 1)])
+    (1024, 1024, 8192, 16), (3072, 1024, 8192, 4), (4096, 1024, 4096, 3), (8, 16, 128, 1),
+    # <= 128 output rows: the 128-row tile form (gemm4t.hip g4t_bm)
+    (128, 512, 4096, 8), (64, 576, 2048, 4), (128, 1152, 1024, 3), (120, 264, 640, 2), (128, 256, 128, 1)])
 def test_gemm4t_vs_fp32(M, N, K, splits):
     from tensorflow_train_distributed_amd.ops import gemm as G
     torch.manual_seed(M + N + K + splits)
@@ -113,6 +116,11 @@ def _conv_wgrad_ref(x, dy, w_shape, stride, pad):
     (64, 9, 64, 256, 3, 1, 3),           # odd spatial size, C = 64 (four taps per 256 columns)
     (16, 12, 128, 264, 3, 2, 1),         # K not a multiple of 256, one split (576 pixels)
     (4, 8, 8, 256, 3, 1, 2),             # C = 8 (256 pixels): 32 taps of 8 channels per 256 columns
+    # 128-row tiles (<= 128 output channels): stage-3 c2 / block-1 c2 / c1, stage-2 c2 (batch 64)
+    (64, 28, 128, 128, 3, 1, None),
+    (64, 56, 128, 128, 3, 2, None),
+    (64, 28, 512, 128, 1, 1, None),
+    (64, 56, 64, 64, 3, 1, None),
 ])
 def test_conv_wgrad4t_vs_fp32(N, H, C, K, R, stride, splits):
     from tensorflow_train_distributed_amd.ops import gemm as G

@@ -23,7 +23,11 @@ SHAPES = [("s5_c2", 7, 512, 512, 3, 1), ("s5b1_c2", 14, 512, 512, 3, 2), ("s5_c1
           ("s5_c3", 7, 512, 2048, 1, 1), ("s5_cd", 14, 1024, 2048, 1, 2), ("s5b1_c1", 14, 1024, 512, 1, 1),
           ("s4_c2", 14, 256, 256, 3, 1), ("s4b1_c2", 28, 256, 256, 3, 2), ("s4_c1", 14, 1024, 256, 1, 1),
           ("s4_c3", 14, 256, 1024, 1, 1), ("s4_cd", 28, 512, 1024, 1, 2), ("s4b1_c1", 28, 512, 256, 1, 1),
-          ("s3_c3", 28, 128, 512, 1, 1), ("s3_cd", 56, 256, 512, 1, 2)]
+          ("s3_c3", 28, 128, 512, 1, 1), ("s3_cd", 56, 256, 512, 1, 2),
+          # fewer than 256 output channels: the 128-row tile form
+          ("s3_c2", 28, 128, 128, 3, 1), ("s3b1_c2", 56, 128, 128, 3, 2), ("s3_c1", 28, 512, 128, 1, 1),
+          ("s3b1_c1", 56, 256, 128, 1, 1), ("s2_c2", 56, 64, 64, 3, 1), ("s2_c1", 56, 256, 64, 1, 1)]
+ONLY = arg("--only", "")
 
 
 def timeit(fn, iters=10):
@@ -41,6 +45,8 @@ def timeit(fn, iters=10):
 def main():
     tot = {}
     for name, H, C, K, R, st in SHAPES:
+        if ONLY and not any(o in name for o in ONLY.split(",")):
+            continue
         pad = R // 2
         P = (H + 2 * pad - R) // st + 1
         x = (torch.rand((B, H, H, C), device="cuda") * 2 - 1).bfloat16()
@@ -49,6 +55,7 @@ def main():
         out = torch.empty(w, device="cuda")
         g = G.conv_geom(x.shape, w, (st, st), (pad, pad))
         arms = {}
+        cus = {"old": 256}  # (the previous kernels launch >= 256 workgroups on these shapes)
         old = G._WGRAD4T
         G._WGRAD4T = 0
         arms["old"] = lambda: G.conv_wgrad(x, dy, w, (st, st), (pad, pad), out=out)
@@ -57,6 +64,9 @@ def main():
                 sp = G.conv_wgrad4t_splits(g, target_blocks=wg)
                 arms["g4t@%d(s%d)" % (wg, sp)] = (lambda sp=sp: G.conv_wgrad4t(x, dy, w, (st, st), (pad, pad),
                                                                                out=out, splits=sp))
+                # CU-time of the launch (what it costs the data-gradient chain next to it)
+                bm = G.wgrad4t_rows(K)
+                cus[("g4t@%d(s%d)" % (wg, sp))] = min(256, -(-K // bm) * -(-(R * R * C) // 256) * sp)
         res = {k: [] for k in arms}
         for _ in range(ROUNDS):
             for k, f in arms.items():
@@ -68,7 +78,7 @@ def main():
             t = min(v)
             tot[k.split("@")[0]] = tot.get(k.split("@")[0], 0.0) + (t if "@" not in k or k.endswith(
                 "(s%d)" % G.conv_wgrad4t_splits(g, target_blocks=WGS[0])) else 0.0)
-            line += "  %s %7.1f us %5.0f TF/s" % (k, t, fl / t / 1e6)
+            line += "  %s %7.1f us %5.0f TF/s %5.1f CU-ms" % (k, t, fl / t / 1e6, t * cus.get(k, 256) / 1e3)
         print(line, flush=True)
         del x, dy, out
     print("totals (first wgs):", {k: round(v, 1) for k, v in tot.items()})
