@@ -260,8 +260,9 @@ __device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int gro
   tn = r / gm;
 }
 
-// SCHED 2: the production one-tile-per-workgroup loop (hand-ordered inline asm); SCHED 0: the
-// same schedule left to the compiler, kept as the A/B oracle of the hand ordering
+// SCHED 3: the production one-tile-per-workgroup loop (hand-ordered inline asm); SCHED 0: a
+// two-barrier schedule left to the compiler, kept as the A/B oracle of the hand ordering (and the
+// form of K = 64, a single K-tile)
 template <int EK, int SCHED>
 __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
@@ -369,14 +370,10 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   };
   for (int kt = 0; kt < ktiles; ++kt) ktile(kt, F{});
   } else {
-  // SCHED 2: the whole main loop as inline asm in a fixed issue order (hipcc grouped all 16
+  // hand-ordered: the whole main loop as inline asm in a fixed issue order (hipcc grouped all 16
   // fragment reads and all 16 DMA pieces of a phase in front of its MFMAs; with one wave per
-  // SIMD nothing else fills the MFMA pipe while they issue):
-  //   phase 0: one fragment read before every 4th MFMA, graduated lgkmcnt for the K-step-0
-  //            fragments still in flight (lgk0);
-  //   phase 1a: one DMA piece before every 4th MFMA; phase 1b: one DMA piece before every 4th
-  //            and one fragment read before every 2nd MFMA. LDS reads and DMA are counted by
-  //            hand (hipcc does not count asm).
+  // SIMD nothing else fills the MFMA pipe while they issue). LDS reads and DMA are counted by
+  // hand (hipcc does not count asm); the phases are described at the SCHED 3 loop below.
   const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
   uint32_t va[2][2], vb[2][2];  // [stage][K-step] fragment base addresses (block offsets immediate)
 #pragma unroll
@@ -410,7 +407,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   };
   // prologue: K-tiles 0 and 1, wait for 0, K-step-0 fragments of K-tile 0 (SCHED 3: K-tile kt
   // in stage (kt + ktiles) & 1, so that the last two K-tiles always sit in stages 0, 1)
-  const int st0 = SCHED == 3 ? (ktiles & 1) : 0;
+  const int st0 = ktiles & 1;
   m0_init(m0_of(0, st0));
   static_for<16>([&](auto Q) { dma1(Q, st0, 0); });
   if (ktiles > 1) {
@@ -419,10 +416,9 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  if constexpr (SCHED != 3) static_for<16>([&](auto R) { rd1(R, va[0][0], vb[0][0], fa[0], fb[0]); });
-  if constexpr (SCHED == 3) {
+  {
   // SCHED 3: the stage of K-tile kt is released in two halves, so the DMA of K-tile kt + 2 starts
-  // 32 MFMAs earlier than in SCHED 2 (every piece gets >= 132 MFMAs, ~2100 cycles, to land
+  // 32 MFMAs earlier than in the two-barrier loop (every piece gets >= 132 MFMAs, ~2100 cycles, to land
   // instead of >= 99) at the price of a third barrier; the stage index is compile-time (the
   // K-tiles go in pairs), so no per-K-tile selects of the fragment / DMA bases:
   //   A  (MFMAs  0-31, K-step 0): the 8 A fragments of K-step 1, one per 3 MFMAs;
@@ -493,51 +489,6 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   }
   ktile3(ktiles - 2, S0{}, F{});
   ktile3(ktiles - 1, S1{}, F{});
-  } else {
-  // HAS2 (K-tile kt + 2 exists) compile-time: no branch around the DMA pieces in the steady loop
-  auto ktile = [&](int kt, auto first, auto has2c) {
-    constexpr bool has2 = decltype(has2c)::value;
-    const bool has1 = kt + 1 < ktiles;
-    const int st = kt & 1;
-    // phase 0
-    static_for<64>([&](auto I) {
-      constexpr int i = decltype(I)::value, a = i / 8, b = i % 8;
-      if constexpr (i % 4 == 0) rd1(std::integral_constant<int, i / 4>{}, va[st][1], vb[st][1], fa[1], fb[1]);
-      if constexpr (i == 0 || need0(i) > need0(i - 1 < 0 ? 0 : i - 1))
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(lgk0(i)) : "memory");
-      mfma1(a, b, fa[0][a], fb[0][b], first);
-    });
-    {
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      // phase 1a: K-tile kt + 2 into this stage (the MFMA sequence is never duplicated per
-      // branch: with the MFMAs inside if / else copies hipcc allocated the accumulators
-      // differently per copy and shuffled them with unpadded v_accvgpr_mov between).
-      // 8 pieces here, 8 in phase 1b (all 16 in the first 32 MFMAs measured slower).
-      static_for<32>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        if constexpr (i % 4 == 0)
-          if constexpr (has2) dma1(std::integral_constant<int, i / 4>{}, st, kt + 2);
-        mfma1(i / 8, i % 8, fa[1][i / 8], fb[1][i % 8], F{});
-      });
-      if constexpr (has2) {
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      asm volatile("s_barrier" ::: "memory");
-      // phase 1b: K-step-0 fragments of K-tile kt + 1 (read unconditionally: past the last
-      // K-tile they are never used)
-      static_for<32>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        if constexpr (i % 4 == 1)
-          if constexpr (has2) dma1(std::integral_constant<int, 8 + i / 4>{}, st, kt + 2);
-        if constexpr (i % 2 == 0) rd1(std::integral_constant<int, i / 2>{}, va[st ^ 1][0], vb[st ^ 1][0], fa[0], fb[0]);
-        mfma1(4 + i / 8, i % 8, fa[1][4 + i / 8], fb[1][i % 8], F{});
-      });
-    }
-  };
-  for (int kt = 0; kt < ktiles - 2; ++kt) ktile(kt, F{}, Tr{});
-  for (int kt = ktiles - 2 < 0 ? 0 : ktiles - 2; kt < ktiles; ++kt) ktile(kt, F{}, F{});
   }
   }
   // the last MFMAs' results -> the epilogue's v_accvgpr_read: XDL write -> read wait states
@@ -554,8 +505,8 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
 }
 
 // ============================================================================================
-// gemm4p: the production form — persistent 4-wave 256 x 256 kernel on the SCHED 2 main loop
-// (16x16x32 MFMAs, LDS-DMA staging, 2 barriers per K-tile; 64 % MFMA busy at 8192^3 with 12.8 %
+// gemm4p: the persistent 4-wave 256 x 256 kernel (TTD_G4_SCHED=30, opt-in) on the round-5
+// two-barrier main loop (16x16x32 MFMAs, LDS-DMA staging; 61 % MFMA busy at 8192^3 with 13.8 %
 // of wave cycles waiting, profiles/r5_gemm4_pmc_8192.txt). One workgroup per CU walks its
 // XCD's tile range (xcd_remap order, column-major blocks of `group` tile rows): as soon as a
 // tile's last K-tile is consumed, the next tile's first two K-tiles are DMA'd into the idle
@@ -650,7 +601,8 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
     static_for<16>([&](auto Q) { dma1(Q, 0, 0); });
     if (ktiles > 1) static_for<16>([&](auto Q) { dma1(Q, 1, 1); });
   };
-  // one K-tile of the SCHED 2 schedule (see gemm4w_kernel); FIRST: phase 0 with C = 0; HAS2:
+  // one K-tile of the two-barrier schedule (phase 0: K-step 0 | K-step-1 fragment reads; 1a: DMA
+  // of K-tile kt + 2, A half; 1b: B half + K-step-0 reads of kt + 1); FIRST: phase 0 with C = 0; HAS2:
   // K-tile kt + 2 exists (compile-time: the steady-state loop body has no branch around its 16
   // DMA pieces — as run-time tests they were 16 scalar branches per K-tile)
   auto ktile = [&](int kt, auto first, auto has2c) {
@@ -769,8 +721,9 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
 
 // TTD_G4_SCHED: main-loop form. 3 (default) = one tile per workgroup, hand-ordered, the stage
 // released in two halves (3 barriers per K-tile, every DMA piece >= 132 MFMAs to land): same box,
-// interleaved, tools/g4_bench.py: 8192^3 1516 vs 1435 TF/s (SCHED 2), hipBLASLt 1578; BERT qkv
-// 1129 vs 1086, ffn2 1330 vs 1283, ffn1 dgrad 1322 vs 1297 TF/s; 2 = the two-barrier SCHED 2;
+// interleaved, tools/g4_bench.py: 8192^3 1516 vs 1435 TF/s for the two-barrier round-5 loop
+// (SCHED 2, removed: git history), hipBLASLt 1578; BERT qkv 1129 vs 1086, ffn2 1330 vs 1283,
+// ffn1 dgrad 1322 vs 1297 TF/s;
 // 30 = the persistent SCHED-2 kernel (gemm4p, next tile's DMA under this tile's epilogue);
 // 0 = the compiler-scheduled one-tile loop (oracle). With the branch-free steady loop (same box,
 // tools/g4_bench.py): 8192^3 1515 (2) vs 1301 (30) TF/s, hipBLASLt 1650; BERT-Large step
@@ -846,32 +799,29 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
     int* c = big::tile_counters(st, 0);
     if (c) tq = c + big::kMaxCtr - 16;
   }
+#define TTDK_G4_ONE(EKV) /* one tile per workgroup: SCHED 3 (>= 2 K-tiles), else the compiler's loop */  \
+  if (K >= 128)                                                                                             \
+    hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 3>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M,  \
+                       N, K, tm, tn, group);                                                                \
+  else                                                                                                      \
+    hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 0>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M,  \
+                       N, K, tm, tn, group);
 #define TTDK_G4(EKV)                                                                                        \
   case EKV:                                                                                                 \
     switch (sched) {                                                                                        \
       case 0: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 0>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
                                  ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 2: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
-      case 3: if (K >= 128) {                                                                              \
-          hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 3>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb,  \
-                             pe, M, N, K, tm, tn, group); break;                                              \
-        }                                                                                                   \
-        hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb,    \
-                           pe, M, N, K, tm, tn, group); break;                                                \
       case 30: {                                                                                          \
         const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
         if (grid < 8 || tm * tn <= g4_cus()) { /* one tile per workgroup: nothing to overlap */           \
-          hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, \
-                             pe, M, N, K, tm, tn, group);                                                   \
+          TTDK_G4_ONE(EKV)                                                                                  \
           break;                                                                                            \
         }                                                                                                   \
         hipLaunchKernelGGL((g4::gemm4p_kernel<EKV>), dim3(grid), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M, N,  \
                            K, tm, tn, group, stag, tq);                                                     \
         break;                                                                                              \
       }                                                                                                     \
-      default: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 2>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda,   \
-                                  B, ldb, pe, M, N, K, tm, tn, group); break;                                      \
+      default: TTDK_G4_ONE(EKV) break;                                                                      \
     }                                                                                                       \
     return hipGetLastError();
   switch (ek) {
@@ -883,5 +833,6 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
     default: break;
   }
 #undef TTDK_G4
+#undef TTDK_G4_ONE
   return hipErrorInvalidValue;
 }

@@ -170,7 +170,7 @@ def set_g4_group(v: int) -> int:
 
 
 def set_g4_sched(v: int) -> int:
-    """Main-loop schedule of the 4-wave GEMM (gemm4w.hip g4_sched): 2 = hand-ordered inline asm,
+    """Main-loop schedule of the 4-wave GEMM (gemm4w.hip g4_sched): 3 = hand-ordered inline asm,
     one tile per workgroup (default), 30 = persistent, 0 = compiler-scheduled (A/B and tests).
     Returns the previous setting."""
     return int(_lib.query("ttdk_set_g4_sched", int(v)))

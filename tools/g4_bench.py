@@ -18,7 +18,7 @@ def arg(name, default):
 T = int(arg("--tokens", "65536"))
 ONLY = arg("--only", None)
 ROUNDS = int(arg("--rounds", "3"))
-ARMS = arg("--arms", "g4:1,g4:2,g4:3,g4:0,big,torch").split(",")
+ARMS = arg("--arms", "g4:3,g4:30,g4:0,big,torch").split(",")
 SHAPES = [  # (name, M, N, K, epilogue)
     ("sq4096", 4096, 4096, 4096, ""),
     ("sq8192", 8192, 8192, 8192, ""),
