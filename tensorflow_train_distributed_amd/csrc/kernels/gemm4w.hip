@@ -84,6 +84,55 @@ struct LoadK {
   }
 };
 
+// Implicit-GEMM convolution A operand (AOP = 1): GEMM row = output pixel (n, p, q), K = (r, s, c)
+// with one 64-channel K-tile inside one filter tap (C % 64 == 0). A row's K-tile address is the
+// pixel's window-corner offset (per lane, per piece) plus the tap's offset (r W + s) C + c0
+// (scalar, advanced by a cursor as the DMA walks the K-tiles); the buffer base sits SHIFT =
+// (ph W + pw) C bytes before x so every in-image offset is >= 0. A tap outside the image (the
+// padding) or a row past M gets an offset past the buffer's end: the buffer load returns zeros.
+struct ConvA {
+  int H, W, C, PQ, Q, sh, sw, ph, pw, R, S;
+  long long x_bytes;
+};
+constexpr uint32_t kOob = 0x80000000u;
+struct LoadConv {
+  ttd_i32x4_t srd;
+  uint32_t voff[8];
+  uint32_t vmask[8];  // bit t: tap t = r S + s lies inside the image for this piece's row
+  __device__ __forceinline__ void init(const bf16_t* x, const ConvA& c, int M, int row0, int tid) {
+    const long long shift = (static_cast<long long>(c.ph) * c.W + c.pw) * c.C * 2;
+    srd = make_srd(reinterpret_cast<const char*>(x) - shift, static_cast<uint32_t>(c.x_bytes + shift));
+    const int chunk = (tid & 7) ^ ((tid >> 4) & 7);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = row0 + i * 32 + (tid >> 3);
+      const int mm = m < M ? m : 0;
+      const int n = mm / c.PQ, rem = mm - n * c.PQ;
+      const int p = rem / c.Q, q = rem - p * c.Q;
+      const int h0 = p * c.sh - c.ph, w0 = q * c.sw - c.pw;
+      voff[i] = static_cast<uint32_t>(((static_cast<long long>(n) * c.H + h0) * c.W + w0) * c.C * 2 + shift + chunk * 16);
+      uint32_t mk = 0;
+      for (int r = 0; r < c.R; ++r)
+        for (int s2 = 0; s2 < c.S; ++s2)
+          if (m < M && static_cast<unsigned>(h0 + r) < static_cast<unsigned>(c.H) &&
+              static_cast<unsigned>(w0 + s2) < static_cast<unsigned>(c.W))
+            mk |= 1u << (r * c.S + s2);
+      vmask[i] = mk;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(int i, int tap) const { return (vmask[i] >> tap) & 1u ? voff[i] : kOob; }
+};
+constexpr int kEkStat = 32;  // BN partial sums (sum, sum of squares) of the stored output per 128 rows
+
+// sum over the 16 lanes of a DPP row (lane 15 of the row ends with the total)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, false));
+  return v;
+}
+
 __device__ __forceinline__ bf16x8_t rd(const char* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
 template <int N>
@@ -140,6 +189,13 @@ __device__ __forceinline__ void epilogue(const f32x4_t (&acc)[8][8], const EpiPa
                                               : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
   constexpr bool LD = (EK & (kEkDGelu | kEkBeta)) != 0;
+  float ssum[4][8], ssq[4][8];  // kEkStat: per-lane column partials (8 columns of each column pair p)
+  if constexpr ((EK & kEkStat) != 0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ssum[p][j] = ssq[p][j] = 0.f;
+  }
   uint2 ldv[2][8];  // [row-block parity][b]: residual (dGELU) or old output (beta), one row block ahead
   auto load_rows = [&](int a, uint2 (&v)[8]) {
     const int m = m0 + wm * 128 + a * 16 + i16;
@@ -206,9 +262,38 @@ __device__ __forceinline__ void epilogue(const f32x4_t (&acc)[8][8], const EpiPa
         const auto s1 = __builtin_amdgcn_permlane16_swap(q[0][1], q[1][1], false, false);
         const uint4 w = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         if (mok && (!CHECK || nst < N)) *reinterpret_cast<uint4*>(base + row + nst) = w;
+        return w;
       };
-      swap_store(po, out);
+      const uint4 wo = swap_store(po, out);
       if constexpr ((EK & kEkAux) != 0) swap_store(pa, E.aux);
+      if constexpr ((EK & kEkStat) != 0) {  // statistics of the values actually stored
+        if (mok) {
+          float v8[8];
+          unpack8(wo, v8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            ssum[p][j] += v8[j];
+            ssq[p][j] += v8[j] * v8[j];
+          }
+        }
+      }
+    }
+  }
+  if constexpr ((EK & kEkStat) != 0) {
+    // the 16 rows of a lane group hold the same 8 columns: sum them across the DPP row; lane 15
+    // writes this wave's 128-row partial row (m0 / 128 + wm) of E.stat [2 tiles_m][2][N]
+    float* const st = E.stat + static_cast<long long>((m0 / 128) + wm) * 2 * N;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int nst = odd ? ncol + 32 * p + 12 : ncol + 32 * p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = row_sum16(ssum[p][j]), b = row_sum16(ssq[p][j]);
+        if (i16 == 15 && (!CHECK || nst + j < N)) {
+          st[nst + j] = a;
+          st[N + nst + j] = b;
+        }
+      }
     }
   }
 }
@@ -263,10 +348,11 @@ __device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int gro
 // SCHED 3: the production one-tile-per-workgroup loop (hand-ordered inline asm); SCHED 0: a
 // two-barrier schedule left to the compiler, kept as the A/B oracle of the hand ordering (and the
 // form of K = 64, a single K-tile)
-template <int EK, int SCHED>
+template <int EK, int SCHED, int AOP = 0>
 __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__ A, long long lda,
                                                      const bf16_t* __restrict__ B, long long ldb, EpiParams E, int M,
-                                                     int N, int K, int tiles_m, int tiles_n, int group) {
+                                                     int N, int K, int tiles_m, int tiles_n, int group, ConvA ca) {
+  static_assert(AOP == 0 || SCHED == 3, "the convolution operand rides the hand-ordered loop");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int nblk = tiles_m * tiles_n;
   const int t = xcd_remap(blockIdx.x, nblk);
@@ -279,8 +365,25 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   const int ktiles = K / 64;
 
   LoadK la, lb;
-  la.init(A, lda, M, m0, tid);
+  LoadConv lc;
+  if constexpr (AOP == 1) lc.init(A, ca, M, m0, tid);
+  else la.init(A, lda, M, m0, tid);
   lb.init(B, ldb, N, n0, tid);
+  // AOP = 1: the A operand's DMA cursor (K-tile whose A pieces go out next): tap index, channel
+  // offset, and the tap's scalar byte offset (r W + s) C + c0 (2 bytes per element)
+  int c_tap = 0, c_c0 = 0, c_r = 0, c_s = 0, c_soff = 0;
+  auto c_advance = [&]() {
+    c_c0 += 64;
+    if (c_c0 == ca.C) {
+      c_c0 = 0;
+      ++c_tap;
+      if (++c_s == ca.S) {
+        c_s = 0;
+        ++c_r;
+      }
+    }
+    c_soff = ((c_r * ca.W + c_s) * ca.C + c_c0) * 2;
+  };
 
   // per-lane fragment offsets for K-step ks: row i16, chunk 4 ks + g, XOR (i16 >> 1) & 7
   const int i16 = lane & 15, g = lane >> 4;
@@ -399,8 +502,13 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   };
   auto dma1 = [&](auto Q, int st, int kt) {
     constexpr int q = decltype(Q)::value;
-    const LoadK& L = q < 8 ? la : lb;
-    dma_chain(L.voff[q & 7], L.srd, kt * 128, q < 15 ? m0_of(q + 1, st) : m0_of(0, st ^ 1));
+    if constexpr (AOP == 1 && q < 8) {
+      dma_chain(lc.off(q, c_tap), lc.srd, c_soff, m0_of(q + 1, st));
+      if constexpr (q == 7) c_advance();
+    } else {
+      const LoadK& L = q < 8 ? la : lb;
+      dma_chain(L.voff[q & 7], L.srd, kt * 128, q < 15 ? m0_of(q + 1, st) : m0_of(0, st ^ 1));
+    }
   };
   auto mfma1 = [&](int a, int b, const bf16x8_t& x, const bf16x8_t& y, auto first) {
     mfma_acc<decltype(first)::value>(acc[a][b], x, y);
@@ -762,6 +870,49 @@ TTDK_EXPORT int ttdk_set_g4_sched(int v) {
   return old;
 }
 
+// Forward convolution y[M = N P Q][K] = conv(x[N][H][W][C], w[K][R][S][C]) on the 4-wave kernel
+// (hand-ordered SCHED 3 loop), plain bf16 store (epi: out with ldo = K, optionally stat — nothing
+// else). stat receives the BN partial sums (sum, sum of squares) of the stored output per 128
+// rows: [2 ceil(M / 256)][2][K]. Unit-stride 1x1 convs read x as a dense [M][C] operand, the
+// others through the implicit-GEMM gather (g4::LoadConv). Needs C % 64 == 0 (a K-tile inside one
+// tap), R S C >= 128, no dilation. hipErrorInvalidValue: not taken (the caller keeps conv_fwd).
+TTDK_EXPORT int ttdk_conv_fwd4w(const bf16_t* x, const bf16_t* w, const TtdkConv* g, const TtdkEpilogue* epi,
+                                hipStream_t st) {
+  using namespace ttdk;
+  EpiParams pe = to_epi(epi);
+  const int M = g->N * g->P * g->Q, N = g->K, K = g->R * g->S * g->C;
+  const long long xb = static_cast<long long>(g->N) * g->H * g->W * g->C * 2;
+  const long long shift = (static_cast<long long>(g->ph) * g->W + g->pw) * g->C * 2;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (g->C % 64 || K < 128 || N % 8 || g->dh != 1 || g->dw != 1 || g->R * g->S > 32 || M < 1 || !al16(x) ||
+      !al16(w) || !al16(pe.out) || xb + shift >= (1LL << 31) || (static_cast<long long>(N) + 256) * K * 2 >= (1LL << 32) ||
+      static_cast<long long>(M) * N * 2 >= (1LL << 40) || pe.ldo != N || pe.bias || pe.residual ||
+      pe.act != kActNone || pe.aux || pe.beta || pe.remap || pe.mode != 0 || pe.by || pe.bH || pe.alpha != 1.f ||
+      pe.ascale0 || pe.ascale1)
+    return hipErrorInvalidValue;
+  const int tm = ceil_div(M, g4::BM), tn = ceil_div(N, g4::BN);
+  const int group = g4_group();
+  const dim3 grid(tm * tn);
+  if (is_pointwise(g)) {
+    if (pe.stat)
+      hipLaunchKernelGGL((g4::gemm4w_kernel<g4::kEkStat, 3, 0>), grid, dim3(g4::T), 0, st, x,
+                         static_cast<long long>(g->C), w, static_cast<long long>(K), pe, M, N, K, tm, tn, group,
+                         g4::ConvA{});
+    else
+      hipLaunchKernelGGL((g4::gemm4w_kernel<0, 3, 0>), grid, dim3(g4::T), 0, st, x, static_cast<long long>(g->C), w,
+                         static_cast<long long>(K), pe, M, N, K, tm, tn, group, g4::ConvA{});
+    return hipGetLastError();
+  }
+  const g4::ConvA ca{g->H, g->W, g->C, g->P * g->Q, g->Q, g->sh, g->sw, g->ph, g->pw, g->R, g->S, xb};
+  if (pe.stat)
+    hipLaunchKernelGGL((g4::gemm4w_kernel<g4::kEkStat, 3, 1>), grid, dim3(g4::T), 0, st, x, 0LL, w,
+                       static_cast<long long>(K), pe, M, N, K, tm, tn, group, ca);
+  else
+    hipLaunchKernelGGL((g4::gemm4w_kernel<0, 3, 1>), grid, dim3(g4::T), 0, st, x, 0LL, w, static_cast<long long>(K),
+                       pe, M, N, K, tm, tn, group, ca);
+  return hipGetLastError();
+}
+
 // C[M,N] = epilogue(alpha * A . B^T), A [M][K] (lda), B [N][K] (ldb) bf16 K-major; K % 64 == 0,
 // N % 8 == 0, ldo % 8 == 0, 16-B aligned operands and outputs. Returns hipErrorInvalidValue for
 // shapes this kernel does not take (the caller keeps another path).
@@ -802,15 +953,15 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
 #define TTDK_G4_ONE(EKV) /* one tile per workgroup: SCHED 3 (>= 2 K-tiles), else the compiler's loop */  \
   if (K >= 128)                                                                                             \
     hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 3>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M,  \
-                       N, K, tm, tn, group);                                                                \
+                       N, K, tm, tn, group, g4::ConvA{});                                                   \
   else                                                                                                      \
     hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 0>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, ldb, pe, M,  \
-                       N, K, tm, tn, group);
+                       N, K, tm, tn, group, g4::ConvA{});
 #define TTDK_G4(EKV)                                                                                        \
   case EKV:                                                                                                 \
     switch (sched) {                                                                                        \
       case 0: hipLaunchKernelGGL((g4::gemm4w_kernel<EKV, 0>), dim3(tm * tn), dim3(g4::T), 0, st, A, lda, B, \
-                                 ldb, pe, M, N, K, tm, tn, group); break;                                          \
+                                 ldb, pe, M, N, K, tm, tn, group, g4::ConvA{}); break;                             \
       case 30: {                                                                                          \
         const int grid = std::min(tm * tn, g4_cus()) & ~7;                                                  \
         if (grid < 8 || tm * tn <= g4_cus()) { /* one tile per workgroup: nothing to overlap */           \

@@ -425,6 +425,11 @@ class ResNet:
             ws = self._w8_slots[self._w8_slot[c.name]]
             y = G.conv_fwd_fp8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
                                ascale=(xslot[3:4], ws[3:4]))
+        elif bm == 256 and G.conv_fwd4w_pays(tuple(x.shape), tuple(P.var[c.name + "_conv/kernel"].shape),
+                                             (c.stride, c.stride), (c.pad, c.pad)):
+            # the 4-wave GEMM (SCHED 3 loop, im2col gather by the operand DMA, BN statistics from
+            # its register epilogue per 128 rows): tools/conv1x1_g4_bench.py, BASELINE round 6
+            y, partial, T = G.conv_fwd4w(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad))
         else:
             partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
             y = G.conv_fwd(x, P.c[c.name + "_conv/kernel"], (c.stride, c.stride), (c.pad, c.pad), stat=partial,

@@ -570,6 +570,52 @@ def conv_fwd(x, w, stride=(1, 1), padding=(0, 0), *, out=None, residual=None, ac
     return out
 
 
+# forward convolutions on the 4-wave GEMM (gemm4w.hip ttdk_conv_fwd4w: SCHED 3 main loop, BN
+# statistics from the register epilogue, im2col gather by the operand DMA). TTD_CONV4W: 1
+# (default) where it measured faster than the 256-row kernel at b1024 (tools/conv4w_bench.py,
+# profiles/r6_conv4w_bench_b1024.txt): >= 256 output channels, reduction K = R*S*C >= 1024 and
+# K * N >= 512 * 1024 (the stage-4/5 3x3 convs 1.19-1.40x, stage-5 1x1 1.11-1.17x; the short-K
+# shapes lose 3-12 % to the statistics epilogue); 2 every conv conv_fwd4w takes; 0 off.
+_CONV4W = int(_os.environ.get("TTD_CONV4W", "1"))
+
+
+def conv_fwd4w_pays(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
+    """The engine's policy for conv_fwd4w (TTD_CONV4W) on top of conv_fwd4w_ok."""
+    if _CONV4W <= 0 or not conv_fwd4w_ok(x_shape, w_shape, stride, padding):
+        return False
+    K, N = w_shape[1] * w_shape[2] * w_shape[3], w_shape[0]
+    return _CONV4W >= 2 or (N >= 256 and K >= 1024 and K * N >= 512 * 1024)
+
+
+def conv_fwd4w_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
+    """Whether conv_fwd4w takes this conv: C % 64 == 0, K % 8 == 0, R*S*C >= 128, operands in range."""
+    g = conv_geom(tuple(x_shape), tuple(w_shape), stride, padding)
+    xb = g.N * g.H * g.W * g.C * 2
+    shift = (g.ph * g.W + g.pw) * g.C * 2
+    return (g.C % 64 == 0 and g.K % 8 == 0 and g.R * g.S * g.C >= 128 and g.R * g.S <= 32
+            and g.dh == 1 and g.dw == 1 and xb + shift < (1 << 31))
+
+
+def conv_fwd4w(x, w, stride=(1, 1), padding=(0, 0), *, stat=True, out=None):
+    """y[N,P,Q,K] = conv(x[N,H,W,C], w[K,R,S,C]) on the 4-wave kernel; with stat, also the BN
+    partial sums of the stored output per 128-row block. Returns (y, partial [T, 2, K], T) (partial
+    None without stat). Raises when the kernel does not take the conv (conv_fwd4w_ok)."""
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.bfloat16, "w")
+    if not conv_fwd4w_ok(tuple(x.shape), tuple(w.shape), stride, padding):
+        raise ValueError("conv_fwd4w does not take x %s, w %s" % (tuple(x.shape), tuple(w.shape)))
+    g = conv_geom(x.shape, w.shape, stride, padding)
+    M = g.N * g.P * g.Q
+    if out is None:
+        out = torch.empty((g.N, g.P, g.Q, g.K), dtype=torch.bfloat16, device=x.device)
+    T = 2 * -(-M // 256)
+    partial = torch.empty((T, 2, g.K), dtype=torch.float32, device=x.device) if stat else None
+    e = _epi(out, ldo=g.K, stat=partial)
+    _log("fwd4w_%dx%d_s%d" % (g.R, g.S, g.sh), M, g.K, g.R * g.S * g.C)
+    _lib.call("ttdk_conv_fwd4w", x.data_ptr(), w.data_ptr(), ctypes.byref(g), ctypes.byref(e), _lib.stream())
+    return out, partial, T
+
+
 def conv_fwd_bnpro_ok(x_shape, w_shape):
     """Whether conv_fwd_bnpro runs: a 1x1 unit-stride conv on the 256-row kernel."""
     N, H, W, C = x_shape

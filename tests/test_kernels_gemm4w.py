@@ -81,3 +81,37 @@ def test_gemm4w_strided_operands(sched):
     b = (torch.rand(384, 256, device="cuda") * 2 - 1).bfloat16()
     out = G.gemm4w(a, b)
     assert _rel(out, a.float() @ b.float().t()) < 8e-3
+
+
+@pytest.mark.parametrize("N,H,C,K,R,stride", [
+    (8, 14, 256, 256, 3, 1),    # stage-4 3x3
+    (8, 28, 128, 128, 3, 2),    # stage-3 block-1 3x3 stride 2
+    (8, 14, 512, 512, 3, 2),    # stage-5 block-1 3x3 stride 2
+    (8, 7, 512, 512, 3, 1),     # stage-5 3x3
+    (8, 14, 256, 1024, 1, 1),   # stage-4 c3 (dense operand)
+    (8, 7, 2048, 512, 1, 1),    # stage-5 c1
+    (8, 28, 512, 1024, 1, 2),   # stage-4 projection (1x1 stride 2: gathered)
+    (3, 9, 64, 72, 3, 1),       # C = 64, odd spatial size, M and K not multiples of 256
+])
+def test_conv_fwd4w_vs_fp32(N, H, C, K, R, stride):
+    """Forward conv on the 4-wave kernel (im2col gather through the operand DMA, zeros for the
+    padding taps) vs F.conv2d in fp32, and its BN partial sums vs the stored output's."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(N + H + C + K + R + stride)
+    pad = R // 2
+    x = (torch.rand(N, H, H, C, device="cuda") * 2 - 1).bfloat16()
+    w = ((torch.rand(K, R, R, C, device="cuda") * 2 - 1) * (1.0 / (R * R * C) ** 0.5)).bfloat16()
+    y, part, T = G.conv_fwd4w(x, w, (stride, stride), (pad, pad))
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=stride, padding=pad)
+    ref = ref.permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 8e-3
+    M = y.numel() // K
+    assert T == 2 * -(-M // 256)
+    yf = y.float().reshape(M, K)
+    s = part.sum(0)
+    assert _rel(s[0], yf.sum(0)) < 1e-4
+    assert _rel(s[1], (yf * yf).sum(0)) < 1e-4
+    # no statistics requested: same output bits
+    y2, p2, _ = G.conv_fwd4w(x, w, (stride, stride), (pad, pad), stat=False)
+    assert p2 is None and torch.equal(y, y2)
