@@ -92,6 +92,7 @@ struct LoadK {
 // padding) or a row past M gets an offset past the buffer's end: the buffer load returns zeros.
 struct ConvA {
   int H, W, C, PQ, Q, sh, sw, ph, pw, R, S;
+  int flip;  // data gradient: taps walked in the filter's reversed order (the [C][R][S][K] B operand)
   long long x_bytes;
 };
 constexpr uint32_t kOob = 0x80000000u;
@@ -123,6 +124,9 @@ struct LoadConv {
   __device__ __forceinline__ uint32_t off(int i, int tap) const { return (vmask[i] >> tap) & 1u ? voff[i] : kOob; }
 };
 constexpr int kEkStat = 32;  // BN partial sums (sum, sum of squares) of the stored output per 128 rows
+// feeding-BN epilogue of a data gradient (E.by, E.bmask, E.stat): stores g = dx * ReLU bits of the
+// feeding conv+BN unit and its backward partial sums (sum g, sum g * y) per 128 rows
+constexpr int kEkFeed = 64;
 
 // sum over the 16 lanes of a DPP row (lane 15 of the row ends with the total)
 __device__ __forceinline__ float row_sum16(float v) {
@@ -188,34 +192,49 @@ __device__ __forceinline__ void epilogue(const f32x4_t (&acc)[8][8], const EpiPa
       bias[b] = (!CHECK || ncol + 16 * b < N) ? *reinterpret_cast<const f32x4_t*>(E.bias + ncol + 16 * b)
                                               : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
+  constexpr bool FEED = (EK & kEkFeed) != 0;
+  constexpr bool STATS = FEED || (EK & kEkStat) != 0;
   constexpr bool LD = (EK & (kEkDGelu | kEkBeta)) != 0;
-  float ssum[4][8], ssq[4][8];  // kEkStat: per-lane column partials (8 columns of each column pair p)
-  if constexpr ((EK & kEkStat) != 0) {
+  // STATS: per-lane column partials of the 4 columns of every block b (sum, sum of squares — FEED:
+  // sum of g and of g * y); the 16 lanes of a group hold the same columns (rows i16 + 16 a)
+  float ssum[8][4], ssq[8][4];
+  if constexpr (STATS) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int b = 0; b < 8; ++b)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ssum[p][j] = ssq[p][j] = 0.f;
+      for (int j = 0; j < 4; ++j) ssum[b][j] = ssq[b][j] = 0.f;
   }
   uint2 ldv[2][8];  // [row-block parity][b]: residual (dGELU) or old output (beta), one row block ahead
-  auto load_rows = [&](int a, uint2 (&v)[8]) {
+  uint2 ldy[2][8];  // FEED: the feeding unit's conv output y, one row block ahead
+  uint32_t ldk[2][2];  // FEED: its ReLU bits, block b's byte (8 channels holding the lane's 4) at bits 8 (b & 3) of word b >> 2
+  auto load_rows = [&](int a, uint2 (&v)[8], uint2 (&yv)[8], uint32_t (&kv)[2]) {
     const int m = m0 + wm * 128 + a * 16 + i16;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const int n = ncol + 16 * b;
       v[b] = make_uint2(0, 0);
+      if constexpr (FEED) {
+        yv[b] = make_uint2(0, 0);
+        if ((b & 3) == 0) kv[b >> 2] = 0;
+      }
       if (!CHECK || (m < M && n < N)) {
         if constexpr ((EK & kEkDGelu) != 0)
           v[b] = *reinterpret_cast<const uint2*>(E.residual + static_cast<long long>(m) * E.ldr + n);
         else if constexpr ((EK & kEkBeta) != 0)
           v[b] = *reinterpret_cast<const uint2*>(out + static_cast<long long>(m) * E.ldo + n);
+        if constexpr (FEED) {
+          const long long o = static_cast<long long>(m) * E.ldo + n;
+          yv[b] = *reinterpret_cast<const uint2*>(E.by + o);
+          kv[b >> 2] |= static_cast<uint32_t>(E.bmask ? E.bmask[o >> 3] : 0xffu) << (8 * (b & 3));
+        }
       }
     }
   };
-  if constexpr (LD) load_rows(0, ldv[0]);
+  if constexpr (LD || FEED) load_rows(0, ldv[0], ldy[0], ldk[0]);
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
-    if constexpr (LD)
-      if (a + 1 < 8) load_rows(a + 1, ldv[(a + 1) & 1]);
+    if constexpr (LD || FEED)
+      if (a + 1 < 8) load_rows(a + 1, ldv[(a + 1) & 1], ldy[(a + 1) & 1], ldk[(a + 1) & 1]);
     const int m = m0 + wm * 128 + a * 16 + i16;
     const bool mok = !CHECK || m < M;
     const long long row = static_cast<long long>(m) * E.ldo;
@@ -251,8 +270,35 @@ __device__ __forceinline__ void epilogue(const f32x4_t (&acc)[8][8], const EpiPa
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = gelu_tanh(v[q]);
         }
+        if constexpr (FEED) {  // the masked gradient g = dx * relu'(the feeding unit's output)
+          const uint32_t bits = (ldk[a & 1][b >> 2] >> (8 * (b & 3))) >> (ncol & 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = (bits >> q) & 1u ? v[q] : 0.f;
+        }
         po[j][0] = pack_bf16x2(v[0], v[1]);
         po[j][1] = pack_bf16x2(v[2], v[3]);
+        if constexpr (STATS) {  // statistics of the values actually stored
+          if (mok) {
+            float r[4];
+            r[0] = bf2f(static_cast<bf16_t>(po[j][0] & 0xffff));
+            r[1] = bf2f(static_cast<bf16_t>(po[j][0] >> 16));
+            r[2] = bf2f(static_cast<bf16_t>(po[j][1] & 0xffff));
+            r[3] = bf2f(static_cast<bf16_t>(po[j][1] >> 16));
+            float yy[4] = {r[0], r[1], r[2], r[3]};
+            if constexpr (FEED) {
+              const uint2 w = ldy[a & 1][b];
+              yy[0] = bf2f(static_cast<bf16_t>(w.x & 0xffff));
+              yy[1] = bf2f(static_cast<bf16_t>(w.x >> 16));
+              yy[2] = bf2f(static_cast<bf16_t>(w.y & 0xffff));
+              yy[3] = bf2f(static_cast<bf16_t>(w.y >> 16));
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              ssum[b][q] += r[q];
+              ssq[b][q] += r[q] * yy[q];
+            }
+          }
+        }
       }
       // even rows (g even) keep block 2p's own columns and receive the odd neighbour's; odd
       // rows receive the even neighbour's block 2p + 1 columns: 8 consecutive columns per lane
@@ -262,39 +308,26 @@ __device__ __forceinline__ void epilogue(const f32x4_t (&acc)[8][8], const EpiPa
         const auto s1 = __builtin_amdgcn_permlane16_swap(q[0][1], q[1][1], false, false);
         const uint4 w = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         if (mok && (!CHECK || nst < N)) *reinterpret_cast<uint4*>(base + row + nst) = w;
-        return w;
       };
-      const uint4 wo = swap_store(po, out);
+      swap_store(po, out);
       if constexpr ((EK & kEkAux) != 0) swap_store(pa, E.aux);
-      if constexpr ((EK & kEkStat) != 0) {  // statistics of the values actually stored
-        if (mok) {
-          float v8[8];
-          unpack8(wo, v8);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            ssum[p][j] += v8[j];
-            ssq[p][j] += v8[j] * v8[j];
-          }
-        }
-      }
     }
   }
-  if constexpr ((EK & kEkStat) != 0) {
-    // the 16 rows of a lane group hold the same 8 columns: sum them across the DPP row; lane 15
+  if constexpr (STATS) {
+    // the 16 rows of a lane group hold the same columns: sum them across the DPP row; lane 15
     // writes this wave's 128-row partial row (m0 / 128 + wm) of E.stat [2 tiles_m][2][N]
     float* const st = E.stat + static_cast<long long>((m0 / 128) + wm) * 2 * N;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int nst = odd ? ncol + 32 * p + 12 : ncol + 32 * p;
+    for (int b = 0; b < 8; ++b)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float a = row_sum16(ssum[p][j]), b = row_sum16(ssq[p][j]);
-        if (i16 == 15 && (!CHECK || nst + j < N)) {
-          st[nst + j] = a;
-          st[N + nst + j] = b;
+      for (int j = 0; j < 4; ++j) {
+        const float sa = row_sum16(ssum[b][j]), sb = row_sum16(ssq[b][j]);
+        const int n = ncol + 16 * b + j;
+        if (i16 == 15 && (!CHECK || n < N)) {
+          st[n] = sa;
+          st[N + n] = sb;
         }
       }
-    }
   }
 }
 
@@ -371,18 +404,22 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   lb.init(B, ldb, N, n0, tid);
   // AOP = 1: the A operand's DMA cursor (K-tile whose A pieces go out next): tap index, channel
   // offset, and the tap's scalar byte offset (r W + s) C + c0 (2 bytes per element)
-  int c_tap = 0, c_c0 = 0, c_r = 0, c_s = 0, c_soff = 0;
+  int c_c0 = 0, c_r = 0, c_s = 0;
+  // (tap 0 in the operand's own order: the reversed walk starts at its last tap)
+  int c_atap = ca.flip ? ca.R * ca.S - 1 : 0;
+  int c_soff = ca.flip ? ((ca.R - 1) * ca.W + ca.S - 1) * ca.C * 2 : 0;
   auto c_advance = [&]() {
     c_c0 += 64;
     if (c_c0 == ca.C) {
       c_c0 = 0;
-      ++c_tap;
       if (++c_s == ca.S) {
         c_s = 0;
         ++c_r;
       }
     }
-    c_soff = ((c_r * ca.W + c_s) * ca.C + c_c0) * 2;
+    const int ra = ca.flip ? ca.R - 1 - c_r : c_r, sa = ca.flip ? ca.S - 1 - c_s : c_s;
+    c_atap = ra * ca.S + sa;
+    c_soff = ((ra * ca.W + sa) * ca.C + c_c0) * 2;
   };
 
   // per-lane fragment offsets for K-step ks: row i16, chunk 4 ks + g, XOR (i16 >> 1) & 7
@@ -503,7 +540,7 @@ __global__ __launch_bounds__(T, 1) void gemm4w_kernel(const bf16_t* __restrict__
   auto dma1 = [&](auto Q, int st, int kt) {
     constexpr int q = decltype(Q)::value;
     if constexpr (AOP == 1 && q < 8) {
-      dma_chain(lc.off(q, c_tap), lc.srd, c_soff, m0_of(q + 1, st));
+      dma_chain(lc.off(q, c_atap), lc.srd, c_soff, m0_of(q + 1, st));
       if constexpr (q == 7) c_advance();
     } else {
       const LoadK& L = q < 8 ? la : lb;
@@ -903,13 +940,46 @@ TTDK_EXPORT int ttdk_conv_fwd4w(const bf16_t* x, const bf16_t* w, const TtdkConv
                          static_cast<long long>(K), pe, M, N, K, tm, tn, group, g4::ConvA{});
     return hipGetLastError();
   }
-  const g4::ConvA ca{g->H, g->W, g->C, g->P * g->Q, g->Q, g->sh, g->sw, g->ph, g->pw, g->R, g->S, xb};
+  const g4::ConvA ca{g->H, g->W, g->C, g->P * g->Q, g->Q, g->sh, g->sw, g->ph, g->pw, g->R, g->S, 0, xb};
   if (pe.stat)
     hipLaunchKernelGGL((g4::gemm4w_kernel<g4::kEkStat, 3, 1>), grid, dim3(g4::T), 0, st, x, 0LL, w,
                        static_cast<long long>(K), pe, M, N, K, tm, tn, group, ca);
   else
     hipLaunchKernelGGL((g4::gemm4w_kernel<0, 3, 1>), grid, dim3(g4::T), 0, st, x, 0LL, w, static_cast<long long>(K),
                        pe, M, N, K, tm, tn, group, ca);
+  return hipGetLastError();
+}
+
+// Unit-stride data gradient dx[N H W][C] = conv_transpose(dy[N][P][Q][K], w) on the 4-wave kernel:
+// wt = w transposed to [C][R][S][K] (the B operand, K-major), dy gathered as a forward conv with
+// padding (R - 1 - ph, S - 1 - pw) whose taps are walked in reverse (ConvA::flip). epi: out with
+// ldo = C, and either nothing else (plain store) or the feeding-BN epilogue (by, bmask, stat:
+// g = dx * ReLU bits stored, partial sums (sum g, sum g * y) per 128 rows, [2 ceil(M / 256)][2][C]).
+// Needs K % 64 == 0 (dy channels), R S K >= 128. hipErrorInvalidValue: not taken.
+TTDK_EXPORT int ttdk_conv_dgrad4w(const bf16_t* dy, const bf16_t* wt, const TtdkConv* g, const TtdkEpilogue* epi,
+                                  hipStream_t st) {
+  using namespace ttdk;
+  EpiParams pe = to_epi(epi);
+  const int M = g->N * g->H * g->W, N = g->C, K = g->R * g->S * g->K;
+  const long long yb = static_cast<long long>(g->N) * g->P * g->Q * g->K * 2;
+  const int pho = g->R - 1 - g->ph, pwo = g->S - 1 - g->pw;
+  const long long shift = (static_cast<long long>(pho) * g->Q + pwo) * g->K * 2;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (g->sh != 1 || g->sw != 1 || g->dh != 1 || g->dw != 1 || g->K % 64 || K < 128 || N % 8 || g->R * g->S > 32 ||
+      pho < 0 || pwo < 0 || M < 1 || !al16(dy) || !al16(wt) || !al16(pe.out) || yb + shift >= (1LL << 31) ||
+      (static_cast<long long>(N) + 256) * K * 2 >= (1LL << 32) || pe.ldo != N || pe.bias || pe.residual ||
+      pe.act != kActNone || pe.aux || pe.beta || pe.remap || pe.mode != 0 || pe.bH || pe.by2 || pe.stat2 ||
+      pe.alpha != 1.f || pe.ascale0 || pe.ascale1 || (pe.by != nullptr) != (pe.stat != nullptr) ||
+      (pe.by && !al16(pe.by)))
+    return hipErrorInvalidValue;
+  const int tm = ceil_div(M, g4::BM), tn = ceil_div(N, g4::BN);
+  const g4::ConvA ca{g->P, g->Q, g->K, g->H * g->W, g->W, 1, 1, pho, pwo, g->R, g->S, 1, yb};
+  if (pe.by)
+    hipLaunchKernelGGL((g4::gemm4w_kernel<g4::kEkFeed, 3, 1>), dim3(tm * tn), dim3(g4::T), 0, st, dy, 0LL, wt,
+                       static_cast<long long>(K), pe, M, N, K, tm, tn, g4_group(), ca);
+  else
+    hipLaunchKernelGGL((g4::gemm4w_kernel<0, 3, 1>), dim3(tm * tn), dim3(g4::T), 0, st, dy, 0LL, wt,
+                       static_cast<long long>(K), pe, M, N, K, tm, tn, g4_group(), ca);
   return hipGetLastError();
 }
 

@@ -57,6 +57,7 @@ _SIGS = {
     "ttdk_gemm4t_ws": [I, I, I, I],
     "ttdk_conv_fwd": [P, P, G, I, I, E, P],
     "ttdk_conv_fwd4w": [P, P, G, E, P],
+    "ttdk_conv_dgrad4w": [P, P, G, E, P],
     "ttdk_conv_dgrad": [P, P, G, I, I, E, P],
     "ttdk_conv_dgrad_bnpro": [P, P, G, P, P, P, E, P],
     "ttdk_conv_dgrad_bnpro_ok": [G],

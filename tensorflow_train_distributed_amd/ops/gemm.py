@@ -616,6 +616,24 @@ def conv_fwd4w(x, w, stride=(1, 1), padding=(0, 0), *, stat=True, out=None):
     return out, partial, T
 
 
+# unit-stride 3x3 data gradients with the feeding-BN epilogue on the 4-wave GEMM (gemm4w.hip
+# ttdk_conv_dgrad4w: dy gathered as a forward conv with reversed taps). TTD_DGRAD4W: 1 (default)
+# the long-K shapes (>= 256 input channels, R*S*K >= 1024, K * N >= 512 * 1024), 0 off.
+_DGRAD4W = int(_os.environ.get("TTD_DGRAD4W", "1"))
+
+
+def conv_dgrad4w_pays(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)) -> bool:
+    """conv_dgrad takes the 4-wave kernel for this unit-stride, non-pointwise data gradient."""
+    C, R, S, K = wt_shape
+    if _DGRAD4W <= 0 or tuple(stride) != (1, 1) or R * S == 1 or K % 64 or C % 8:
+        return False
+    g = conv_geom(tuple(x_shape), (K, R, S, C), stride, padding)
+    if g.ph > R - 1 or g.pw > S - 1 or g.N * g.P * g.Q * K * 2 + ((R - 1 - g.ph) * g.Q + S - 1 - g.pw) * K * 2 >= (1 << 31):
+        return False
+    KK = R * S * K
+    return _DGRAD4W >= 2 or (C >= 256 and KK >= 1024 and KK * C >= 512 * 1024)
+
+
 def conv_fwd_bnpro_ok(x_shape, w_shape):
     """Whether conv_fwd_bnpro runs: a 1x1 unit-stride conv on the 256-row kernel."""
     N, H, W, C = x_shape
@@ -802,6 +820,15 @@ def conv_dgrad(dy, wt, x_shape, stride=(1, 1), padding=(0, 0), *, out=None, beta
                       int(ready), ctypes.byref(e), _lib.stream())
         elif bn_pro is not None:
             _bnpro_call(dy, wt, g, bn_pro, e)
+        elif (not beta and partial2 is None and residual is None
+              and conv_dgrad4w_pays(tuple(x_shape), tuple(wt.shape), stride, padding)):
+            # the 4-wave kernel: statistics rows are 128-pixel blocks
+            T = 2 * -(-(g.N * g.H * g.W) // 256)
+            partial = torch.empty((T, 2, C), dtype=torch.float32, device=dy.device)
+            e = _epi(out, ldo=C, stat=partial, by=y, bmask=mask)
+            _log("dgrad4w_%dx%d_s1" % (R, S), g.N * g.H * g.W, C, R * S * K)
+            _lib.call("ttdk_conv_dgrad4w", dy.data_ptr(), wt.data_ptr(), ctypes.byref(g), ctypes.byref(e),
+                      _lib.stream())
         else:
             bm, bn, _ = dgrad_stat_tile(tuple(x_shape), tuple(wt.shape))
             _log("dgrad_%dx%d_s%d" % (R, S, stride[0]), g.N * g.H * g.W, C, R * S * K)

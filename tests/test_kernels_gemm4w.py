@@ -115,3 +115,48 @@ def test_conv_fwd4w_vs_fp32(N, H, C, K, R, stride):
     # no statistics requested: same output bits
     y2, p2, _ = G.conv_fwd4w(x, w, (stride, stride), (pad, pad), stat=False)
     assert p2 is None and torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("N,H,C,K,R", [
+    (8, 14, 256, 256, 3),   # stage-4 c2 data gradient
+    (8, 7, 512, 512, 3),    # stage-5 c2
+    (3, 9, 72, 64, 3),      # K = 64 channels of dy, C = 72, odd spatial size
+])
+def test_conv_dgrad4w_feed_vs_fp32(N, H, C, K, R):
+    """3x3 unit-stride data gradient on the 4-wave kernel (dy gathered with reversed taps) with the
+    feeding-BN epilogue: g = dx * ReLU bits stored, partial sums (sum g, sum g * y), vs fp32."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    torch.manual_seed(N + H + C + K)
+    pad = R // 2
+    dy = (torch.rand(N, H, H, K, device="cuda") * 2 - 1).bfloat16()
+    w = ((torch.rand(K, R, R, C, device="cuda") * 2 - 1) * (1.0 / (R * R * K) ** 0.5)).bfloat16()
+    wt = w.permute(3, 1, 2, 0).contiguous()  # [C][R][S][K]
+    y = (torch.rand(N, H, H, C, device="cuda") * 2 - 1).bfloat16()
+    M = N * H * H
+    mask = torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device="cuda")
+    old = G._DGRAD4W
+    G._DGRAD4W = 2
+    try:
+        out, part, T = G.conv_dgrad(dy, wt, (N, H, H, C), (1, 1), (pad, pad), bn_stat=(y, mask))
+        kinds = []
+        saved, G._LOG = G._LOG, []
+        try:
+            G.conv_dgrad(dy, wt, (N, H, H, C), (1, 1), (pad, pad), bn_stat=(y, mask))
+            kinds = [e_[0] for e_ in G.gemm_log()]
+        finally:
+            G._LOG = saved
+    finally:
+        G._DGRAD4W = old
+    assert any(k_.startswith("dgrad4w") for k_ in kinds), kinds
+    dx = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                    padding=pad).permute(0, 2, 3, 1).reshape(M, C)
+    bits = ((mask.view(-1, 1).int() >> torch.arange(8, device="cuda")) & 1).reshape(M, C).float()
+    ref = dx * bits
+    got = out.float().reshape(M, C)
+    assert _rel(got, ref) < 8e-3
+    assert torch.all(got[bits == 0] == 0)
+    assert T == 2 * -(-M // 256)
+    s = part.sum(0)
+    yf = y.float().reshape(M, C)
+    assert _rel(s[0], got.sum(0)) < 1e-4
+    assert _rel(s[1], (got * yf).sum(0)) < 1e-4

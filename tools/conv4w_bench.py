@@ -49,3 +49,25 @@ for name, H, C, K, R, st in SHAPES:
     print("%-8s M=%7d N=%5d K=%5d  conv_fwd %7.1f us %5.0f TF/s  conv_fwd4w %7.1f us %5.0f TF/s  (%.2fx)"
           % (name, M, K, R * R * C, to, fl / to / 1e6, tn, fl / tn / 1e6, to / tn), flush=True)
 print("total conv_fwd %.1f us, conv_fwd4w %.1f us" % tuple(tot))
+
+# unit-stride 3x3 data gradients with the feeding-BN epilogue (conv_dgrad(bn_stat=...)): the
+# 256-row gather kernel vs the 4-wave kernel (TTD_DGRAD4W policy forced per arm)
+print()
+tot = [0.0, 0.0]
+for name, H, C, K in (("s4_c2", 14, 256, 256), ("s5_c2", 7, 512, 512)):
+    dy = (torch.randn(B, H, H, K, device="cuda") * 0.5).bfloat16()
+    wt = (torch.randn(C, 3, 3, K, device="cuda") * 0.05).bfloat16()
+    y = (torch.randn(B, H, H, C, device="cuda")).bfloat16()
+    mask = torch.randint(0, 256, (B * H * H * C // 8,), dtype=torch.uint8, device="cuda")
+    out = torch.empty((B, H, H, C), dtype=torch.bfloat16, device="cuda")
+    res = []
+    for mode in (0, 2):
+        G._DGRAD4W = mode
+        res.append(t(lambda: G.conv_dgrad(dy, wt, (B, H, H, C), (1, 1), (1, 1), out=out, bn_stat=(y, mask))))
+    G._DGRAD4W = 1
+    fl = 2.0 * B * H * H * C * 9 * K
+    tot[0] += res[0]
+    tot[1] += res[1]
+    print("%-8s dgrad M=%7d N=%5d K=%5d  256-row %7.1f us %5.0f TF/s  4-wave %7.1f us %5.0f TF/s  (%.2fx)"
+          % (name, B * H * H, C, 9 * K, res[0], fl / res[0] / 1e6, res[1], fl / res[1] / 1e6, res[0] / res[1]), flush=True)
+print("total 256-row %.1f us, 4-wave %.1f us" % tuple(tot))
