@@ -89,8 +89,10 @@ def build_resnet(args, dev, rank, world):
                    "seq_len": None, "parallelism": "dp%d" % world,
                    "optimizer": ("LAMB wd 5e-5" if args.optimizer == "lamb" else "momentum-SGD 0.9, wd 5e-5")
                    + ", fp32 master",
-                   "precision": "fp8 e4m3 forward convs (delayed scaling), bf16 backward" if args.precision == "fp8"
-                   else "bf16"},
+                   "precision": ("fp8: e4m3 forward of the 3x3 and 1x1 convs with >= 128 channels in and out, "
+                                 "e5m2 x e4m3 unit-stride data gradients and e5m2 x e4m3 weight gradients "
+                                 "(delayed scaling); stem, strided data gradients, BN and FC in bf16")
+                   if args.precision == "fp8" else "bf16"},
     }
     return step, B, info
 

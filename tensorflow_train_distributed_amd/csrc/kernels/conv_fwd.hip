@@ -110,8 +110,14 @@ TTDK_EXPORT int ttdk_conv_dgrad_fp8(const uint8_t* dy8, const uint8_t* wt8, cons
   if (pe.by && (pe.stat == nullptr || pe.ldo % 8 || pe.act)) return hipErrorInvalidValue;
   const int N = g->C, K = g->R * g->S * g->K;
   const int M = g->N * g->H * g->W;
-  const big::ConvP pa = conv_params(dy8, g->P, g->Q, g->K, g->H, g->W, g, M);
   const big::DenseP pb{wt8, K, N};
+  if (is_pointwise(g)) {
+    // 1x1: dy8 is the dense K-major A operand (no per-row gather addressing)
+    const big::DenseP pd{dy8, g->K, M};
+    if (N >= 256) return big::launch<256, big::OpDenseK<128, 1>, big::OpDenseK<128, 1>, 2>(pd, pb, pe, M, N, K, 1, st);
+    return big::launch<128, big::OpDenseK<128, 1>, big::OpDenseK<64, 1>, 2>(pd, pb, pe, M, N, K, 1, st);
+  }
+  const big::ConvP pa = conv_params(dy8, g->P, g->Q, g->K, g->H, g->W, g, M);
   if (N >= 256) return big::launch<256, big::OpConvK<128, 1, true, true>, big::OpDenseK<128, 1>, 2>(pa, pb, pe, M, N, K, 1, st);
   return big::launch<128, big::OpConvK<128, 1, true, true>, big::OpDenseK<64, 1>, 2>(pa, pb, pe, M, N, K, 1, st);
 }

@@ -108,6 +108,18 @@ class ResNet:
         # fp8 forward and the e5m2 dz of the fp8 data gradient): ops.gemm.conv_wgrad_fp8
         self.fp8_wgrad = os.environ.get("TTD_FP8_WGRAD", "1") != "0"
         self.fp8_only_input = os.environ.get("TTD_FP8_ONLY_INPUT", "1") != "0"
+        # precision="fp8": the 1x1 convs with >= 128 input and output channels on fp8 too — forward
+        # from the e4m3 copy the producing BN apply writes, unit-stride data gradients from the e5m2
+        # dz the BN backward-apply pass writes (with the shortcut-gradient accumulate and the
+        # feeding BN's statistics in the epilogue), weight gradients from both copies
+        # (TTD_FP8_1X1=0: 3x3 convs only, the 1x1 convs keep their fused bf16 kernels)
+        self.fp8_1x1 = os.environ.get("TTD_FP8_1X1", "1") != "0"
+        # ... and their weight gradients from the fp8 copies (TTD_FP8_1X1_WGRAD=0: bf16 weight
+        # gradients on the 4-wave transposed-read kernel; the bf16 input and dz stay stored)
+        self.fp8_1x1_wgrad = os.environ.get("TTD_FP8_1X1_WGRAD", "1") != "0"
+        # ... the strided 1x1 projection shortcuts' forward too (TTD_FP8_1X1_S2=1; their data
+        # gradient is bf16 either way: the fp8 one has no sampled-pixel form)
+        self.fp8_1x1_s2 = os.environ.get("TTD_FP8_1X1_S2", "0") != "0"
         self._x8 = {}
         self._x_unstored = set()
         # projection-shortcut BN applied inside the block's last BN pass (its normalised output is
@@ -185,10 +197,13 @@ class ResNet:
     def _fp8_conv(self, c: ConvSpec) -> bool:
         # fp8 where it pays end to end: the 3x3 convs (compute-bound: fp8 MFMA at 2x the bf16
         # rate, 15-43 % faster at the b1024 shapes, tools/fp8_conv_ab.py), K in 128-element
-        # tiles, >= 128 output channels. The 1x1 convs are store-bound (5-23 % faster alone),
-        # and the fp8 copy of their input that the producing BN pass must write cost more than
-        # that: every eligible conv in fp8 measured 1 % slower per step than bf16.
-        return self.precision == "fp8" and c.k > 1 and c.cin_store % 128 == 0 and c.cout >= 128
+        # tiles, >= 128 output channels. The 1x1 convs are store-bound (5-23 % faster alone);
+        # forward-only fp8 there (the producing BN pass writing an fp8 copy next to the bf16 one)
+        # measured 1 % slower per step, so with fp8_1x1 they also take the fp8 data and weight
+        # gradients and the bf16 input copy is dropped where nothing else reads it.
+        if self.precision != "fp8" or c.cin_store % 128 or c.cout < 128:
+            return False
+        return c.k > 1 or (self.fp8_1x1 and c.k == 1 and (c.stride == 1 or self.fp8_1x1_s2))
 
     def _init_fp8(self):
         P = self.params
@@ -235,8 +250,22 @@ class ResNet:
         self._fp8 = True
 
     def _fp8_dgrad_conv(self, c: ConvSpec) -> bool:
-        return (self.precision == "fp8" and self.fp8_dgrad and c.k == 3 and c.stride == 1 and c.cout % 128 == 0
-                and c.cin_store % 8 == 0 and not self._c3_ok(c, 56, 56))
+        if not (self.precision == "fp8" and self.fp8_dgrad and c.stride == 1 and c.cout % 128 == 0):
+            return False
+        if c.k == 1:
+            # (not a c3 whose forward runs bf16 on the streaming kernel with c2's BN apply fused:
+            # no e4m3 input for an fp8 weight gradient, and its fused BN-backward dgrad is cheaper)
+            return self._fp8_conv(c) and not (self._pw_part("c23") and self._pw_fwd_ok(c, True))
+        return c.k == 3 and c.cin_store % 8 == 0 and not self._c3_ok(c, 56, 56)
+
+    def _g8_take(self, c: ConvSpec, need_dx, feeds, feeds2, dx, dx_beta, dx_sampled) -> bool:
+        """This backward of c goes through the e5m2 dz copy (ops.gemm.conv_dgrad_fp8 from the
+        second step on; the first step's pass only collects the gradient amax), so the bf16 fused
+        data-gradient kernels (BN-backward operand prologue, streaming pointwise) are bypassed.
+        The fp8 data gradient has the feeding-BN epilogue (one fed unit) and a dense beta
+        accumulate, not the sampled-pixel one of a strided projection's gradient."""
+        return (self._fp8 is not None and need_dx and c.name in self._g8 and self._wp_cur is not None
+                and feeds is not None and feeds2 is None and (dx is None or bool(dx_beta)) and not dx_sampled)
 
     def _fp8_step_begin(self):
         from ..ops import kernels as K
@@ -528,7 +557,8 @@ class ResNet:
                             fold_stream=self._fold_stream(), keep=self._side_keep)
             self._ready_main(c.name + "_bn/moving_variance")
             return out, None
-        if (need_dx and dstat is not None and feeds is not None and feeds2 is None
+        g8_take = self._g8_take(c, need_dx, feeds, feeds2, dx, dx_beta, dx_sampled)
+        if (need_dx and dstat is not None and feeds is not None and feeds2 is None and not g8_take
                 and self.fuse_bn_bwd and self._pw_part("dgrad") and self._pw_dgrad_ok(c)):
             # BN backward applied inside the data gradient's operand load (streaming pointwise
             # kernel): dz is written once there for the weight gradient, never re-read by the dgrad
@@ -568,7 +598,7 @@ class ResNet:
             return out, (partial, T)
         stride, pad = (c.stride, c.stride), (c.pad, c.pad)
         if (need_dx and dstat is not None and self.fuse_bn_bwd and self.bn_pro and not wgrad_last and not sampled_only
-                and not unstored
+                and not unstored and not g8_take
                 and self.device.type == "cuda" and Kc <= self.BNPRO_MAX_K and c.cin_store <= self.BNPRO_MAX_N
                 and G.dgrad_bnpro_ok(tuple(x.shape), (c.cin_store, c.k, c.k, Kc), stride, pad)):
             # BN backward formed inside the data gradient's operand tile (dz stored there once for
@@ -597,8 +627,8 @@ class ResNet:
         dz8 = None
         wgrad_done = False
         if dstat is not None:
-            g8 = (self._fp8 is not None and need_dx and c.name in self._g8 and self._wp_cur is not None
-                  and feeds is not None and feeds2 is None and dx is None)
+            # (dx given: a c1 data gradient accumulating into the shortcut gradient, beta = 1)
+            g8 = g8_take
             # fp8 weight gradient without an fp8 data gradient (strided 3x3): dz8 still produced
             # from the first step on (the slot collects its amax), consumed from the second
             # Also whenever the forward stored only the fp8 copy of x (_x8_only) but the fp8 data
@@ -642,7 +672,8 @@ class ResNet:
             wt8 = self._wt8_buf[off:off + int(np.prod(shape))].view(shape)
             i8 = self._g8[c.name]
             out, partial, T = G.conv_dgrad_fp8(dz8, wt8, x.shape, stride, pad, bn_stat=(fy, fmask),
-                                               ascale=(self._g_slots[i8][3:4], self._wt8_slots[i8][3:4]))
+                                               ascale=(self._g_slots[i8][3:4], self._wt8_slots[i8][3:4]),
+                                               out=dx, beta=dx_beta if dx is not None else 0, beta_s2=bs2)
             return out, (partial, T)
         if (feeds is not None and feeds2 is None and dx is None and self.fuse_bn_bwd and self.c3_dgrad == 2
                 and self._c3_ok(c, x.shape[1], x.shape[2])):
@@ -734,7 +765,7 @@ class ResNet:
         second step on). TTD_FP8_ONLY_INPUT=0 keeps the bf16 copy."""
         from ..ops import gemm as G
         return (self.fp8_only_input and self.fp8_wgrad and self._fp8 is not None and self._fp8_bwd_steps >= 1
-                and self._fp8_conv(c) and c.name in self._gq
+                and self._fp8_conv(c) and c.name in self._gq and (c.k > 1 or self.fp8_1x1_wgrad)
                 and G.conv_wgrad_fp8_ok(tuple(x_shape), tuple(self.params.var[c.name + "_conv/kernel"].shape),
                                         (c.stride, c.stride), (c.pad, c.pad)))
 
@@ -743,6 +774,7 @@ class ResNet:
         fp8 forward quantised its input and the fp8 data gradient quantises its dz."""
         from ..ops import gemm as G
         return (self.fp8_wgrad and self._fp8 is not None and c.name in self._gq and c.name in self._x8
+                and (c.k > 1 or self.fp8_1x1_wgrad)
                 and G.conv_wgrad_fp8_ok(tuple(x_shape), tuple(self.params.var[c.name + "_conv/kernel"].shape),
                                         (c.stride, c.stride), (c.pad, c.pad)))
 
@@ -929,7 +961,10 @@ class ResNet:
                 c2[2] = torch.empty(o2.numel() // 8, dtype=torch.uint8, device=o2.device)
                 o2_8 = None
             else:
-                o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]), pro=pro2)
+                # (the last block's c3 gets its output gradient from the pooling backward without
+                # BN sums: that path has no e5m2 dz, so its bf16 input stays stored)
+                o2, c2, o2_8 = unit(blk["c2"], o1, True, inp8=o1_8, want8=fp8 and self._fp8_conv(blk["c3"]), pro=pro2,
+                                    consumer=blk["c3"] if nxt is not None else None)
             defer3 = (nxt is not None and self._pw_part("c31") and self._pw_fwd_ok(nxt["c1"], True)
                       and not self._fp8_conv(nxt["c1"]))
             c3_in = y2 if fuse23 else o2

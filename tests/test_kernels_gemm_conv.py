@@ -701,6 +701,62 @@ def test_conv_dgrad_fp8_e5m2_vs_fp32_oracle(cfg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(32, 14, 14, 1024, 256), (128, 7, 7, 512, 2048), (8, 28, 28, 512, 128)])
+def test_conv1x1_fp8_units_vs_fp32_oracle(cfg):
+    """The 1x1 fp8 unit of precision="fp8" (ResNet._fp8_conv with fp8_1x1): forward e4m3 x e4m3,
+    data gradient e5m2 dz x e4m3 filter accumulating into the shortcut gradient (beta = 1) with the
+    feeding BN's masked gradient + (sum g, sum g*y) epilogue, weight gradient e5m2 x e4m3 — each
+    vs the fp32 op on the dequantised operands (tight) and vs the bf16 kernels (fp8 rounding)."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    N, H, W, C, Kc = cfg
+    torch.manual_seed(23 + C)
+    M = N * H * W
+    x = torch.randn(N, H, W, C, device="cuda").relu().bfloat16()
+    w = (torch.randn(Kc, 1, 1, C, device="cuda") / C ** 0.5).bfloat16()
+    dy = (torch.randn(N, H, W, Kc, device="cuda") * 1e-3).bfloat16()
+    s_x = torch.tensor([448.0 / float(x.float().abs().max())], device="cuda")
+    s_w = torch.tensor([448.0 / float(w.float().abs().max())], device="cuda")
+    s_dy = torch.tensor([57344.0 * 0.5 / float(dy.float().abs().max())], device="cuda")
+    x8, w8 = K.quant_fp8(x, s_x), K.quant_fp8(w, s_w)
+    dy8 = K.quant_fp8(dy, s_dy, e5m2=True)
+    wt = K.krsc_to_crsk(w)
+    wt8 = K.quant_fp8(wt, s_w)
+    # exact decodes (fp8 values are bf16-representable at unit scale), scaled in fp32
+    one = torch.ones(1, device="cuda")
+    xq = K.dequant_fp8(x8, one).float() / s_x
+    wq = K.dequant_fp8(w8, one).float().view(Kc, C) / s_w
+    dyq = K.dequant_fp8(dy8, one, e5m2=True).float() / s_dy
+    # forward
+    y = G.conv_fwd_fp8(x8, w8, (1, 1), (0, 0), ascale=(1.0 / s_x, 1.0 / s_w))
+    assert _rel(y, (xq.view(M, C) @ wq.t()).view(N, H, W, Kc)) < 1e-2
+    assert _rel(y, G.conv_fwd(x, w, (1, 1), (0, 0)).float()) < 0.08
+    # data gradient: dx = old + dz . W, masked, with the feeding BN's sums
+    old = (torch.randn(N, H, W, C, device="cuda") * 1e-3).bfloat16()
+    out = old.clone()
+    yb = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    mask = torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device="cuda")
+    inv = (1.0 / s_dy, 1.0 / s_w)
+    _, part, T = G.conv_dgrad_fp8(dy8, wt8, (N, H, W, C), (1, 1), (0, 0), ascale=inv, out=out, beta=1,
+                                  bn_stat=(yb, mask))
+    bits = ((mask.view(-1, 1) >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1).view(N, H, W, C).float()
+    wtq = K.dequant_fp8(wt8, one).float().view(C, Kc) / s_w
+    ref = ((dyq.view(M, Kc) @ wtq.t()).view(N, H, W, C) + old.float()) * bits
+    assert _rel(out, ref) < 1e-2
+    sums = part[:T].sum(0)
+    assert torch.allclose(sums[0], out.float().view(-1, C).sum(0), rtol=2e-2, atol=1e-5)
+    assert torch.allclose(sums[1], (out.float() * yb.float()).view(-1, C).sum(0), rtol=2e-2, atol=1e-4)
+    ref_bf = (G.conv_dgrad(dy, wt, (N, H, W, C), (1, 1), (0, 0)).float() + old.float()) * bits
+    assert _rel(out, ref_bf) < 0.12
+    # weight gradient
+    assert G.conv_wgrad_fp8_ok(x8.shape, (Kc, 1, 1, C))
+    dw = G.conv_wgrad_fp8(x8, dy8, (Kc, 1, 1, C), (1, 1), (0, 0), ascale=(1.0 / s_dy, 1.0 / s_x))
+    ref_w = (dyq.view(M, Kc).t() @ xq.view(M, C)).view(Kc, 1, 1, C)
+    assert _rel(dw, ref_w) < 1e-4
+    assert _rel(dw, G.conv_wgrad(x, dy, (Kc, 1, 1, C), (1, 1), (0, 0))) < 0.1
+
+
+@pytest.mark.gpu
 def test_bn_backward_apply_e5m2_copy_and_amax():
     """The BN backward-apply pass's OCP e5m2 copy of dz (delayed scale from the slot) dequantises
     to dz within e5m2 rounding, and the slot's amax lanes receive max |dz|."""

@@ -187,12 +187,18 @@ def test_resnet_step_segmented_capture_matches_eager():
 
 
 @pytest.mark.gpu
-def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
+@pytest.mark.parametrize("fp8_1x1,min_cos", [(False, 0.9), (True, 0.8)])
+def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb(monkeypatch, fp8_1x1, min_cos):
     """precision="fp8": the 3x3 convs with 128-multiple input channels run the fp8 block-scaled
     MFMA forward with delayed activation scaling, and the unit-stride 3x3 data gradients the fp8
     MFMA with e5m2 gradients (delayed scaling; step 1 calibrates both); the step must track the
-    bf16 engine and train with LAMB."""
+    bf16 engine and train with LAMB. fp8_1x1 (TTD_FP8_1X1, the default): the 1x1 convs with >= 128
+    channels in and out too — forward, data and weight gradients — which puts e5m2 rounding on
+    every data gradient of this 16-image, 64..256-channel net (gradient cosine vs bf16 0.85 here;
+    at ResNet-50 b1024 the loss tracks bf16 to 0.0 % over 120 LAMB steps,
+    profiles/r6_fp8_1x1_ab.txt)."""
     from tensorflow_train_distributed_amd.train.flat import FlatLAMB, Schedule
+    monkeypatch.setenv("TTD_FP8_1X1", "1" if fp8_1x1 else "0")
     torch.manual_seed(0)
     stages = ((64, 2, 1), (128, 2, 2), (256, 1, 2))
     x = torch.randn(16, 64, 64, 3, device="cuda").bfloat16()
@@ -201,13 +207,15 @@ def test_resnet_fp8_forward_path_tracks_bf16_and_trains_with_lamb():
     f8 = ResNet(stages, num_classes=10, device="cuda", seed=7, precision="fp8")
     assert sum(f8._fp8_conv(c) for c in f8.conv_list()) >= 3
     assert len(f8._g8) >= 1  # a unit-stride 3x3 data gradient on the fp8 MFMA (e5m2 gradients) from step 2
+    assert any(c.k == 1 and f8._fp8_conv(c) for c in f8.conv_list()) == fp8_1x1
+    assert any(c.k == 1 and c.name in f8._g8 for c in f8.conv_list()) == fp8_1x1
     s_ref = ref.forward_backward(x, y).clone()
     f8.forward_backward(x, y)  # step 1 calibrates the delayed activation scales
     s8 = f8.forward_backward(x, y).clone()
     assert abs(float(s8[0]) - float(s_ref[0])) < 0.05 * float(s_ref[0])
     a, b = f8.params.grad, ref.params.grad
     cos = float(torch.dot(a, b) / (a.norm() * b.norm()))
-    assert cos > 0.9, cos
+    assert cos > min_cos, cos
     opt = FlatLAMB(f8.params, Schedule(kind=0, base_lr=0.02), weight_decay=1e-4)
     losses = []
     for _ in range(12):
