@@ -337,6 +337,7 @@ class ResNet:
     # (dz channels, dx channels) of the data gradients that run faster on the streaming kernel with
     # the unit's BN backward as prologue and the LDS-DMA epilogue (tools/pw_bench.py, b1024):
     # stage-2 c3 (256 -> 64) and c1 (64 -> 256, accumulating into the shortcut gradient)
+    # (the stage-3 c1s, 128 -> 256 / 512, measured slower there: 66.7 / 67.7 vs 65.9 ms per step)
     PW_DGRAD_SHAPES = {(256, 64), (64, 256)}
 
     # 1x1 dgrads with the BN backward as LDS operand prologue where it measured faster than the
