@@ -540,6 +540,308 @@ __global__ __launch_bounds__(T, 1) void gemm4t_kernel(const bf16_t* __restrict__
   if (tid == 0) ctr[t] = 0;  // ready for the next launch on this counter block
 }
 
+// ------------------------------------------------------------------------------ fp8 form
+// dW[M,N] (+)= sa * sb * A8^T . B8: A8 = dy in OCP e5m2 [K][M] (K = pixels), B8 = x in e4m3 —
+// dense [K][N] or the im2col gather of x [N][H][W][C] — on v_mfma_scale_f32_32x32x64_f8f6f4 (fp8
+// at twice the bf16 rate; block scales fixed at 2^0, the per-tensor inverse scales sa / sb are
+// device scalars applied in the epilogue). The weight gradients of the fp8 convolutions
+// (precision="fp8"; the 8-wave conv_wgrad_fp8 kernel is the fallback): same K-tile footprint and
+// the same phase schedule as the bf16 kernel above:
+//  * K-tile = 128 k-rows x 256 B per operand (32 KB), two K-steps of 64 k;
+//  * 32 x 32 fragments: lane l holds column l & 31, k = 32 (l >> 5) .. +31 of the K-step (32 B),
+//    four ds_read_b64_tr_b8 (lane i of a 16-lane group addresses k-row k0 + i / 2 at column
+//    byte 8 (i & 1) of its 16-column half and receives 8 consecutive k of its own column); per
+//    K-step 4 A + 4 B fragments = 64 VGPRs, two sets double-buffered across the K-steps; 16
+//    MFMAs of 32 passes per K-step into 4 x 4 accumulators of 16 AGPRs;
+//  * LDS rows of 256 B: the 16-B chunk c of k-row r sits at c ^ ((r & 7) << 1), so the 8 k-rows
+//    x 2 column halves of one half-wave's transposed read fall on 16 different chunks (each of
+//    the 64 banks once); the DMA fetches, per lane, the global chunk that lands in its
+//    lane-linear LDS slot (the XOR depends only on the lane: one offset per operand);
+//  * output lane l, item v of accumulator (a, b): row m0 + 128 wm + 32 a + (l & 31), column
+//    n0 + 128 wn + 32 b + 8 (v / 4) + 4 (l >> 5) + v % 4 (4 consecutive columns per 16-B store).
+namespace f8 {
+constexpr int OP = 128 * 256;     // operand K-tile image bytes
+constexpr int NA = 4, NB = 4, NF = NA + NB, NMF = NA * NB, PA = 8, NQ = 16;
+constexpr int SB = 2 * OP;        // B stages at SB, SB + OP
+constexpr int SMEMB = 4 * OP;
+constexpr int SLABB = 256 * 256;  // floats of one split's partial tile
+}  // namespace f8
+
+typedef __attribute__((ext_vector_type(2))) int ttd_i32x2_t;
+typedef __attribute__((ext_vector_type(8))) int ttd_i32x8_t;
+typedef __attribute__((ext_vector_type(16))) float ttd_f32x16_t;
+typedef __attribute__((address_space(3))) ttd_i32x2_t lds_i2_t;
+
+__device__ __forceinline__ ttd_i32x2_t trd8(const lds_char_t* p) {
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_i2_t*)p);
+}
+
+// acc (+)= x8 . dy8 products: src0 = the B fragment (x, e4m3: cbsz 0), src1 = the A fragment (dy,
+// e5m2: blgp 1), block scales `one` = 127 (2^0 in E8M0). The leading s_nop 1: hipcc may
+// rematerialise `one` (a VALU write) right before the asm, and a VALU-written MFMA operand needs 2
+// wait states.
+template <bool FIRST>
+__device__ __forceinline__ void mfma8(ttd_f32x16_t& c, const ttd_i32x8_t& a, const ttd_i32x8_t& b, int one) {
+  if constexpr (FIRST)
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] blgp:1"
+                 : "=a"(c)
+                 : "v"(b), "v"(a), "v"(one)
+                 : "memory");
+  else
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] blgp:1"
+                 : "+a"(c)
+                 : "v"(b), "v"(a), "v"(one)
+                 : "memory");
+}
+
+__device__ __forceinline__ uint32_t gather_voff8(const Gather& G, const GCol& gc, int k) {
+  const int n = static_cast<int>(__umulhi(static_cast<unsigned>(k), G.pq_m) >> G.pq_s);
+  const int rem = k - n * G.PQ;
+  const int p = static_cast<int>(__umulhi(static_cast<unsigned>(rem), G.q_m) >> G.q_s);
+  const int q = rem - p * G.Q;
+  const int hb = p * G.sh - G.ph, wb = q * G.sw - G.pw;
+  const bool ok = static_cast<unsigned>(hb + gc.r[0]) < static_cast<unsigned>(G.H) &&
+                  static_cast<unsigned>(wb + gc.s[0]) < static_cast<unsigned>(G.W);
+  return ok ? static_cast<uint32_t>(((n * G.H + hb) * G.W + wb) * G.C + gc.toff[0]) : kOob;
+}
+
+template <bool GB>
+__global__ __launch_bounds__(T, 1) void gemm4t8_kernel(const uint8_t* __restrict__ A, long long lda,
+                                                      const uint8_t* __restrict__ B, long long ldb, int M, int N,
+                                                      int K, int tiles_m, int tiles_n, int splits, int kt_per,
+                                                      float* __restrict__ ws, float* __restrict__ out, int beta,
+                                                      const float* __restrict__ sa, const float* __restrict__ sbv,
+                                                      int* __restrict__ ctr, Gather G, long long b_bytes) {
+  using namespace f8;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEMB + 16];
+  asm volatile("" : "+s"(out), "+s"(ws), "+s"(ctr), "+s"(beta), "+s"(sa), "+s"(sbv));
+  const int tiles = tiles_m * tiles_n;
+  const int w = xcd_remap(blockIdx.x, tiles * splits);
+  const int split = w / tiles, t = w - split * tiles;
+  int tm, tn;
+  tile_of(t, tiles_m, tiles_n, 8, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kt0 = split * kt_per;
+  const int nk = min(kt_per, K / 128 - kt0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  lds_char_t* const lds = (lds_char_t*)smem;
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
+  // fragment read base (K-step 0, read 0, fragment 0): k-row 32 (l >> 5) + (l & 15) / 2, chunk
+  // (8 w | h) ^ (l & 14) with h = the lane's 16-column half; fragment j is base ^ (32 j), K-step
+  // and read q are immediates (16 KB, 2 KB)
+  const uint32_t rrow = static_cast<uint32_t>(32 * (lane >> 5) + ((lane & 15) >> 1));
+  const uint32_t hx = static_cast<uint32_t>((lane >> 4) & 1), fx = static_cast<uint32_t>(lane & 14);
+  const uint32_t bA0 = sb + rrow * 256 + ((((wm * 8) | hx) ^ fx) << 4) + 8 * (lane & 1);
+  const uint32_t bB0 = sb + SB + rrow * 256 + ((((wn * 8) | hx) ^ fx) << 4) + 8 * (lane & 1);
+  const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
+  // DMA: piece i of thread tid = k-row 16 i + tid / 16, physical chunk tid % 16 = logical chunk
+  // (tid % 16) ^ ((tid / 16 & 7) << 1) (columns past the operand's end clamped to its last 16)
+  const int pr = tid >> 4, lcol = ((tid & 15) ^ ((pr & 7) << 1)) * 16;
+  const ttd_i32x4_t srd_a = make_srd(A, static_cast<uint32_t>(static_cast<long long>(K) * lda));
+  const uint32_t voff_a = static_cast<uint32_t>(static_cast<long long>(pr) * lda + min(m0 + lcol, M - 16));
+  ttd_i32x4_t srd_b;
+  uint32_t voff_b = 0;
+  GCol gc;
+  uint32_t gv[8];  // GB: this lane's source offsets of the 8 B pieces of the next K-tile to load
+  if constexpr (GB) {
+    srd_b = make_srd(B, static_cast<uint32_t>(b_bytes));
+    const int col = min(n0 + lcol, N - 16);
+    const int tap = col / G.C, c = col - tap * G.C;
+    gc.r[0] = tap / G.S;
+    gc.s[0] = tap - gc.r[0] * G.S;
+    gc.toff[0] = (gc.r[0] * G.W + gc.s[0]) * G.C + c;
+  } else {
+    srd_b = make_srd(B, static_cast<uint32_t>(static_cast<long long>(K) * ldb));
+    voff_b = static_cast<uint32_t>(static_cast<long long>(pr) * ldb + min(n0 + lcol, N - 16));
+  }
+  auto gather_piece = [&](int kt, int i) {
+    if constexpr (GB) gv[i] = gather_voff8(G, gc, (kt0 + kt) * 128 + i * 16 + pr);
+  };
+  const int kstride_a = static_cast<int>(lda * 128), kstride_b = static_cast<int>(ldb * 128);
+  const int prow_a = static_cast<int>(lda * 16), prow_b = static_cast<int>(ldb * 16);
+  int one = 127;
+  asm volatile("" : "+v"(one));
+
+  ttd_f32x16_t acc[NA][NB];
+  ttd_i32x2_t fr[2][NF][4];  // [set][fragment: 0..NA-1 A, NA.. B][read q]
+
+  // read r (0 .. 4 NF - 1) of K-step S of the image in stage st into fragment set SET
+  auto rd1 = [&](auto R, auto S, int st, auto SET) {
+    constexpr int r = decltype(R)::value, s = decltype(S)::value, set = decltype(SET)::value;
+    constexpr int fi = r / 4, q = r % 4, blk = fr_blk<NA, NB>(fi);
+    constexpr bool isa = fr_is_a<NA, NB>(fi);
+    constexpr int imm = s * 16384 + q * 2048;
+    const uint32_t base = (isa ? bA0 : bB0) + st * OP;
+    fr[set][isa ? blk : NA + blk][q] = trd8((const lds_char_t*)(uintptr_t)((blk ? (base ^ (32u * blk)) : base) + imm));
+  };
+  auto frag = [&](int set, int slot) {
+    const ttd_i32x2_t* v = fr[set][slot];
+    const auto lo = __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3);
+    const auto hi = __builtin_shufflevector(v[2], v[3], 0, 1, 2, 3);
+    return static_cast<ttd_i32x8_t>(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto m0_of = [&](int qq, int st) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
+        ldsw + (qq < PA ? st * OP + qq * 4096 : SB + st * OP + (qq - PA) * 4096))));
+  };
+  auto dma1 = [&](auto Q, int st, int kt) {  // piece q of K-tile kt into stage st (M0 = its base)
+    constexpr int qq = decltype(Q)::value;
+    const uint32_t next = qq < NQ - 1 ? m0_of(qq + 1, st) : m0_of(0, st ^ 1);
+    if constexpr (qq < PA) {
+      dma_chain(voff_a, srd_a, (kt0 + kt) * kstride_a + qq * prow_a, next);
+    } else {
+      constexpr int i = qq - PA;
+      if constexpr (GB) dma_chain(gv[i], srd_b, 0, next);
+      else dma_chain(voff_b, srd_b, (kt0 + kt) * kstride_b + i * prow_b, next);
+    }
+  };
+
+  // phases per K-tile (as the bf16 kernel): 0 = K-step 0 (16 MFMAs) | the 32 reads of K-step 1;
+  // 1a = first half of K-step 1 | A pieces of K-tile kt + 2 into the freed stage; 1b = second
+  // half | B pieces of kt + 2 | the 32 reads of K-tile kt + 1, K-step 0
+  constexpr int NR = 4 * NF, H0 = NMF, H1 = NMF / 2;
+  auto ktile = [&](int kt, auto first, auto has2c) {
+    constexpr bool FIRST = decltype(first)::value;
+    constexpr bool has2 = decltype(has2c)::value;
+    const int st = kt & 1;
+    static_for<H0>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      static_for<NR>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (j * H0 / NR == i) rd1(J, std::integral_constant<int, 1>{}, st, std::integral_constant<int, 1>{});
+      });
+      mfma8<FIRST>(acc[i / NB][i % NB], frag(0, i / NB), frag(0, NA + i % NB), one);
+      if constexpr (GB && has2 && (i & 1)) gather_piece(kt + 2, i / 2);
+    });
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    asm volatile("s_barrier" ::: "memory");
+    static_for<H1>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (has2) dma1(std::integral_constant<int, i>{}, st, kt + 2);
+      mfma8<false>(acc[i / NB][i % NB], frag(1, i / NB), frag(1, NA + i % NB), one);
+    });
+    if constexpr (has2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    static_for<H1>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (has2) dma1(std::integral_constant<int, PA + i>{}, st, kt + 2);
+      static_for<NR>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (j * H1 / NR == i) rd1(J, std::integral_constant<int, 0>{}, st ^ 1, std::integral_constant<int, 0>{});
+      });
+      mfma8<false>(acc[NA / 2 + i / NB][i % NB], frag(1, NA / 2 + i / NB), frag(1, NA + i % NB), one);
+    });
+  };
+
+  // prologue: K-tiles 0 and 1 into stages 0 and 1, K-step 0 fragments of K-tile 0
+  m0_init(m0_of(0, 0));
+  if constexpr (GB)
+    for (int i = 0; i < 8; ++i) gather_piece(0, i);
+  static_for<NQ>([&](auto Q) { dma1(Q, 0, 0); });
+  if constexpr (GB)
+    if (nk > 1)
+      for (int i = 0; i < 8; ++i) gather_piece(1, i);
+  static_for<NQ>([&](auto Q) { dma1(Q, 1, 1); });
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NQ) : "memory");
+  static_for<NR>([&](auto R) { rd1(R, std::integral_constant<int, 0>{}, 0, std::integral_constant<int, 0>{}); });
+  if (nk >= 3) {
+    ktile(0, std::true_type{}, std::true_type{});
+    for (int kt = 1; kt < nk - 2; ++kt) ktile(kt, std::false_type{}, std::true_type{});
+    ktile(nk - 2, std::false_type{}, std::false_type{});
+    ktile(nk - 1, std::false_type{}, std::false_type{});
+  } else {
+    ktile(0, std::true_type{}, std::false_type{});
+    if (nk == 2) ktile(1, std::false_type{}, std::false_type{});
+  }
+  // a 32-pass MFMA's result: >= 34 wait states before a non-MFMA reader
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) asm volatile("" : "+a"(acc[a][b]));
+
+  const float scale = sa[0] * sbv[0];
+  const bool whole = m0 + 256 <= M && n0 + 256 <= N;
+  auto store = [&](int a, int b, int v4, f32x4_t v) {
+    const int m = m0 + wm * 128 + a * 32 + (lane & 31), n = n0 + wn * 128 + b * 32 + 8 * v4 + 4 * (lane >> 5);
+    if (whole || (m < M && n < N)) {
+      f32x4_t* o = reinterpret_cast<f32x4_t*>(out + static_cast<long long>(m) * N + n);
+      if (beta) v += *o;
+      *o = v;
+    }
+  };
+  auto part = [&](const ttd_f32x16_t& c, int v4) {
+    return f32x4_t{c[4 * v4], c[4 * v4 + 1], c[4 * v4 + 2], c[4 * v4 + 3]};
+  };
+  // lane-linear partial tile: accumulator (a, b), quarter v4 at ((a NB + b) 4 + v4) 256 + 4 lane
+  const long long lin = static_cast<long long>(wave) * NMF * 1024 + lane * 4;
+  if (splits == 1) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        asm volatile("" : "+a"(acc[a][b]));
+#pragma unroll
+        for (int v4 = 0; v4 < 4; ++v4) store(a, b, v4, part(acc[a][b], v4) * scale);
+      }
+    return;
+  }
+  float* slab = ws + static_cast<long long>(split * tiles + t) * SLABB + lin;
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      asm volatile("" : "+a"(acc[a][b]));
+#pragma unroll
+      for (int v4 = 0; v4 < 4; ++v4)
+        *reinterpret_cast<f32x4_t*>(slab + ((a * NB + b) * 4 + v4) * 256) = part(acc[a][b], v4);
+    }
+  // release the partials, count arrivals per tile
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __threadfence();
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem + SMEMB);
+  if (tid == 0) flag[0] = atomicAdd(ctr + t, 1) == splits - 1;
+  __syncthreads();
+  if (!flag[0]) return;
+  __threadfence();  // acquire: the other splits' partials
+  // last split of this tile: the partials summed in split order (deterministic whoever is last)
+  const float* src0 = ws + static_cast<long long>(t) * SLABB + lin;
+  const long long sstride = static_cast<long long>(tiles) * SLABB;
+#pragma unroll 1
+  for (int ab = 0; ab < NMF; ++ab) {
+    f32x4_t v[4];
+#pragma unroll
+    for (int v4 = 0; v4 < 4; ++v4) v[v4] = *reinterpret_cast<const f32x4_t*>(src0 + (ab * 4 + v4) * 256);
+    int s = 1;
+    for (; s + 4 <= splits; s += 4) {
+      f32x4_t x[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v4 = 0; v4 < 4; ++v4)
+          x[u][v4] = __builtin_nontemporal_load(
+              reinterpret_cast<const f32x4_t*>(src0 + (s + u) * sstride + (ab * 4 + v4) * 256));
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v4 = 0; v4 < 4; ++v4) v[v4] += x[u][v4];
+    }
+    for (; s < splits; ++s)
+#pragma unroll
+      for (int v4 = 0; v4 < 4; ++v4)
+        v[v4] += *reinterpret_cast<const f32x4_t*>(src0 + s * sstride + (ab * 4 + v4) * 256);
+#pragma unroll
+    for (int v4 = 0; v4 < 4; ++v4) store(ab / NB, ab % NB, v4, v[v4] * scale);
+  }
+  if (tid == 0) ctr[t] = 0;  // ready for the next launch on this counter block
+}
+
 }  // namespace g4t
 }  // namespace
 }  // namespace ttdk
@@ -681,5 +983,71 @@ TTDK_EXPORT int ttdk_conv_wgrad4t(const bf16_t* x, const bf16_t* dy, const TtdkC
     hipLaunchKernelGGL((g4t::gemm4t_kernel<false, true>), dim3(tiles * splits), dim3(g4t::T), 0, st, dy,
                        static_cast<long long>(g->K), x, 0LL, M, N, K, tiles_m, tiles_n, splits, per, ws, dw, beta, 1.f,
                        ctr, nullptr, nullptr, G, xb);
+  return hipGetLastError();
+}
+
+// floats of workspace ttdk_conv_wgrad4t8 needs (-1: the fp8 kernel does not take the conv): C and
+// K multiples of 16 (16-B DMA chunks of 16 channels), >= 16 output rows / columns, pixels a
+// multiple of 128 (whole K-tiles), operands under 2 GiB (the gather's out-of-range offset)
+TTDK_EXPORT long long ttdk_conv_wgrad4t8_ws(const TtdkConv* g, int splits) {
+  using namespace ttdk;
+  const int M = g->K, N = g->R * g->S * g->C;
+  const long long K = static_cast<long long>(g->N) * g->P * g->Q;
+  const long long xb = static_cast<long long>(g->N) * g->H * g->W * g->C, yb = K * g->K;
+  if (!g4t_enabled() || g->C % 16 || g->K % 16 || M < 16 || N < 16 || K % 128 || K < 128 || g->dh != 1 ||
+      g->dw != 1 || xb >= (1LL << 31) || yb >= (1LL << 31) || (!is_pointwise(g) && (g->P * g->Q < 2 || g->Q < 2)))
+    return -1;
+  const int ktiles = static_cast<int>(K / 128);
+  splits = std::max(1, std::min(splits, ktiles / 2));
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  return static_cast<long long>(splits) * ceil_div(M, 256) * ceil_div(N, 256) * 256 * 256;
+}
+
+// fp8 convolution weight gradient dw[K][R][S][C] (+)= sa * sx * sum over pixels of dy8 (x) im2col(x8)
+// on the 4-wave transposed-read kernel (g4t::gemm4t8_kernel): dy8 [pixels][K] OCP e5m2, x8 e4m3
+// ([pixels][C] for unit-stride 1x1 convs, else gathered), sa / sx the inverse quantisation scales
+// (device fp32); split-K summed inside the launch. ws: ttdk_conv_wgrad4t8_ws floats.
+// hipErrorInvalidValue: the kernel does not take the conv (the caller keeps conv_wgrad_fp8).
+TTDK_EXPORT int ttdk_conv_wgrad4t8(const uint8_t* x8, const uint8_t* dy8, const TtdkConv* g, float* dw, float* ws,
+                                   int splits, int beta, const float* sa, const float* sx, hipStream_t st) {
+  using namespace ttdk;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (ttdk_conv_wgrad4t8_ws(g, splits) < 0 || !sa || !sx || !al16(x8) || !al16(dy8) || !al16(dw))
+    return hipErrorInvalidValue;
+  const int M = g->K, N = g->R * g->S * g->C, K = g->N * g->P * g->Q;
+  const int ktiles = K / 128;
+  splits = std::max(1, std::min(splits, ktiles / 2));
+  const int per = ceil_div(ktiles, splits);
+  splits = ceil_div(ktiles, per);
+  const int tiles_m = ceil_div(M, 256), tiles_n = ceil_div(N, 256), tiles = tiles_m * tiles_n;
+  int* ctr = nullptr;
+  if (splits > 1) {
+    ctr = big::tile_counters(st, tiles);
+    if (!ctr || !ws) return hipErrorInvalidValue;
+  }
+  g4t::Gather G{};
+  const dim3 grid(tiles * splits);
+  if (is_pointwise(g)) {
+    hipLaunchKernelGGL((g4t::gemm4t8_kernel<false>), grid, dim3(g4t::T), 0, st, dy8, static_cast<long long>(g->K), x8,
+                       static_cast<long long>(g->C), M, N, K, tiles_m, tiles_n, splits, per, ws, dw, beta, sa, sx, ctr,
+                       G, 0LL);
+    return hipGetLastError();
+  }
+  G.H = g->H;
+  G.W = g->W;
+  G.C = g->C;
+  G.Q = g->Q;
+  G.PQ = g->P * g->Q;
+  G.S = g->S;
+  G.sh = g->sh;
+  G.sw = g->sw;
+  G.ph = g->ph;
+  G.pw = g->pw;
+  magic_div(static_cast<unsigned>(G.PQ), &G.pq_m, &G.pq_s);
+  magic_div(static_cast<unsigned>(G.Q), &G.q_m, &G.q_s);
+  const long long xb = static_cast<long long>(g->N) * g->H * g->W * g->C;
+  hipLaunchKernelGGL((g4t::gemm4t8_kernel<true>), grid, dim3(g4t::T), 0, st, dy8, static_cast<long long>(g->K), x8, 0LL,
+                     M, N, K, tiles_m, tiles_n, splits, per, ws, dw, beta, sa, sx, ctr, G, xb);
   return hipGetLastError();
 }

@@ -70,6 +70,8 @@ _SIGS = {
     "ttdk_conv_wgrad4t_ws": [G, I],
     "ttdk_conv_wgrad_bn": [P, P, P, P, G, P, P, I, I, I, I, P],
     "ttdk_conv_wgrad_fp8": [P, P, G, P, P, I, I, P, P, P],
+    "ttdk_conv_wgrad4t8": [P, P, G, P, P, I, I, P, P, P],
+    "ttdk_conv_wgrad4t8_ws": [G, I],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
     "ttdk_set_big_pers": [I],
     # gemm_f32.hip
@@ -147,7 +149,7 @@ def register(sigs: dict):
 
 _RESTYPE = {"ttdk_conv_dgrad_subpixel_stat_rows": c_longlong, "ttdk_colsum_ws_floats": c_longlong,
             "ttdk_gemm_wgrad_bias_ws": c_longlong, "ttdk_gemm4t_ws": c_longlong,
-            "ttdk_conv_wgrad4t_ws": c_longlong}
+            "ttdk_conv_wgrad4t_ws": c_longlong, "ttdk_conv_wgrad4t8_ws": c_longlong}
 
 
 def fn(name):

@@ -904,6 +904,9 @@ _WGRAD4T = int(_os.environ.get("TTD_WGRAD4T", "1"))
 # standalone, cost 0.5 ms: profiles/r6_wgrad4t_step_ab.txt); 0: per shape (128 3x3, 256 1x1)
 _WGRAD4T_WGS = int(_os.environ.get("TTD_WGRAD4T_WGS", "128"))
 _WGRAD4T_MIN_KT = int(_os.environ.get("TTD_WGRAD4T_MIN_KT", "32"))
+# fp8 weight gradients (conv_wgrad_fp8) on the 4-wave transposed-read kernel's fp8 form
+# (gemm4t.hip gemm4t8_kernel); TTD_WGRAD4T8=0: the 8-wave 256x128 kernel (conv_wgrad.hip)
+_WGRAD4T8 = _os.environ.get("TTD_WGRAD4T8", "1") != "0"
 # convs with fewer than 256 output channels (>= TTD_WGRAD4T_MINM) on the kernel's 128-row tile form
 # (gemm4t.hip g4t_bm): TTD_WGRAD4T_SMALL "c3" the filters larger than 1x1, "all" the 1x1 ones too,
 # "none" (default) the previous kernels. Measured (profiles/r6_wgrad4t_small_m.txt): the 128-row
@@ -1017,6 +1020,24 @@ def conv_wgrad_fp8(x8, dy8, w_shape, stride=(1, 1), padding=(0, 0), *, ascale, o
     if out is None:
         out = torch.empty(tuple(w_shape), dtype=torch.float32, device=x8.device)
     M, N, K = g.K, g.R * g.S * g.C, g.N * g.P * g.Q
+    # (1x1 convs with a 4-tile output or less need 64 K-splits whose in-kernel sum by one workgroup
+    # outweighs the faster loop: 0.85-0.89x there, 1.33x at 512x2048; 3x3 1.27-1.54x:
+    # tools/wgrad_fp8_bench.py, profiles/r6_wgrad_fp8_bench_b1024.txt)
+    big1 = M >= 256 and N >= 256 and M * N >= 512 * 1024
+    if (_WGRAD4T8 and (g.R * g.S > 1 or big1 or splits is not None)
+            and int(_lib.query("ttdk_conv_wgrad4t8_ws", ctypes.byref(g), 1)) >= 0):
+        # the 4-wave transposed-read kernel (gemm4t.hip gemm4t8_kernel: 32x32x64 fp8 MFMA, split-K
+        # summed in the launch); splits sized like the bf16 one's (K-tiles of 128 pixels)
+        if splits is None:
+            tiles = -(-M // 256) * -(-N // 256)
+            target = _WGRAD4T_WGS or (128 if g.R * g.S > 1 else 256)
+            splits = max(1, min((K // 128) // max(1, _WGRAD4T_MIN_KT // 2), -(-target // tiles)))
+        nws = int(_lib.query("ttdk_conv_wgrad4t8_ws", ctypes.byref(g), int(splits)))
+        ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x8.device)
+        _log("wgrad4t8_%dx%d_s%d" % (g.R, g.S, g.sh), M, N, K, splits)
+        _lib.call("ttdk_conv_wgrad4t8", x8.data_ptr(), dy8.data_ptr(), ctypes.byref(g), out.data_ptr(), ws.data_ptr(),
+                  int(splits), int(beta), ascale[0].data_ptr(), ascale[1].data_ptr(), _lib.stream())
+        return out
     if splits is None:
         tiles = -(-M // 256) * -(-N // 128)
         splits = max(1, min((K // 128) // 16, -(-BIG_WGRAD_WGS // tiles)))

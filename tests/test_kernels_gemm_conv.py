@@ -813,14 +813,19 @@ def test_weight_gradient_with_fused_bias_rowsum_vs_fp32(M, N, K, splits, beta):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("four_wave", [True, False])
 @pytest.mark.parametrize("cfg", [(2, 16, 16, 256, 256, 1), (1, 16, 16, 128, 128, 1), (4, 8, 8, 512, 512, 1),
-                                 (2, 16, 16, 128, 256, 2), (3, 16, 8, 256, 512, 1), (2, 14, 14, 256, 256, 1)])
-def test_conv_wgrad_fp8_vs_fp32_oracle(cfg):
+                                 (2, 16, 16, 128, 256, 2), (3, 16, 8, 256, 512, 1), (2, 14, 14, 256, 256, 1),
+                                 (16, 8, 8, 512, 512, 1), (8, 16, 16, 256, 256, 2)])
+def test_conv_wgrad_fp8_vs_fp32_oracle(monkeypatch, cfg, four_wave):
     """fp8 weight gradient (e5m2 dy x e4m3 im2col(x), both MN-major through ds_read_b64_tr_b8, block-
     scaled MFMA, split-K) of a 3x3 conv vs the fp32 weight gradient of the DEQUANTISED operands
-    (tight: only the summation order differs) and vs the bf16 weight gradient (fp8 rounding: loose)."""
+    (tight: only the summation order differs) and vs the bf16 weight gradient (fp8 rounding: loose).
+    four_wave: the 4-wave transposed-read kernel's fp8 form (gemm4t8_kernel, 32x32x64 MFMA, split-K
+    summed in the launch; partial 256-column tiles at N = 1152 / 2304), else the 8-wave kernel."""
     from tensorflow_train_distributed_amd.ops import gemm as G
     from tensorflow_train_distributed_amd.ops import kernels as K
+    monkeypatch.setattr(G, "_WGRAD4T8", four_wave)
     N, H, W, C, Kc, s = cfg
     torch.manual_seed(17 + C)
     x = torch.randn(N, H, W, C, device="cuda").relu().bfloat16()
