@@ -49,7 +49,11 @@ def test_resnet50_engine_matches_reference():
     ge = torch.cat([g_engine[m.params.offsets[n]:m.params.offsets[n] + leaves[n].numel()] for n in names])
     gr = torch.cat([leaves[n].grad.flatten() for n in names])
     cos = float(torch.dot(ge, gr) / (ge.norm() * gr.norm()))
-    assert cos > 0.95, (cos, bad[:8])
+    rels = sorted(r[1] for r in report)
+    print("cosine %.5f, per-variable rel median %.4f p90 %.4f max %.4f" % (cos, rels[len(rels) // 2], rels[int(0.9 * len(rels))], rels[-1]))
+    # (measured 0.966: the bf16 forward drift flips near-zero ReLU masks of this 5-stage net;
+    # per-unit numerics are pinned by test_convbn_unit_backward_oracle)
+    assert cos > 0.96, (cos, bad[:8])
     # End to end, the bf16 forward drifts ~1-2% from the fp32 oracle by the last stage, so
     # ReLU masks differ on near-zero activations; per-unit exactness is checked by
     # test_convbn_unit_backward_oracle with shared masks. Here: direction + head exactness.
