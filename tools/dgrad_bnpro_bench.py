@@ -2,7 +2,7 @@
 """A/B of the BN-backward operand prologue on the 256-row dgrad at ResNet-50 b1024 shapes:
 (a) bwd_apply pass (dz = a*g + b*y + c stored) + plain dgrad, vs (b) one dgrad that forms dz
 in LDS and stores it. Times per launch pair (HIP events) and the HBM bytes the pair must move.
-usage: python tools/dgrad_bnpro_bench.py"""
+usage: python tools/dgrad_bnpro_bench.py [--only=s3_c1,s4_c3]"""
 import json
 import os
 import sys
@@ -10,6 +10,10 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+_ONLY = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--only=")]
+_ONLY = _ONLY[0].split(",") if _ONLY else []
 
 
 def timed(fn, iters=10):
@@ -36,6 +40,8 @@ def main():
                                 ("s5_c3", 7, 2048, 512, False), ("s3_c1", 28, 128, 512, True),
                                 ("s4_c1", 14, 256, 1024, True), ("s5_c1", 7, 512, 2048, True),
                                 ("s3b1_c1", 56, 128, 256, True)]:
+        if _ONLY and name not in _ONLY:
+            continue
         g = torch.randn(B, H, H, K, device=dev).bfloat16()
         y = torch.randn(B, H, H, K, device=dev).bfloat16()
         coef = torch.randn(3, K, device=dev) * 0.1
