@@ -172,6 +172,12 @@ class BertPretraining:
         # hipBLASLt) is an A/B and oracle mode only, TTD_BERT_BLASLT: 1 = the forward's bias-only
         # GEMMs, 2 = also the plain / accumulating data gradients, 3 = the weight gradients too.
         self.blaslt = int(os.environ.get("TTD_BERT_BLASLT", "0")) if self.device.type == "cuda" else 0
+        # row-stride padding (elements) of the [tokens, intermediate] activations (FFN1 output, its
+        # pre-activation, the dGELU gradient): with a power-of-two row stride (4096 x 2 B) every row
+        # of a 256-row output tile falls on the same HBM channel group; measured on the FFN1 GEMM
+        # (tools/g4_bench.py shapes): plain store 573 -> 482 us, bias + GELU + aux 640 -> 572 us
+        # (stride 4352). TTD_BERT_IPAD=0: dense rows
+        self.inter_pad = int(os.environ.get("TTD_BERT_IPAD", "256"))
         self._wt = None
         self._wt_batch = None
         # TTD_BERT_WT_BATCH=0: one transpose launch per weight copy instead of one batched launch
@@ -280,6 +286,14 @@ class BertPretraining:
         for w, t in rest:
             K.krsc_to_crsk(w.view(w.shape[0], 1, 1, w.shape[1]), out=t.view(t.shape[0], 1, 1, t.shape[1]))
 
+    def _inter_buf(self, rows):
+        """[rows, intermediate] bf16 activation whose row stride is padded by inter_pad elements
+        (a column view of a wider buffer; every GEMM here takes row-strided operands)."""
+        I = self.cfg.intermediate_size
+        pad = self.inter_pad if self.device.type == "cuda" else 0
+        buf = torch.empty((rows, I + pad), dtype=torch.bfloat16, device=self.device)
+        return buf[:, :I] if pad else buf
+
     def _dgrad(self, dy, l, which, **kw):
         """dx = dy · W for encoder weight `which` (0 = fused QKV, 1.. = _WT_NAMES) of layer l."""
         from ..ops import gemm as G
@@ -350,7 +364,7 @@ class BertPretraining:
             if self.blaslt >= 3:  # A/B: weight gradients through the library too (fp32 output)
                 torch.mm(dy.t(), x, out_dtype=torch.float32, out=wout)
                 if bout is not None:
-                    K.colsum(dy, out=bout)
+                    K.colsum(dy if dy.is_contiguous() else dy.contiguous(), out=bout)
                 return
             splits = G.gemm_wgrad_splits(M, N, Kd, big_wgs=self.wgrad_wgs)
             if bout is not None and self.bias_in_wgrad and G.wgrad_bias_ok(M, N, Kd, splits):
@@ -359,7 +373,8 @@ class BertPretraining:
                 return
             wgrad(dy, x, wout)
             if bout is not None:
-                K.colsum(dy, out=bout)
+                # (the column-sum kernel reads dense rows: a row-padded dy is compacted first)
+                K.colsum(dy if dy.is_contiguous() else dy.contiguous(), out=bout)
 
         deferred = []
 
@@ -441,8 +456,8 @@ class BertPretraining:
                                              P.var[self._ln(l, "attention/output/LayerNorm/beta")], res=x, eps=eps,
                                              p_in=hd, site_in=site(l, 1), rng=rng)
             del proj
-            pre = torch.empty((Tk, c.intermediate_size), dtype=bf, device=dev)
-            inter = G.gemm(y1, P.c[self._ln(l, "intermediate/dense/kernel")], trans_b=True,
+            pre = self._inter_buf(Tk)
+            inter = G.gemm(y1, P.c[self._ln(l, "intermediate/dense/kernel")], trans_b=True, out=self._inter_buf(Tk),
                            bias=P.var[self._ln(l, "intermediate/dense/bias")], act=G.ACT_GELU, aux=pre)
             nb = self._ln(l, "output/dense/bias")
             o2 = self._plain(inter, P.c[self._ln(l, "output/dense/kernel")], P.var[nb], P.c[nb])
@@ -529,11 +544,12 @@ class BertPretraining:
                 # the intermediate bias gradient = column sums of dpre, taken from the per-tile
                 # statistics of the dGELU dgrad epilogue that produces dpre (no separate column-sum
                 # pass over the [tokens, 4096] gradient)
-                dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre, stat=bias_part, tile=(256, 0))
+                dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre, stat=bias_part, tile=(256, 0),
+                                   out=self._inter_buf(Tk))
                 K.col_reduce2(bias_part, bias_part.shape[0], o0=b_inter)
                 b_inter = None
             else:
-                dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre)
+                dpre = self._dgrad(dout2, l, 3, act=G.ACT_DGELU, residual=pre, out=self._inter_buf(Tk))
             del dout2, inter, pre
             wgrad_bias(dpre, y1, g[self._ln(l, "intermediate/dense/kernel")], b_inter, defer=True)
             self._dgrad(dpre, l, 2, out=G1, beta=1)

@@ -451,6 +451,8 @@ def bias_act_dropout_bwd(dy, x, bias, act=ACT_NONE, rate=0.0, seed=0, offset=0, 
 
 def colsum(x2d, out=None, beta=0):
     rows, C = x2d.shape
+    if not x2d.is_contiguous():
+        raise ValueError("colsum reads dense rows (got strides %s)" % (tuple(x2d.stride()),))
     if out is None:
         out = torch.empty(C, dtype=torch.float32, device=x2d.device)
     nws = _lib.query("ttdk_colsum_ws_floats", rows, C, _DT[x2d.dtype])
