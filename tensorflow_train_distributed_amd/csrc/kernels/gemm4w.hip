@@ -860,6 +860,283 @@ __global__ __launch_bounds__(T, 1) void gemm4p_kernel(const bf16_t* __restrict__
   }
 }
 
+
+// ------------------------------------------------------------------------------ fp8 forward
+// fp8 convolution / GEMM on the block-scaled MFMA: C[M][N] (bf16) = sa * sb * A8 . B8^T with A8
+// e4m3 K-major — the dense [M][K] rows of a unit-stride 1x1 conv input or the implicit-GEMM
+// gather of x [N][H][W][C] (C % 128 == 0: a 128-channel K-tile inside one filter tap) — and B8 the
+// [N][K] e4m3 filter (precision="fp8" forward convs; the 8-wave conv_fwd_fp8 kernel is the
+// fallback). The 4-wave transposed-read kernel's fp8 form (gemm4t.hip gemm4t8_kernel) with
+// K-major operands:
+//  * the K-tile images are this file's [256 rows][128 B] (128 k per row), chunk c of row r at
+//    c ^ ((r >> 1) & 7): the loaders are the bf16 ones with byte offsets;
+//  * a lane's 32 x 32 x 64 fragment (row l & 31, k 32 (l >> 5) .. +31 of the K-step) is two
+//    ds_read_b128 of consecutive chunks (16 consecutive rows per 16-lane group: all 64 banks);
+//  * two K-steps of 64 k per K-tile, 4 A + 4 B fragments per K-step (64 VGPRs, two sets), 16
+//    MFMAs of 32 passes into 4 x 4 accumulators of 16 AGPRs; the phase schedule and DMA order of
+//    gemm4t8_kernel (one DMA piece per MFMA in the second K-step, one barrier after each K-step);
+//  * epilogue: bf16 store (4 columns per lane and accumulator quarter) and, with `stat`, the BN
+//    partial sums (sum, sum of squares of the stored values) per 128 rows: [2 ceil(M/256)][2][N].
+// AOP: 0 dense A, 1 conv gather. B_E5M2: the A operand in OCP e5m2 (data gradients).
+typedef __attribute__((ext_vector_type(8))) int ttd_i32x8_t;
+typedef __attribute__((ext_vector_type(16))) float ttd_f32x16_t;
+typedef __attribute__((address_space(3))) bf16x8_t lds_b8x8_t;  // a 16-B LDS read (32-bit LDS address)
+
+template <bool FIRST, bool E5M2>
+__device__ __forceinline__ void mfma8k(ttd_f32x16_t& c, const ttd_i32x8_t& a, const ttd_i32x8_t& b, int one) {
+  // src0 = the B fragment (filter, e4m3), src1 = the A fragment (blgp 1 when e5m2); the leading
+  // s_nop 1: `one` may be a VALU write right before the asm
+  if constexpr (FIRST && E5M2)
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] blgp:1"
+                 : "=a"(c) : "v"(b), "v"(a), "v"(one) : "memory");
+  else if constexpr (FIRST)
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0]"
+                 : "=a"(c) : "v"(b), "v"(a), "v"(one) : "memory");
+  else if constexpr (E5M2)
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] blgp:1"
+                 : "+a"(c) : "v"(b), "v"(a), "v"(one) : "memory");
+  else
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+                 : "+a"(c) : "v"(b), "v"(a), "v"(one) : "memory");
+}
+
+struct K8Args {
+  const uint8_t* A;
+  long long lda;  // AOP 0
+  const uint8_t* B;
+  long long ldb;
+  bf16_t* out;
+  long long ldo;
+  float* stat;  // nullptr: no statistics
+  const float* sa;
+  const float* sb;
+  int M, N, K, tiles_m, tiles_n, group;
+};
+
+template <int AOP, bool E5M2>
+__global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
+  constexpr int NA = 4, NB = 4, NF = 8, NMF = 16, PA = 8, NQ = 16, NR = 2 * NF, H0 = NMF, H1 = NMF / 2;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  const int M = P.M, N = P.N;
+  const int nblk = P.tiles_m * P.tiles_n;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  int tm_, tn_;
+  tile_of(t, P.tiles_m, P.tiles_n, P.group, tm_, tn_);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nk = P.K / 128;
+
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)smem));
+  // fragment read base: row (l & 31) of the wave's block 0, chunk ((l >> 5) << 1) ^ ((l >> 1) & 7);
+  // K-step s, read q: chunk ^ (4 s | q) (immediate XOR), block j: + 32 j rows
+  const uint32_t L = static_cast<uint32_t>(((lane >> 5) << 1) ^ ((lane >> 1) & 7));
+  const uint32_t rA = sb + static_cast<uint32_t>((wm * 128 + (lane & 31)) * 128) + (L << 4);
+  const uint32_t rB = sb + OPB + static_cast<uint32_t>((wn * 128 + (lane & 31)) * 128) + (L << 4);
+  const uint32_t ldsw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sb + wave * 1024)));
+
+  // loaders: piece i of thread tid = image row 32 i + tid / 8, physical chunk tid % 8 = logical
+  // chunk (tid & 7) ^ ((tid >> 4) & 7); rows past the end clamped (A dense, B) or zero (A conv)
+  const int chunk = (tid & 7) ^ ((tid >> 4) & 7);
+  ttd_i32x4_t srd_a, srd_b;
+  uint32_t voa[8], vob[8], vmask[8];
+  srd_b = make_srd(P.B, static_cast<uint32_t>(static_cast<long long>(N) * P.ldb));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = min(n0 + i * 32 + (tid >> 3), N - 1);
+    vob[i] = static_cast<uint32_t>(static_cast<long long>(r) * P.ldb + chunk * 16);
+  }
+  long long shift = 0;
+  if constexpr (AOP == 0) {
+    srd_a = make_srd(P.A, static_cast<uint32_t>(static_cast<long long>(M) * P.lda));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = min(m0 + i * 32 + (tid >> 3), M - 1);
+      voa[i] = static_cast<uint32_t>(static_cast<long long>(r) * P.lda + chunk * 16);
+      vmask[i] = 0;
+    }
+  } else {
+    shift = (static_cast<long long>(ca.ph) * ca.W + ca.pw) * ca.C;
+    srd_a = make_srd(P.A - shift, static_cast<uint32_t>(ca.x_bytes + shift));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + i * 32 + (tid >> 3);
+      const int mm = m < M ? m : 0;
+      const int n = mm / ca.PQ, rem = mm - n * ca.PQ;
+      const int p = rem / ca.Q, q = rem - p * ca.Q;
+      const int h0 = p * ca.sh - ca.ph, w0 = q * ca.sw - ca.pw;
+      voa[i] = static_cast<uint32_t>(((static_cast<long long>(n) * ca.H + h0) * ca.W + w0) * ca.C + shift + chunk * 16);
+      uint32_t mk = 0;
+      for (int r = 0; r < ca.R; ++r)
+        for (int s2 = 0; s2 < ca.S; ++s2)
+          if (m < M && static_cast<unsigned>(h0 + r) < static_cast<unsigned>(ca.H) &&
+              static_cast<unsigned>(w0 + s2) < static_cast<unsigned>(ca.W))
+            mk |= 1u << (r * ca.S + s2);
+      vmask[i] = mk;
+    }
+  }
+  // conv A cursor (the K-tile whose A pieces go out next): tap, channel offset, scalar bytes
+  int c_c0 = 0, c_r = 0, c_s = 0, c_tap = 0, c_soff = 0;
+  auto c_advance = [&]() {
+    c_c0 += 128;
+    if (c_c0 == ca.C) {
+      c_c0 = 0;
+      if (++c_s == ca.S) {
+        c_s = 0;
+        ++c_r;
+      }
+    }
+    c_tap = c_r * ca.S + c_s;
+    c_soff = (c_r * ca.W + c_s) * ca.C + c_c0;
+  };
+  int one = 127;
+  asm volatile("" : "+v"(one));
+
+  ttd_f32x16_t acc[NA][NB];
+  bf16x8_t fr[2][NF][2];  // [set][fragment: 0..NA-1 A, NA.. B][read q]
+
+  auto rd1 = [&](auto R, auto S, int st, auto SET) {
+    constexpr int r = decltype(R)::value, s = decltype(S)::value, set = decltype(SET)::value;
+    constexpr int fi = r / 2, q = r % 2;
+    constexpr bool isa = fi == 0 || fi > NB;
+    constexpr int blk = fi == 0 ? 0 : (fi <= NB ? fi - 1 : fi - NB);
+    const uint32_t base = (isa ? rA : rB) + st * STAGE;
+    const uint32_t addr = (base ^ static_cast<uint32_t>((4 * s | q) << 4)) + blk * 4096;
+    fr[set][isa ? blk : NA + blk][q] = *reinterpret_cast<const lds_b8x8_t*>(static_cast<uintptr_t>(addr));
+  };
+  auto frag = [&](int set, int slot) {
+    return __builtin_bit_cast(ttd_i32x8_t, __builtin_shufflevector(fr[set][slot][0], fr[set][slot][1], 0, 1, 2, 3, 4,
+                                                                     5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15));
+  };
+  auto m0_of = [&](int qq, int st) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<int>(ldsw + st * STAGE + (qq < PA ? qq * 4096 : OPB + (qq - PA) * 4096))));
+  };
+  auto dma1 = [&](auto Q, int st, int kt) {
+    constexpr int qq = decltype(Q)::value;
+    const uint32_t next = qq < NQ - 1 ? m0_of(qq + 1, st) : m0_of(0, st ^ 1);
+    if constexpr (qq < PA) {
+      if constexpr (AOP == 0) dma_chain(voa[qq], srd_a, kt * 128, next);
+      else dma_chain((vmask[qq] >> c_tap) & 1u ? voa[qq] : kOob, srd_a, c_soff, next);
+      if constexpr (AOP == 1 && qq == PA - 1) c_advance();
+    } else {
+      dma_chain(vob[qq - PA], srd_b, kt * 128, next);
+    }
+  };
+
+  auto ktile = [&](int kt, auto first, auto has2c) {
+    constexpr bool FIRST = decltype(first)::value;
+    constexpr bool has2 = decltype(has2c)::value;
+    const int st = kt & 1;
+    static_for<H0>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      static_for<NR>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (j * H0 / NR == i) rd1(J, std::integral_constant<int, 1>{}, st, std::integral_constant<int, 1>{});
+      });
+      mfma8k<FIRST, E5M2>(acc[i / NB][i % NB], frag(0, i / NB), frag(0, NA + i % NB), one);
+    });
+    wait_lgkm0();
+    asm volatile("s_barrier" ::: "memory");
+    static_for<H1>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (has2) dma1(std::integral_constant<int, i>{}, st, kt + 2);
+      mfma8k<false, E5M2>(acc[i / NB][i % NB], frag(1, i / NB), frag(1, NA + i % NB), one);
+    });
+    if constexpr (has2) wait_vm<PA>();
+    else wait_vm<0>();
+    asm volatile("s_barrier" ::: "memory");
+    static_for<H1>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (has2) dma1(std::integral_constant<int, PA + i>{}, st, kt + 2);
+      static_for<NR>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if constexpr (j * H1 / NR == i) rd1(J, std::integral_constant<int, 0>{}, st ^ 1, std::integral_constant<int, 0>{});
+      });
+      mfma8k<false, E5M2>(acc[NA / 2 + i / NB][i % NB], frag(1, NA / 2 + i / NB), frag(1, NA + i % NB), one);
+    });
+  };
+
+  m0_init(m0_of(0, 0));
+  static_for<NQ>([&](auto Q) { dma1(Q, 0, 0); });
+  static_for<NQ>([&](auto Q) { dma1(Q, 1, 1); });
+  wait_lgkm0();
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NQ) : "memory");
+  static_for<NR>([&](auto R) { rd1(R, std::integral_constant<int, 0>{}, 0, std::integral_constant<int, 0>{}); });
+  if (nk >= 3) {
+    ktile(0, std::true_type{}, std::true_type{});
+    for (int kt = 1; kt < nk - 2; ++kt) ktile(kt, std::false_type{}, std::true_type{});
+    ktile(nk - 2, std::false_type{}, std::false_type{});
+    ktile(nk - 1, std::false_type{}, std::false_type{});
+  } else {
+    ktile(0, std::true_type{}, std::false_type{});
+    if (nk == 2) ktile(1, std::false_type{}, std::false_type{});
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) asm volatile("" : "+a"(acc[a][b]));
+
+  // epilogue: lane l, accumulator (a, b), quarter v4: row m0 + 128 wm + 32 a + (l & 31), columns
+  // n0 + 128 wn + 32 b + 8 v4 + 4 (l >> 5) .. +3
+  const float scale = P.sa[0] * P.sb[0];
+  const bool stats = P.stat != nullptr;
+  const int hi = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    float ssum[4][4], ssq[4][4];
+#pragma unroll
+    for (int v4 = 0; v4 < 4; ++v4)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ssum[v4][j] = ssq[v4][j] = 0.f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      asm volatile("" : "+a"(acc[a][b]));
+      const int m = m0 + wm * 128 + a * 32 + (lane & 31);
+      const bool mok = m < M;
+#pragma unroll
+      for (int v4 = 0; v4 < 4; ++v4) {
+        const int n = n0 + wn * 128 + b * 32 + 8 * v4 + 4 * hi;
+        const float x0 = acc[a][b][4 * v4] * scale, x1 = acc[a][b][4 * v4 + 1] * scale;
+        const float x2 = acc[a][b][4 * v4 + 2] * scale, x3 = acc[a][b][4 * v4 + 3] * scale;
+        const uint2 w = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
+        if (mok && n < N) *reinterpret_cast<uint2*>(P.out + static_cast<long long>(m) * P.ldo + n) = w;
+        if (stats && mok) {
+          const float r[4] = {bf2f(static_cast<bf16_t>(w.x & 0xffff)), bf2f(static_cast<bf16_t>(w.x >> 16)),
+                              bf2f(static_cast<bf16_t>(w.y & 0xffff)), bf2f(static_cast<bf16_t>(w.y >> 16))};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ssum[v4][j] += r[j];
+            ssq[v4][j] += r[j] * r[j];
+          }
+        }
+      }
+    }
+    if (stats) {
+      // the 32 lanes of a half-wave hold the same columns (rows l & 31): sum them; lane 31 / 63
+      // writes this wave's 128-row partial row (m0 / 128 + wm)
+      float* const st = P.stat + static_cast<long long>((m0 / 128) + wm) * 2 * N;
+#pragma unroll
+      for (int v4 = 0; v4 < 4; ++v4)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // DPP row sums (lane 15 of each 16-lane row), then row_bcast:15 adds row 0's total into
+          // row 1 (and row 2's into row 3): lanes 31 / 63 hold the half-wave totals
+          float s = row_sum16(ssum[v4][j]), q2 = row_sum16(ssq[v4][j]);
+          s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0x142, 0xa, 0xf, false));
+          q2 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, q2), 0x142, 0xa, 0xf, false));
+          const int n = n0 + wn * 128 + b * 32 + 8 * v4 + 4 * hi + j;
+          if ((lane & 31) == 31 && n < N) {
+            st[n] = s;
+            st[N + n] = q2;
+          }
+        }
+    }
+  }
+}
+
 }  // namespace g4
 }  // namespace
 }  // namespace ttdk
@@ -1056,4 +1333,48 @@ TTDK_EXPORT int ttdk_gemm4w_bf16(const bf16_t* A, long long lda, const bf16_t* B
 #undef TTDK_G4
 #undef TTDK_G4_ONE
   return hipErrorInvalidValue;
+}
+
+// fp8 forward convolution on the 4-wave kernel (g4::gemm4k8_kernel): y[M = N P Q][K] (bf16) =
+// sa * sw * conv(x8 [N][H][W][C] e4m3, w8 [K][R][S][C] e4m3), unit-stride 1x1 convs reading x8 as
+// dense [M][C] rows, the others through the implicit-GEMM gather; stat (optional): BN partial sums
+// of the stored output per 128 rows, [2 ceil(M / 256)][2][K]. Needs C % 128 == 0, K % 8 == 0,
+// no dilation, operands under 2 GiB. hipErrorInvalidValue: not taken (the caller keeps the 8-wave
+// conv_fwd_fp8).
+TTDK_EXPORT int ttdk_conv_fwd4k8(const uint8_t* x8, const uint8_t* w8, const TtdkConv* g, bf16_t* out, float* stat,
+                                 const float* sa, const float* sw, hipStream_t st) {
+  using namespace ttdk;
+  const int M = g->N * g->P * g->Q, N = g->K, K = g->R * g->S * g->C;
+  const long long xb = static_cast<long long>(g->N) * g->H * g->W * g->C;
+  const long long shift = (static_cast<long long>(g->ph) * g->W + g->pw) * g->C;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (g->C % 128 || N % 8 || N < 8 || M < 1 || g->dh != 1 || g->dw != 1 || g->R * g->S > 32 || !sa || !sw ||
+      !al16(x8) || !al16(w8) || !al16(out) || xb + shift >= (1LL << 31) ||
+      (static_cast<long long>(N) + 256) * K >= (1LL << 32))
+    return hipErrorInvalidValue;
+  g4::K8Args P{};
+  P.A = x8;
+  P.lda = g->C;
+  P.B = w8;
+  P.ldb = K;
+  P.out = out;
+  P.ldo = N;
+  P.stat = stat;
+  P.sa = sa;
+  P.sb = sw;
+  P.M = M;
+  P.N = N;
+  P.K = K;
+  P.tiles_m = ceil_div(M, g4::BM);
+  P.tiles_n = ceil_div(N, g4::BN);
+  P.group = g4_group();
+  const dim3 grid(P.tiles_m * P.tiles_n);
+  if (is_pointwise(g)) {
+    if (static_cast<long long>(M) * g->C >= (1LL << 32)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((g4::gemm4k8_kernel<0, false>), grid, dim3(g4::T), 0, st, P, g4::ConvA{});
+    return hipGetLastError();
+  }
+  g4::ConvA ca{g->H, g->W, g->C, g->P * g->Q, g->Q, g->sh, g->sw, g->ph, g->pw, g->R, g->S, 0, xb};
+  hipLaunchKernelGGL((g4::gemm4k8_kernel<1, false>), grid, dim3(g4::T), 0, st, P, ca);
+  return hipGetLastError();
 }

@@ -449,12 +449,17 @@ class ResNet:
             else:
                 y, partial, T = G.pw_conv(x, w2, stat=True)
         elif use8:
-            partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
             xq, xslot = x8
             self._x8[c.name] = x8  # the fp8 weight gradient reuses the quantised input
             ws = self._w8_slots[self._w8_slot[c.name]]
-            y = G.conv_fwd_fp8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
-                               ascale=(xslot[3:4], ws[3:4]))
+            if G.conv_fwd4k8_ok(tuple(xq.shape), tuple(self._w8[c.name].shape), (c.stride, c.stride), (c.pad, c.pad)):
+                # the 4-wave fp8 kernel (BN statistics per 128 rows)
+                y, partial, T = G.conv_fwd4k8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad),
+                                              ascale=(xslot[3:4], ws[3:4]))
+            else:
+                partial = torch.empty((T, 2, c.cout), dtype=torch.float32, device=x.device)
+                y = G.conv_fwd_fp8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad), stat=partial,
+                                   ascale=(xslot[3:4], ws[3:4]))
         elif bm == 256 and G.conv_fwd4w_pays(tuple(x.shape), tuple(P.var[c.name + "_conv/kernel"].shape),
                                              (c.stride, c.stride), (c.pad, c.pad)):
             # the 4-wave GEMM (SCHED 3 loop, im2col gather by the operand DMA, BN statistics from

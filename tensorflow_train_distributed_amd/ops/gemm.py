@@ -1177,6 +1177,41 @@ def conv_fwd_fp8(x8, w8, stride=(1, 1), padding=(0, 0), *, alpha=1.0, out=None, 
     return out
 
 
+# fp8 forward convs on the 4-wave kernel's fp8 K-major form (gemm4w.hip gemm4k8_kernel: 32x32x64
+# block-scaled MFMA, implicit-GEMM DMA gather, BN statistics per 128 rows); TTD_CONV4K8=0: the
+# 8-wave conv_fwd_fp8 kernel
+_CONV4K8 = _os.environ.get("TTD_CONV4K8", "1") != "0"
+
+
+def conv_fwd4k8_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
+    """Whether conv_fwd4k8 takes this conv (mirror of ttdk_conv_fwd4k8's admission)."""
+    if not _CONV4K8:
+        return False
+    g = conv_geom(tuple(x_shape), tuple(w_shape), stride, padding)
+    M, N, K = g.N * g.P * g.Q, g.K, g.R * g.S * g.C
+    xb = g.N * g.H * g.W * g.C + (g.ph * g.W + g.pw) * g.C
+    return (g.C % 128 == 0 and N % 8 == 0 and N >= 8 and M >= 1 and g.R * g.S <= 32 and xb < (1 << 31)
+            and (N + 256) * K < (1 << 32) and M * g.C < (1 << 32))
+
+
+def conv_fwd4k8(x8, w8, stride=(1, 1), padding=(0, 0), *, ascale, stat=True, out=None):
+    """fp8 forward conv on the 4-wave kernel: x8 [N,H,W,C] e4m3 (uint8), w8 [K,R,S,C] e4m3, ascale
+    = (inverse scale of x8, of w8) as device fp32 scalars; bf16 output. stat=True: also the BN
+    partial sums of the stored output per 128 rows -> (out, partial [T][2][K], T = 2 ceil(M/256)).
+    Raises when the kernel does not take the conv."""
+    g = conv_geom(x8.shape, w8.shape, stride, padding)
+    M = g.N * g.P * g.Q
+    if out is None:
+        out = torch.empty((g.N, g.P, g.Q, g.K), dtype=torch.bfloat16, device=x8.device)
+    T = 2 * (-(-M // 256))
+    partial = torch.empty((T, 2, g.K), dtype=torch.float32, device=x8.device) if stat else None
+    _log("fwd4k8_%dx%d_s%d" % (g.R, g.S, g.sh), M, g.K, g.R * g.S * g.C)
+    _lib.call("ttdk_conv_fwd4k8", x8.data_ptr(), w8.data_ptr(), ctypes.byref(g), out.data_ptr(),
+              partial.data_ptr() if partial is not None else None, ascale[0].data_ptr(), ascale[1].data_ptr(),
+              _lib.stream())
+    return (out, partial, T) if stat else out
+
+
 def conv_dgrad_fp8_ok(x_shape, wt_shape, stride=(1, 1), padding=(0, 0)):
     """Whether conv_dgrad_fp8 takes this data gradient: unit stride, the output gradient's
     channels (wt_shape[-1]) a multiple of 128, wt_shape = [C, R, S, K]."""

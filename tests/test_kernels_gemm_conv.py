@@ -757,6 +757,39 @@ def test_conv1x1_fp8_units_vs_fp32_oracle(cfg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(4, 14, 14, 256, 256, 3, 1, 1), (8, 7, 7, 512, 512, 3, 1, 1), (4, 28, 28, 128, 128, 3, 2, 1),
+                                 (16, 14, 14, 1024, 256, 1, 1, 0), (8, 14, 14, 512, 1024, 1, 2, 0),
+                                 (3, 9, 11, 128, 200, 3, 1, 1)])
+def test_conv_fwd4k8_vs_fp32_oracle(cfg):
+    """fp8 forward conv on the 4-wave kernel (gemm4w.hip gemm4k8_kernel: 32x32x64 block-scaled MFMA,
+    K-major fragments, implicit-GEMM DMA gather / dense 1x1 rows) vs F.conv2d on the exactly
+    decoded operands (tight), with the BN partial sums per 128 rows vs the stored output, and vs
+    the 8-wave fp8 kernel; partial row / column tiles in the last case."""
+    from tensorflow_train_distributed_amd.ops import gemm as G
+    from tensorflow_train_distributed_amd.ops import kernels as K
+    N, H, W, C, Kc, R, s, p = cfg
+    torch.manual_seed(31 + C)
+    x = torch.randn(N, H, W, C, device="cuda").relu().bfloat16()
+    w = (torch.randn(Kc, R, R, C, device="cuda") / (R * R * C) ** 0.5).bfloat16()
+    s_x = torch.tensor([448.0 / float(x.float().abs().max())], device="cuda")
+    s_w = torch.tensor([448.0 / float(w.float().abs().max())], device="cuda")
+    x8, w8 = K.quant_fp8(x, s_x), K.quant_fp8(w, s_w)
+    one = torch.ones(1, device="cuda")
+    xq = K.dequant_fp8(x8, one).float() / s_x
+    wq = K.dequant_fp8(w8, one).float() / s_w
+    assert G.conv_fwd4k8_ok(x8.shape, w8.shape, (s, s), (p, p))
+    y, part, T = G.conv_fwd4k8(x8, w8, (s, s), (p, p), ascale=(1.0 / s_x, 1.0 / s_w))
+    ref = F.conv2d(_nchw(xq), wq.permute(0, 3, 1, 2), stride=s, padding=p)
+    assert _rel(y, _nhwc(ref)) < 1e-2
+    yf = y.float().reshape(-1, Kc)
+    sums = part[:T].sum(0)
+    torch.testing.assert_close(sums[0], yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(sums[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+    y8 = G.conv_fwd_fp8(x8, w8, (s, s), (p, p), ascale=(1.0 / s_x, 1.0 / s_w))
+    assert _rel(y, y8.float()) < 1e-2
+
+
+@pytest.mark.gpu
 def test_bn_backward_apply_e5m2_copy_and_amax():
     """The BN backward-apply pass's OCP e5m2 copy of dz (delayed scale from the slot) dequantises
     to dz within e5m2 rounding, and the slot's amax lanes receive max |dz|."""
