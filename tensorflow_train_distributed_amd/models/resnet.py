@@ -452,8 +452,8 @@ class ResNet:
             xq, xslot = x8
             self._x8[c.name] = x8  # the fp8 weight gradient reuses the quantised input
             ws = self._w8_slots[self._w8_slot[c.name]]
-            if G.conv_fwd4k8_ok(tuple(xq.shape), tuple(self._w8[c.name].shape), (c.stride, c.stride), (c.pad, c.pad)):
-                # the 4-wave fp8 kernel (BN statistics per 128 rows)
+            if G.conv_fwd4k8_pays(tuple(xq.shape), tuple(self._w8[c.name].shape), (c.stride, c.stride), (c.pad, c.pad)):
+                # the 4-wave fp8 kernel on the long-reduction shapes (BN statistics per 128 rows)
                 y, partial, T = G.conv_fwd4k8(xq, self._w8[c.name], (c.stride, c.stride), (c.pad, c.pad),
                                               ascale=(xslot[3:4], ws[3:4]))
             else:

@@ -1194,6 +1194,15 @@ def conv_fwd4k8_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
             and (N + 256) * K < (1 << 32) and M * g.C < (1 << 32))
 
 
+def conv_fwd4k8_pays(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
+    """The engine's policy: the 4-wave fp8 forward where it measured faster than the 8-wave one
+    (tools/fp8_conv_ab.py, profiles/r6_fp8_conv_fwd_ab_b1024.txt): reductions of >= 1024 with >= 256
+    output channels (stage-3/4 3x3 1.54x / 1.95x, 1024 -> 256 1x1 1.14x); the short-K and
+    128-channel shapes are 0.75-0.92x."""
+    K = w_shape[1] * w_shape[2] * w_shape[3]
+    return conv_fwd4k8_ok(x_shape, w_shape, stride, padding) and K >= 1024 and w_shape[0] >= 256
+
+
 def conv_fwd4k8(x8, w8, stride=(1, 1), padding=(0, 0), *, ascale, stat=True, out=None):
     """fp8 forward conv on the 4-wave kernel: x8 [N,H,W,C] e4m3 (uint8), w8 [K,R,S,C] e4m3, ascale
     = (inverse scale of x8, of w8) as device fp32 scalars; bf16 output. stat=True: also the BN

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""bf16 vs fp8 (e4m3) forward convs at ResNet-50 b1024 shapes, with the BN-statistics
+"""bf16 vs fp8 (e4m3) forward convs (8-wave conv_fwd_fp8 and the 4-wave conv_fwd4k8) at ResNet-50 b1024 shapes, with the BN-statistics
 epilogue as the engine runs them. usage: python tools/fp8_conv_ab.py"""
 import sys
 
@@ -43,9 +43,11 @@ for H, C, Ko, k, s in shapes:
         x8 = K.quant_fp8(x, torch.ones(1, device="cuda"))
         w8 = K.quant_fp8(w, torch.ones(1, device="cuda"))
         t8 = timeit(lambda: G.conv_fwd_fp8(x8, w8, (s, s), (pad, pad), stat=st))
+        one = torch.ones(1, device="cuda")
+        t4 = timeit(lambda: G.conv_fwd4k8(x8, w8, (s, s), (pad, pad), ascale=(one, one)))
     else:
-        t8 = float("nan")
+        t8 = t4 = float("nan")
     fl = 2.0 * M * Ko * k * k * C
-    print("%2dx%-2d %4d->%-4d k%d: bf16 %7.1f us (%4.0f TF/s)  fp8 %7.1f us (%4.0f TF/s)" %
-          (H, H, C, Ko, k, tb, fl / tb / 1e6, t8, fl / t8 / 1e6), flush=True)
+    print("%2dx%-2d %4d->%-4d k%d: bf16 %7.1f us (%4.0f TF/s)  fp8 8-wave %7.1f us (%4.0f TF/s)  fp8 4-wave %7.1f us "
+          "(%4.0f TF/s)" % (H, H, C, Ko, k, tb, fl / tb / 1e6, t8, fl / t8 / 1e6, t4, fl / t4 / 1e6), flush=True)
     del x, w
