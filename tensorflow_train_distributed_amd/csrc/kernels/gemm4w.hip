@@ -908,12 +908,16 @@ struct K8Args {
   bf16_t* out;
   long long ldo;
   float* stat;  // nullptr: no statistics
+  const bf16_t* by;       // FEED: the feeding unit's conv output y [M][ldo]
+  const uint8_t* bmask;   // FEED: its ReLU bits (bit n of byte (m ldo + n) / 8)
   const float* sa;
   const float* sb;
   int M, N, K, tiles_m, tiles_n, group;
 };
 
-template <int AOP, bool E5M2>
+// FEED (data gradients): g = dx * ReLU bits of the feeding conv+BN unit is stored, the statistics
+// are (sum g, sum g y) — the bf16 feeding-BN epilogue of this file
+template <int AOP, bool E5M2, bool FEED = false>
 __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
   constexpr int NA = 4, NB = 4, NF = 8, NMF = 16, PA = 8, NQ = 16, NR = 2 * NF, H0 = NMF, H1 = NMF / 2;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -977,7 +981,10 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
     }
   }
   // conv A cursor (the K-tile whose A pieces go out next): tap, channel offset, scalar bytes
-  int c_c0 = 0, c_r = 0, c_s = 0, c_tap = 0, c_soff = 0;
+  // (flip, data gradients: the taps in the filter's reversed order, starting at the last)
+  int c_c0 = 0, c_r = 0, c_s = 0;
+  int c_tap = ca.flip ? ca.R * ca.S - 1 : 0;
+  int c_soff = ca.flip ? ((ca.R - 1) * ca.W + ca.S - 1) * ca.C : 0;
   auto c_advance = [&]() {
     c_c0 += 128;
     if (c_c0 == ca.C) {
@@ -987,8 +994,9 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
         ++c_r;
       }
     }
-    c_tap = c_r * ca.S + c_s;
-    c_soff = (c_r * ca.W + c_s) * ca.C + c_c0;
+    const int ra = ca.flip ? ca.R - 1 - c_r : c_r, sa2 = ca.flip ? ca.S - 1 - c_s : c_s;
+    c_tap = ra * ca.S + sa2;
+    c_soff = (ra * ca.W + sa2) * ca.C + c_c0;
   };
   int one = 127;
   asm volatile("" : "+v"(one));
@@ -1099,17 +1107,30 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
 #pragma unroll
       for (int v4 = 0; v4 < 4; ++v4) {
         const int n = n0 + wn * 128 + b * 32 + 8 * v4 + 4 * hi;
-        const float x0 = acc[a][b][4 * v4] * scale, x1 = acc[a][b][4 * v4 + 1] * scale;
-        const float x2 = acc[a][b][4 * v4 + 2] * scale, x3 = acc[a][b][4 * v4 + 3] * scale;
-        const uint2 w = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
-        if (mok && n < N) *reinterpret_cast<uint2*>(P.out + static_cast<long long>(m) * P.ldo + n) = w;
-        if (stats && mok) {
+        float x[4] = {acc[a][b][4 * v4] * scale, acc[a][b][4 * v4 + 1] * scale, acc[a][b][4 * v4 + 2] * scale,
+                      acc[a][b][4 * v4 + 3] * scale};
+        const bool ok = mok && n < N;
+        const long long o = static_cast<long long>(m) * P.ldo + n;
+        float yv[4];
+        if constexpr (FEED) {
+          const uint32_t bits = ok ? (static_cast<uint32_t>(P.bmask[o >> 3]) >> (n & 7)) : 0u;
+          const uint2 yw = ok ? *reinterpret_cast<const uint2*>(P.by + o) : make_uint2(0, 0);
+          yv[0] = bf2f(static_cast<bf16_t>(yw.x & 0xffff));
+          yv[1] = bf2f(static_cast<bf16_t>(yw.x >> 16));
+          yv[2] = bf2f(static_cast<bf16_t>(yw.y & 0xffff));
+          yv[3] = bf2f(static_cast<bf16_t>(yw.y >> 16));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[j] = (bits >> j) & 1u ? x[j] : 0.f;
+        }
+        const uint2 w = make_uint2(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]));
+        if (ok) *reinterpret_cast<uint2*>(P.out + o) = w;
+        if (stats && ok) {
           const float r[4] = {bf2f(static_cast<bf16_t>(w.x & 0xffff)), bf2f(static_cast<bf16_t>(w.x >> 16)),
                               bf2f(static_cast<bf16_t>(w.y & 0xffff)), bf2f(static_cast<bf16_t>(w.y >> 16))};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             ssum[v4][j] += r[j];
-            ssq[v4][j] += r[j] * r[j];
+            ssq[v4][j] += r[j] * (FEED ? yv[j] : r[j]);
           }
         }
       }
@@ -1376,5 +1397,57 @@ TTDK_EXPORT int ttdk_conv_fwd4k8(const uint8_t* x8, const uint8_t* w8, const Ttd
   }
   g4::ConvA ca{g->H, g->W, g->C, g->P * g->Q, g->Q, g->sh, g->sw, g->ph, g->pw, g->R, g->S, 0, xb};
   hipLaunchKernelGGL((g4::gemm4k8_kernel<1, false>), grid, dim3(g4::T), 0, st, P, ca);
+  return hipGetLastError();
+}
+
+// fp8 data gradient of a unit-stride conv on the 4-wave kernel (g4::gemm4k8_kernel, A = dy8 in OCP
+// e5m2 gathered as a forward conv with padding R - 1 - ph and the taps reversed, B = the [C][R][S][K]
+// e4m3 filter; dense dy8 rows for 1x1 convs): dx (bf16) = sa * sw * ..., with by / bmask / stat the
+// feeding-BN epilogue (g = dx * ReLU bits stored, (sum g, sum g y) per 128 rows: [2 ceil(M/256)][2][C]),
+// else a plain store. Needs K % 128 == 0 (the gradient's channels), C % 8 == 0, no accumulate.
+// hipErrorInvalidValue: not taken (the caller keeps conv_dgrad_fp8's 8-wave kernel).
+TTDK_EXPORT int ttdk_conv_dgrad4k8(const uint8_t* dy8, const uint8_t* wt8, const TtdkConv* g, bf16_t* out,
+                                   const bf16_t* by, const uint8_t* bmask, float* stat, const float* sa,
+                                   const float* sw, hipStream_t st) {
+  using namespace ttdk;
+  const int M = g->N * g->H * g->W, N = g->C, K = g->R * g->S * g->K;
+  const long long yb = static_cast<long long>(g->N) * g->P * g->Q * g->K;
+  const int pho = g->R - 1 - g->ph, pwo = g->S - 1 - g->pw;
+  const long long shift = (static_cast<long long>(pho) * g->Q + pwo) * g->K;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (g->sh != 1 || g->sw != 1 || g->dh != 1 || g->dw != 1 || g->K % 128 || N % 8 || N < 8 || g->R * g->S > 32 ||
+      pho < 0 || pwo < 0 || M < 1 || !sa || !sw || !al16(dy8) || !al16(wt8) || !al16(out) ||
+      yb + shift >= (1LL << 31) || (static_cast<long long>(N) + 256) * K >= (1LL << 32) ||
+      (by != nullptr) != (stat != nullptr) || (by != nullptr) != (bmask != nullptr) || (by && (reinterpret_cast<uintptr_t>(by) & 7)))
+    return hipErrorInvalidValue;
+  g4::K8Args P{};
+  P.B = wt8;
+  P.ldb = K;
+  P.out = out;
+  P.ldo = N;
+  P.stat = stat;
+  P.by = by;
+  P.bmask = bmask;
+  P.sa = sa;
+  P.sb = sw;
+  P.M = M;
+  P.N = N;
+  P.K = K;
+  P.tiles_m = ceil_div(M, g4::BM);
+  P.tiles_n = ceil_div(N, g4::BN);
+  P.group = g4_group();
+  const dim3 grid(P.tiles_m * P.tiles_n);
+  const bool feed = by != nullptr;
+  if (g->R == 1 && g->S == 1 && g->ph == 0 && g->pw == 0) {
+    P.A = dy8;
+    P.lda = g->K;
+    if (feed) hipLaunchKernelGGL((g4::gemm4k8_kernel<0, true, true>), grid, dim3(g4::T), 0, st, P, g4::ConvA{});
+    else hipLaunchKernelGGL((g4::gemm4k8_kernel<0, true, false>), grid, dim3(g4::T), 0, st, P, g4::ConvA{});
+    return hipGetLastError();
+  }
+  P.A = dy8;
+  const g4::ConvA ca{g->P, g->Q, g->K, g->H * g->W, g->W, 1, 1, pho, pwo, g->R, g->S, 1, yb};
+  if (feed) hipLaunchKernelGGL((g4::gemm4k8_kernel<1, true, true>), grid, dim3(g4::T), 0, st, P, ca);
+  else hipLaunchKernelGGL((g4::gemm4k8_kernel<1, true, false>), grid, dim3(g4::T), 0, st, P, ca);
   return hipGetLastError();
 }

@@ -1181,6 +1181,11 @@ def conv_fwd_fp8(x8, w8, stride=(1, 1), padding=(0, 0), *, alpha=1.0, out=None, 
 # block-scaled MFMA, implicit-GEMM DMA gather, BN statistics per 128 rows); TTD_CONV4K8=0: the
 # 8-wave conv_fwd_fp8 kernel
 _CONV4K8 = _os.environ.get("TTD_CONV4K8", "1") != "0"
+# ... and, opt-in (TTD_DGRAD4K8=1), the unit-stride fp8 data gradients with >= 1024-element
+# reductions and >= 256 input channels (gemm4w.hip gemm4k8_kernel with reversed taps and the
+# feeding-BN epilogue): in the ResNet-50 fp8 step 64.30 / 64.27 vs 63.76 / 63.89 ms with the
+# 8-wave kernel (its epilogue loads of y and the ReLU bits are not prefetched), so off by default
+_DGRAD4K8 = _os.environ.get("TTD_DGRAD4K8", "0") != "0"
 
 
 def conv_fwd4k8_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
@@ -1243,6 +1248,18 @@ def conv_dgrad_fp8(dy8, wt8, x_shape, stride=(1, 1), padding=(0, 0), *, ascale, 
     if out is None:
         out = torch.empty(tuple(x_shape), dtype=torch.bfloat16, device=dy8.device)
     M = g.N * g.H * g.W
+    if _DGRAD4K8 and not beta and R * S * K >= 1024 and C >= 256:
+        # the 4-wave fp8 kernel (gemm4w.hip gemm4k8_kernel, reversed-tap gather of dy8) on the
+        # long-reduction shapes; its statistics come per 128 rows
+        T = 2 * (-(-M // 256))
+        y, mask = bn_stat if bn_stat is not None else (None, None)
+        partial = torch.empty((T, 2, C), dtype=torch.float32, device=dy8.device) if bn_stat is not None else None
+        _log("dgrad4k8_%dx%d_s%d" % (R, S, stride[0]), M, C, R * S * K)
+        _lib.call("ttdk_conv_dgrad4k8", dy8.data_ptr(), wt8.data_ptr(), ctypes.byref(g), out.data_ptr(),
+                  y.data_ptr() if y is not None else None, mask.data_ptr() if mask is not None else None,
+                  partial.data_ptr() if partial is not None else None, ascale[0].data_ptr(), ascale[1].data_ptr(),
+                  _lib.stream())
+        return (out, partial, T) if bn_stat is not None else out
     _log("dgrad8_%dx%d_s%d" % (R, S, stride[0]), M, C, R * S * K)
     if bn_stat is not None:
         y, mask = bn_stat

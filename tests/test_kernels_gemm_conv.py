@@ -661,13 +661,17 @@ def test_weight_prep_matches_per_conv_transposes_and_phase_filters():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [(8, 14, 14, 256, 256), (4, 28, 28, 128, 128), (2, 7, 7, 512, 512)])
-def test_conv_dgrad_fp8_e5m2_vs_fp32_oracle(cfg):
+@pytest.mark.parametrize("four_wave", [True, False])
+@pytest.mark.parametrize("cfg", [(8, 14, 14, 256, 256), (4, 28, 28, 128, 128), (2, 7, 7, 512, 512), (3, 9, 11, 264, 128)])
+def test_conv_dgrad_fp8_e5m2_vs_fp32_oracle(monkeypatch, cfg, four_wave):
     """fp8 data gradient (e5m2 dy x e4m3 transposed filter, block-scaled MFMA) of a 3x3/s1 conv vs
     F.conv2d's fp32 input gradient on the DEQUANTISED operands (tight), vs the bf16 operands
     (fp8 rounding: loose), and with the feeding-BN statistics epilogue vs the bf16 dgrad's."""
     from tensorflow_train_distributed_amd.ops import gemm as G
     from tensorflow_train_distributed_amd.ops import kernels as K
+    # four_wave: the 4-wave fp8 kernel (reversed-tap gather, feeding-BN epilogue) where the engine
+    # takes it (>= 1024-element reduction, >= 256 channels; the 4th shape has partial tiles)
+    monkeypatch.setattr(G, "_DGRAD4K8", four_wave)
     N, H, W, C, Kc = cfg
     torch.manual_seed(11)
     w = (torch.randn(Kc, 3, 3, C, device="cuda") / (9 * C) ** 0.5).bfloat16()
