@@ -1099,6 +1099,24 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
     for (int v4 = 0; v4 < 4; ++v4)
 #pragma unroll
       for (int j = 0; j < 4; ++j) ssum[v4][j] = ssq[v4][j] = 0.f;
+    // FEED: this column block's y values and ReLU bytes for all 16 (a, v4) issued up front (16
+    // loads in flight per lane instead of one exposed latency per store)
+    uint2 fy[NA][4];
+    uint32_t fb[NA][4];
+    if constexpr (FEED) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const int m = m0 + wm * 128 + a * 32 + (lane & 31);
+#pragma unroll
+        for (int v4 = 0; v4 < 4; ++v4) {
+          const int n = n0 + wn * 128 + b * 32 + 8 * v4 + 4 * hi;
+          const long long o = static_cast<long long>(m) * P.ldo + n;
+          const bool ok = m < M && n < N;
+          fy[a][v4] = ok ? *reinterpret_cast<const uint2*>(P.by + o) : make_uint2(0, 0);
+          fb[a][v4] = ok ? static_cast<uint32_t>(P.bmask[o >> 3]) : 0u;
+        }
+      }
+    }
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       asm volatile("" : "+a"(acc[a][b]));
@@ -1113,8 +1131,8 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
         const long long o = static_cast<long long>(m) * P.ldo + n;
         float yv[4];
         if constexpr (FEED) {
-          const uint32_t bits = ok ? (static_cast<uint32_t>(P.bmask[o >> 3]) >> (n & 7)) : 0u;
-          const uint2 yw = ok ? *reinterpret_cast<const uint2*>(P.by + o) : make_uint2(0, 0);
+          const uint32_t bits = fb[a][v4] >> (n & 7);
+          const uint2 yw = fy[a][v4];
           yv[0] = bf2f(static_cast<bf16_t>(yw.x & 0xffff));
           yv[1] = bf2f(static_cast<bf16_t>(yw.x >> 16));
           yv[2] = bf2f(static_cast<bf16_t>(yw.y & 0xffff));

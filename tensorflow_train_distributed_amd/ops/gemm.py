@@ -1181,11 +1181,11 @@ def conv_fwd_fp8(x8, w8, stride=(1, 1), padding=(0, 0), *, alpha=1.0, out=None, 
 # block-scaled MFMA, implicit-GEMM DMA gather, BN statistics per 128 rows); TTD_CONV4K8=0: the
 # 8-wave conv_fwd_fp8 kernel
 _CONV4K8 = _os.environ.get("TTD_CONV4K8", "1") != "0"
-# ... and, opt-in (TTD_DGRAD4K8=1), the unit-stride fp8 data gradients with >= 1024-element
-# reductions and >= 256 input channels (gemm4w.hip gemm4k8_kernel with reversed taps and the
-# feeding-BN epilogue): in the ResNet-50 fp8 step 64.30 / 64.27 vs 63.76 / 63.89 ms with the
-# 8-wave kernel (its epilogue loads of y and the ReLU bits are not prefetched), so off by default
-_DGRAD4K8 = _os.environ.get("TTD_DGRAD4K8", "0") != "0"
+# ... and the unit-stride fp8 data gradients with >= 1024-element reductions and >= 256 input
+# channels (gemm4w.hip gemm4k8_kernel with reversed taps and the feeding-BN epilogue, its y / ReLU
+# loads issued per column block ahead of the stores): ResNet-50 fp8 step 62.43 / 62.59 vs 63.55 /
+# 63.34 ms with the 8-wave kernel (TTD_DGRAD4K8=0)
+_DGRAD4K8 = _os.environ.get("TTD_DGRAD4K8", "1") != "0"
 
 
 def conv_fwd4k8_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
