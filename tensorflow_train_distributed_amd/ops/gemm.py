@@ -1186,6 +1186,8 @@ _CONV4K8 = _os.environ.get("TTD_CONV4K8", "1") != "0"
 # loads issued per column block ahead of the stores): ResNet-50 fp8 step 62.43 / 62.59 vs 63.55 /
 # 63.34 ms with the 8-wave kernel (TTD_DGRAD4K8=0)
 _DGRAD4K8 = _os.environ.get("TTD_DGRAD4K8", "1") != "0"
+_DGRAD4K8_MINK = int(_os.environ.get("TTD_DGRAD4K8_MINK", "1024"))
+_DGRAD4K8_MINC = int(_os.environ.get("TTD_DGRAD4K8_MINC", "256"))
 
 
 def conv_fwd4k8_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
@@ -1248,7 +1250,7 @@ def conv_dgrad_fp8(dy8, wt8, x_shape, stride=(1, 1), padding=(0, 0), *, ascale, 
     if out is None:
         out = torch.empty(tuple(x_shape), dtype=torch.bfloat16, device=dy8.device)
     M = g.N * g.H * g.W
-    if _DGRAD4K8 and not beta and R * S * K >= 1024 and C >= 256:
+    if _DGRAD4K8 and not beta and R * S * K >= _DGRAD4K8_MINK and C >= _DGRAD4K8_MINC:
         # the 4-wave fp8 kernel (gemm4w.hip gemm4k8_kernel, reversed-tap gather of dy8) on the
         # long-reduction shapes; its statistics come per 128 rows
         T = 2 * (-(-M // 256))
