@@ -1186,7 +1186,7 @@ _CONV4K8 = _os.environ.get("TTD_CONV4K8", "1") != "0"
 # loads issued per column block ahead of the stores): ResNet-50 fp8 step 62.43 / 62.59 vs 63.55 /
 # 63.34 ms with the 8-wave kernel (TTD_DGRAD4K8=0)
 _DGRAD4K8 = _os.environ.get("TTD_DGRAD4K8", "1") != "0"
-_DGRAD4K8_MINK = int(_os.environ.get("TTD_DGRAD4K8_MINK", "1024"))
+_DGRAD4K8_MINK = int(_os.environ.get("TTD_DGRAD4K8_MINK", "512"))  # (1024: 63.60 / 63.28 vs 63.32 / 62.98 ms)
 _DGRAD4K8_MINC = int(_os.environ.get("TTD_DGRAD4K8_MINC", "256"))
 
 
