@@ -910,6 +910,7 @@ struct K8Args {
   float* stat;  // nullptr: no statistics
   const bf16_t* by;       // FEED: the feeding unit's conv output y [M][ldo]
   const uint8_t* bmask;   // FEED: its ReLU bits (bit n of byte (m ldo + n) / 8)
+  int beta;               // FEED: g = (dx + the stored gradient) * bits (a shortcut-gradient accumulate)
   const float* sa;
   const float* sb;
   int M, N, K, tiles_m, tiles_n, group;
@@ -1101,7 +1102,7 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
       for (int j = 0; j < 4; ++j) ssum[v4][j] = ssq[v4][j] = 0.f;
     // FEED: this column block's y values and ReLU bytes for all 16 (a, v4) issued up front (16
     // loads in flight per lane instead of one exposed latency per store)
-    uint2 fy[NA][4];
+    uint2 fy[NA][4], fo[NA][4];
     uint32_t fb[NA][4];
     if constexpr (FEED) {
 #pragma unroll
@@ -1114,6 +1115,7 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
           const bool ok = m < M && n < N;
           fy[a][v4] = ok ? *reinterpret_cast<const uint2*>(P.by + o) : make_uint2(0, 0);
           fb[a][v4] = ok ? static_cast<uint32_t>(P.bmask[o >> 3]) : 0u;
+          fo[a][v4] = ok && P.beta ? *reinterpret_cast<const uint2*>(P.out + o) : make_uint2(0, 0);
         }
       }
     }
@@ -1137,8 +1139,14 @@ __global__ __launch_bounds__(T, 1) void gemm4k8_kernel(K8Args P, ConvA ca) {
           yv[1] = bf2f(static_cast<bf16_t>(yw.x >> 16));
           yv[2] = bf2f(static_cast<bf16_t>(yw.y & 0xffff));
           yv[3] = bf2f(static_cast<bf16_t>(yw.y >> 16));
+          const uint2 ow = fo[a][v4];  // (the bf16 path's rounding: bf16(dx) + old, then the mask)
+          const float od[4] = {bf2f(static_cast<bf16_t>(ow.x & 0xffff)), bf2f(static_cast<bf16_t>(ow.x >> 16)),
+                               bf2f(static_cast<bf16_t>(ow.y & 0xffff)), bf2f(static_cast<bf16_t>(ow.y >> 16))};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) x[j] = (bits >> j) & 1u ? x[j] : 0.f;
+          for (int j = 0; j < 4; ++j) {
+            if (P.beta) x[j] = bf2f(f2bf(x[j])) + od[j];
+            x[j] = (bits >> j) & 1u ? x[j] : 0.f;
+          }
         }
         const uint2 w = make_uint2(pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]));
         if (ok) *reinterpret_cast<uint2*>(P.out + o) = w;
@@ -1422,10 +1430,11 @@ TTDK_EXPORT int ttdk_conv_fwd4k8(const uint8_t* x8, const uint8_t* w8, const Ttd
 // e5m2 gathered as a forward conv with padding R - 1 - ph and the taps reversed, B = the [C][R][S][K]
 // e4m3 filter; dense dy8 rows for 1x1 convs): dx (bf16) = sa * sw * ..., with by / bmask / stat the
 // feeding-BN epilogue (g = dx * ReLU bits stored, (sum g, sum g y) per 128 rows: [2 ceil(M/256)][2][C]),
-// else a plain store. Needs K % 128 == 0 (the gradient's channels), C % 8 == 0, no accumulate.
+// else a plain store; beta (with the feeding epilogue only): g = (dx + out) * bits. Needs K % 128 == 0
+// (the gradient's channels), C % 8 == 0.
 // hipErrorInvalidValue: not taken (the caller keeps conv_dgrad_fp8's 8-wave kernel).
 TTDK_EXPORT int ttdk_conv_dgrad4k8(const uint8_t* dy8, const uint8_t* wt8, const TtdkConv* g, bf16_t* out,
-                                   const bf16_t* by, const uint8_t* bmask, float* stat, const float* sa,
+                                   const bf16_t* by, const uint8_t* bmask, float* stat, int beta, const float* sa,
                                    const float* sw, hipStream_t st) {
   using namespace ttdk;
   const int M = g->N * g->H * g->W, N = g->C, K = g->R * g->S * g->K;
@@ -1436,7 +1445,8 @@ TTDK_EXPORT int ttdk_conv_dgrad4k8(const uint8_t* dy8, const uint8_t* wt8, const
   if (g->sh != 1 || g->sw != 1 || g->dh != 1 || g->dw != 1 || g->K % 128 || N % 8 || N < 8 || g->R * g->S > 32 ||
       pho < 0 || pwo < 0 || M < 1 || !sa || !sw || !al16(dy8) || !al16(wt8) || !al16(out) ||
       yb + shift >= (1LL << 31) || (static_cast<long long>(N) + 256) * K >= (1LL << 32) ||
-      (by != nullptr) != (stat != nullptr) || (by != nullptr) != (bmask != nullptr) || (by && (reinterpret_cast<uintptr_t>(by) & 7)))
+      (by != nullptr) != (stat != nullptr) || (by != nullptr) != (bmask != nullptr) || (by && (reinterpret_cast<uintptr_t>(by) & 7)) ||
+      (beta && !by))
     return hipErrorInvalidValue;
   g4::K8Args P{};
   P.B = wt8;
@@ -1446,6 +1456,7 @@ TTDK_EXPORT int ttdk_conv_dgrad4k8(const uint8_t* dy8, const uint8_t* wt8, const
   P.stat = stat;
   P.by = by;
   P.bmask = bmask;
+  P.beta = beta;
   P.sa = sa;
   P.sb = sw;
   P.M = M;

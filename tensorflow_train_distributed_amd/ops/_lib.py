@@ -72,7 +72,7 @@ _SIGS = {
     "ttdk_conv_wgrad_fp8": [P, P, G, P, P, I, I, P, P, P],
     "ttdk_conv_wgrad4t8": [P, P, G, P, P, I, I, P, P, P],
     "ttdk_conv_fwd4k8": [P, P, G, P, P, P, P, P],
-    "ttdk_conv_dgrad4k8": [P, P, G, P, P, P, P, P, P, P],
+    "ttdk_conv_dgrad4k8": [P, P, G, P, P, P, P, I, P, P, P],
     "ttdk_conv_wgrad4t8_ws": [G, I],
     "ttdk_splitk_reduce": [P, I, L, P, I, P],
     "ttdk_set_big_pers": [I],

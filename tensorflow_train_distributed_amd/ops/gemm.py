@@ -1188,6 +1188,9 @@ _CONV4K8 = _os.environ.get("TTD_CONV4K8", "1") != "0"
 _DGRAD4K8 = _os.environ.get("TTD_DGRAD4K8", "1") != "0"
 _DGRAD4K8_MINK = int(_os.environ.get("TTD_DGRAD4K8_MINK", "512"))  # (1024: 63.60 / 63.28 vs 63.32 / 62.98 ms)
 _DGRAD4K8_MINC = int(_os.environ.get("TTD_DGRAD4K8_MINC", "256"))
+# ... including the accumulating (shortcut-gradient) ones: TTD_DGRAD4K8_BETA=1 (the stage-4 c1 data
+# gradients then: 63.88 / 63.82 vs 63.57 / 63.42 ms with them on the 8-wave kernel; off)
+_DGRAD4K8_BETA = _os.environ.get("TTD_DGRAD4K8_BETA", "0") != "0"
 
 
 def conv_fwd4k8_ok(x_shape, w_shape, stride=(1, 1), padding=(0, 0)) -> bool:
@@ -1250,7 +1253,8 @@ def conv_dgrad_fp8(dy8, wt8, x_shape, stride=(1, 1), padding=(0, 0), *, ascale, 
     if out is None:
         out = torch.empty(tuple(x_shape), dtype=torch.bfloat16, device=dy8.device)
     M = g.N * g.H * g.W
-    if _DGRAD4K8 and not beta and R * S * K >= _DGRAD4K8_MINK and C >= _DGRAD4K8_MINC:
+    if (_DGRAD4K8 and (not beta or (_DGRAD4K8_BETA and bn_stat is not None and beta_s2 is None))
+            and R * S * K >= _DGRAD4K8_MINK and C >= _DGRAD4K8_MINC):
         # the 4-wave fp8 kernel (gemm4w.hip gemm4k8_kernel, reversed-tap gather of dy8) on the
         # long-reduction shapes; its statistics come per 128 rows
         T = 2 * (-(-M // 256))
@@ -1259,8 +1263,8 @@ def conv_dgrad_fp8(dy8, wt8, x_shape, stride=(1, 1), padding=(0, 0), *, ascale, 
         _log("dgrad4k8_%dx%d_s%d" % (R, S, stride[0]), M, C, R * S * K)
         _lib.call("ttdk_conv_dgrad4k8", dy8.data_ptr(), wt8.data_ptr(), ctypes.byref(g), out.data_ptr(),
                   y.data_ptr() if y is not None else None, mask.data_ptr() if mask is not None else None,
-                  partial.data_ptr() if partial is not None else None, ascale[0].data_ptr(), ascale[1].data_ptr(),
-                  _lib.stream())
+                  partial.data_ptr() if partial is not None else None, int(bool(beta)), ascale[0].data_ptr(),
+                  ascale[1].data_ptr(), _lib.stream())
         return (out, partial, T) if bn_stat is not None else out
     _log("dgrad8_%dx%d_s%d" % (R, S, stride[0]), M, C, R * S * K)
     if bn_stat is not None:

@@ -705,14 +705,22 @@ def test_conv_dgrad_fp8_e5m2_vs_fp32_oracle(monkeypatch, cfg, four_wave):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [(32, 14, 14, 1024, 256), (128, 7, 7, 512, 2048), (8, 28, 28, 512, 128)])
-def test_conv1x1_fp8_units_vs_fp32_oracle(cfg):
+@pytest.mark.parametrize("four_wave", [True, False])
+@pytest.mark.parametrize("cfg", [(32, 14, 14, 1024, 256), (128, 7, 7, 512, 2048), (8, 28, 28, 512, 128),
+                                 (32, 14, 14, 256, 512)])
+def test_conv1x1_fp8_units_vs_fp32_oracle(monkeypatch, cfg, four_wave):
     """The 1x1 fp8 unit of precision="fp8" (ResNet._fp8_conv with fp8_1x1): forward e4m3 x e4m3,
     data gradient e5m2 dz x e4m3 filter accumulating into the shortcut gradient (beta = 1) with the
     feeding BN's masked gradient + (sum g, sum g*y) epilogue, weight gradient e5m2 x e4m3 — each
     vs the fp32 op on the dequantised operands (tight) and vs the bf16 kernels (fp8 rounding)."""
     from tensorflow_train_distributed_amd.ops import gemm as G
     from tensorflow_train_distributed_amd.ops import kernels as K
+    # four_wave: the data gradient (with the accumulate) on the 4-wave fp8 kernel wherever it takes
+    # the shape (thresholds lowered for the test), else the 8-wave kernel
+    monkeypatch.setattr(G, "_DGRAD4K8", four_wave)
+    monkeypatch.setattr(G, "_DGRAD4K8_MINK", 128)
+    monkeypatch.setattr(G, "_DGRAD4K8_MINC", 8)
+    monkeypatch.setattr(G, "_DGRAD4K8_BETA", True)
     N, H, W, C, Kc = cfg
     torch.manual_seed(23 + C)
     M = N * H * W
